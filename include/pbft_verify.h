@@ -1,0 +1,113 @@
+/*
+ * pbft_verify.h — C ABI of the MI355X batch Ed25519 verifier that gates PBFT's
+ * prepare/commit quorums.  Shared library: pbft_amd/libpbft_verify.so (gfx950).
+ *
+ * Reference interfaces each entry point replaces (ameya-deshmukh/pbft):
+ *   pbft_verify_batch*     validate_prepare  src/behavior.rs:159-175 and
+ *                          validate_commit   src/behavior.rs:184-195, whose
+ *                          signature checks are TODOs (src/behavior.rs:127, :185);
+ *                          called per message from inject_node_event
+ *                          src/behavior.rs:340-412.  Here one call verifies a
+ *                          whole (view, seq) round window and returns a bitmap.
+ *   pbft_verify_set_keys   libp2p-core 0.31 identity::ed25519 PublicKey decode
+ *                          (keys created at src/main.rs:39-40; PeerId bytes are
+ *                          00 24 08 01 12 20 || A[32]).
+ *   pbft_digest_blake2b512 digest() src/message.rs:209-212 (request digest,
+ *                          checked by PrePrepare::validate_digest :139-145).
+ *   pbft_digest_sha256     the SHA-256 request digest named by BASELINE.json.
+ *   pbft_sign_batch        RFC 8032 signing of the replicas' own Prepare/Commit
+ *                          envelopes (the reference multicasts them unsigned,
+ *                          src/behavior.rs:116-122, :356-362).
+ *
+ * Semantics: ed25519-dalek 1.0.1 PublicKey::verify_strict (Cargo.lock:668-679):
+ * s < L, A and R decompress per curve25519-dalek 3.2.1, neither small order,
+ * k = SHA-512(R || A || M) mod L over the raw bytes, accept iff
+ * [s]B - [k]A == R as points.  An invalid signature is NOT an error: bit = 0.
+ *
+ * Conventions:
+ *  - Return 0 on success, a negative PBFT_E* code on failure; never aborts.
+ *  - Caller owns host buffers; the context owns its device buffers.
+ *  - Bitmaps: bit i is bit (i % 64) of word i / 64 (LSB first); bits >= N are 0.
+ *  - One context per host thread (contexts are not internally locked).
+ *  - Byte strings (R, S, A, keys) are the 32-byte little-endian encodings.
+ */
+#ifndef PBFT_VERIFY_H
+#define PBFT_VERIFY_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PBFT_OK 0
+#define PBFT_EINVAL (-1)   /* bad argument (null pointer, size out of range)   */
+#define PBFT_EHIP (-2)     /* HIP runtime error (message in pbft_last_error)   */
+#define PBFT_ENOKEYS (-3)  /* pbft_verify_set_keys has not been called        */
+#define PBFT_ENOMEM (-4)   /* device or pinned allocation failed              */
+#define PBFT_ENODEV (-5)   /* no gfx950 device at the requested ordinal       */
+#define PBFT_EBUSY (-6)    /* an async batch is in flight on this context     */
+
+typedef struct pbft_ctx pbft_ctx;
+
+/* Create a context on HIP device `device`; builds the base-point comb table. */
+int pbft_verify_ctx_create(int device, pbft_ctx **out);
+int pbft_verify_ctx_destroy(pbft_ctx *ctx);
+
+/* Install the replica key set A[n][32] (n <= 65535).  Decompresses every key,
+ * rejects small-order keys, and builds each key's -A comb table in HBM.
+ * key_ok (optional, n bytes): 1 = key usable, 0 = every signature under it
+ * rejects (bad encoding or small order).  Replaces any previous key set. */
+int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *key_ok);
+
+/* Blocking batch verify from host buffers (PCIe copies included).
+ * R[N][32], S[N][32], key_idx[N] (index into the key set), msg[N][msg_stride]
+ * of which the first msg_len bytes are the signed message.  bitmap_out has
+ * ceil(N/64) words. */
+int pbft_verify_batch(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
+                      const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                      uint64_t *bitmap_out);
+
+/* Non-blocking form: enqueue copies + kernel; the host buffers must stay valid
+ * until pbft_verify_wait returns.  One batch in flight per context. */
+int pbft_verify_batch_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
+                            const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                            uint64_t *bitmap_out);
+/* Returns 1 if the in-flight batch finished (bitmap written), 0 if still running. */
+int pbft_verify_poll(pbft_ctx *ctx);
+int pbft_verify_wait(pbft_ctx *ctx);
+
+/* Device-resident form: all pointers are device pointers on the context's
+ * device; stream is a hipStream_t (NULL = the context's stream).  Enqueues the
+ * kernel only.  d_msg must stay readable for N*msg_stride + 16 bytes. */
+int pbft_verify_batch_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d_S, const uint16_t *d_key_idx,
+                             const uint8_t *d_msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                             uint64_t *d_bitmap, void *stream);
+
+/* Request digests over N variable-length byte strings packed in `data`:
+ * item i is data[offsets[i] .. offsets[i] + lens[i]).  out: N x 64 (Blake2b-512)
+ * or N x 32 (SHA-256) bytes.  Blocking, host buffers. */
+int pbft_digest_blake2b512(pbft_ctx *ctx, const uint8_t *data, const uint64_t *offsets, const uint32_t *lens,
+                           uint64_t N, uint8_t *out);
+int pbft_digest_sha256(pbft_ctx *ctx, const uint8_t *data, const uint64_t *offsets, const uint32_t *lens,
+                       uint64_t N, uint8_t *out);
+
+/* RFC 8032 batch signing: seeds[n_seeds][32] secret seeds; signature i signs
+ * msg[i][0..msg_len) with seeds[seed_idx[i]].  Writes R[N][32], S[N][32];
+ * pub (optional) receives the n_seeds public keys.  Blocking, host buffers. */
+int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const uint16_t *seed_idx,
+                    const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint8_t *R,
+                    uint8_t *S, uint8_t *pub);
+
+/* Diagnostics */
+const char *pbft_last_error(void);
+const char *pbft_build_info(void); /* kernel windows, arch, version */
+/* Device time of the last verify kernel launched by this context, in ms
+ * (HIP events on the launch stream). */
+float pbft_last_kernel_ms(pbft_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PBFT_VERIFY_H */

@@ -1,0 +1,73 @@
+"""ctypes binding of libpbft_verify.so (the C ABI in include/pbft_verify.h).
+
+This is plumbing for tests and bench.py: the product is the HIP library.  There
+is NO CPU fallback: if the in-tree shared library is missing, or no gfx950 GPU
+is visible, every entry point raises PbftError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libpbft_verify.so")
+
+# every symbol include/pbft_verify.h declares
+EXPORTS = (
+    "pbft_verify_ctx_create", "pbft_verify_ctx_destroy", "pbft_verify_set_keys",
+    "pbft_verify_batch", "pbft_verify_batch_async", "pbft_verify_poll", "pbft_verify_wait",
+    "pbft_verify_batch_device", "pbft_digest_blake2b512", "pbft_digest_sha256",
+    "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms",
+)
+
+ERRORS = {0: "PBFT_OK", -1: "PBFT_EINVAL", -2: "PBFT_EHIP", -3: "PBFT_ENOKEYS",
+          -4: "PBFT_ENOMEM", -5: "PBFT_ENODEV", -6: "PBFT_EBUSY"}
+
+
+class PbftError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load the in-tree HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise PbftError(-5, f"{LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp, u8p = ctypes.c_void_p, ctypes.c_void_p
+    i32, u32, u64 = ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+    sig = {
+        "pbft_verify_ctx_create": (i32, [i32, ctypes.POINTER(vp)]),
+        "pbft_verify_ctx_destroy": (i32, [vp]),
+        "pbft_verify_set_keys": (i32, [vp, u8p, u32, u8p]),
+        "pbft_verify_batch": (i32, [vp, u8p, u8p, vp, u8p, u32, u32, u64, vp]),
+        "pbft_verify_batch_async": (i32, [vp, u8p, u8p, vp, u8p, u32, u32, u64, vp]),
+        "pbft_verify_poll": (i32, [vp]),
+        "pbft_verify_wait": (i32, [vp]),
+        "pbft_verify_batch_device": (i32, [vp, vp, vp, vp, vp, u32, u32, u64, vp, vp]),
+        "pbft_digest_blake2b512": (i32, [vp, u8p, vp, vp, u64, u8p]),
+        "pbft_digest_sha256": (i32, [vp, u8p, vp, vp, u64, u8p]),
+        "pbft_sign_batch": (i32, [vp, u8p, u32, vp, u8p, u32, u32, u64, u8p, u8p, u8p]),
+        "pbft_last_error": (ctypes.c_char_p, []),
+        "pbft_build_info": (ctypes.c_char_p, []),
+        "pbft_last_kernel_ms": (ctypes.c_float, [vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise PbftError(rc, load().pbft_last_error().decode(errors="replace"))
+    return rc

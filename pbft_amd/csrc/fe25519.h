@@ -1,0 +1,254 @@
+// GF(2^255 - 19) arithmetic for gfx950, one field element per lane.
+//
+// Representation: 10 unsigned limbs in radix 2^25.5 (26,25,26,25,... bits), held
+// in 32-bit VGPRs.  Products are 32x32->64 and accumulate with v_mad_u64_u32
+// (measured on MI355X: ~1.3x the issue cost of a 32-bit VOP3 op),
+// so a multiply is 100 mads + one 64-bit carry chain; a square is 55 mads.
+//
+// Bounds discipline (checked by tools/limb_bounds.py):
+//  * "carried"  : output of fe_mul/fe_sq/fe_carry: limbs <= 2^26 / 2^25 (+2^14 slack)
+//  * fe_add     : no carry; inputs carried -> limbs <= 2^27
+//  * fe_sub     : f + 2p - g; g must be carried; result limbs <= 3*2^26
+//  * fe_mul/sq  : accept any operands produced by one add/sub of carried values;
+//                 every 64-bit column stays < 2^63.3.
+// Semantics mirrored: curve25519-dalek 3.2.1 FieldElement (Cargo.lock:604-614).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#ifndef FE_FN
+#define FE_FN __host__ __device__ __forceinline__
+#endif
+
+namespace pbft {
+
+struct fe { uint32_t v[10]; };
+
+#define M26 0x3FFFFFFu
+#define M25 0x1FFFFFFu
+
+FE_FN void fe_zero(fe& h) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = 0;
+}
+FE_FN void fe_one(fe& h) { fe_zero(h); h.v[0] = 1; }
+
+FE_FN void fe_add(fe& h, const fe& f, const fe& g) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = f.v[i] + g.v[i];
+}
+
+// h = f - g + 2p  (g carried)
+FE_FN void fe_sub(fe& h, const fe& f, const fe& g) {
+  h.v[0] = f.v[0] + 0x7FFFFDAu - g.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = f.v[i] + ((i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu) - g.v[i];
+}
+
+// h = -f  (f carried)
+FE_FN void fe_neg(fe& h, const fe& f) {
+  h.v[0] = 0x7FFFFDAu - f.v[0];
+#pragma unroll
+  for (int i = 1; i < 10; ++i) h.v[i] = ((i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu) - f.v[i];
+}
+
+// one carry pass over u32 limbs (inputs < 2^31)
+FE_FN void fe_carry(fe& h) {
+  uint32_t c;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int sh = (i & 1) ? 25 : 26;
+    c = h.v[i] >> sh; h.v[i] &= (i & 1) ? M25 : M26; h.v[i + 1] += c;
+  }
+  c = h.v[9] >> 25; h.v[9] &= M25; h.v[0] += 19u * c;
+  c = h.v[0] >> 26; h.v[0] &= M26; h.v[1] += c;
+}
+
+#define MUL64(a, b) ((uint64_t)(a) * (uint64_t)(b))
+
+FE_FN void fe_reduce_wide(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t h3,
+                                               uint64_t h4, uint64_t h5, uint64_t h6, uint64_t h7,
+                                               uint64_t h8, uint64_t h9) {
+  uint64_t c;
+  c = h0 >> 26; h1 += c; h0 &= M26;
+  c = h4 >> 26; h5 += c; h4 &= M26;
+  c = h1 >> 25; h2 += c; h1 &= M25;
+  c = h5 >> 25; h6 += c; h5 &= M25;
+  c = h2 >> 26; h3 += c; h2 &= M26;
+  c = h6 >> 26; h7 += c; h6 &= M26;
+  c = h3 >> 25; h4 += c; h3 &= M25;
+  c = h7 >> 25; h8 += c; h7 &= M25;
+  c = h4 >> 26; h5 += c; h4 &= M26;
+  c = h8 >> 26; h9 += c; h8 &= M26;
+  c = h9 >> 25; h0 += c * 19u; h9 &= M25;
+  c = h0 >> 26; h1 += c; h0 &= M26;
+  h.v[0] = (uint32_t)h0; h.v[1] = (uint32_t)h1; h.v[2] = (uint32_t)h2; h.v[3] = (uint32_t)h3;
+  h.v[4] = (uint32_t)h4; h.v[5] = (uint32_t)h5; h.v[6] = (uint32_t)h6; h.v[7] = (uint32_t)h7;
+  h.v[8] = (uint32_t)h8; h.v[9] = (uint32_t)h9;
+}
+
+FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
+  const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
+  const uint32_t g1_19 = 19u * g1, g2_19 = 19u * g2, g3_19 = 19u * g3, g4_19 = 19u * g4, g5_19 = 19u * g5;
+  const uint32_t g6_19 = 19u * g6, g7_19 = 19u * g7, g8_19 = 19u * g8, g9_19 = 19u * g9;
+  const uint32_t f1_2 = 2u * f1, f3_2 = 2u * f3, f5_2 = 2u * f5, f7_2 = 2u * f7, f9_2 = 2u * f9;
+
+  uint64_t h0 = MUL64(f0, g0) + MUL64(f1_2, g9_19) + MUL64(f2, g8_19) + MUL64(f3_2, g7_19) + MUL64(f4, g6_19) +
+                MUL64(f5_2, g5_19) + MUL64(f6, g4_19) + MUL64(f7_2, g3_19) + MUL64(f8, g2_19) + MUL64(f9_2, g1_19);
+  uint64_t h1 = MUL64(f0, g1) + MUL64(f1, g0) + MUL64(f2, g9_19) + MUL64(f3, g8_19) + MUL64(f4, g7_19) +
+                MUL64(f5, g6_19) + MUL64(f6, g5_19) + MUL64(f7, g4_19) + MUL64(f8, g3_19) + MUL64(f9, g2_19);
+  uint64_t h2 = MUL64(f0, g2) + MUL64(f1_2, g1) + MUL64(f2, g0) + MUL64(f3_2, g9_19) + MUL64(f4, g8_19) +
+                MUL64(f5_2, g7_19) + MUL64(f6, g6_19) + MUL64(f7_2, g5_19) + MUL64(f8, g4_19) + MUL64(f9_2, g3_19);
+  uint64_t h3 = MUL64(f0, g3) + MUL64(f1, g2) + MUL64(f2, g1) + MUL64(f3, g0) + MUL64(f4, g9_19) +
+                MUL64(f5, g8_19) + MUL64(f6, g7_19) + MUL64(f7, g6_19) + MUL64(f8, g5_19) + MUL64(f9, g4_19);
+  uint64_t h4 = MUL64(f0, g4) + MUL64(f1_2, g3) + MUL64(f2, g2) + MUL64(f3_2, g1) + MUL64(f4, g0) +
+                MUL64(f5_2, g9_19) + MUL64(f6, g8_19) + MUL64(f7_2, g7_19) + MUL64(f8, g6_19) + MUL64(f9_2, g5_19);
+  uint64_t h5 = MUL64(f0, g5) + MUL64(f1, g4) + MUL64(f2, g3) + MUL64(f3, g2) + MUL64(f4, g1) +
+                MUL64(f5, g0) + MUL64(f6, g9_19) + MUL64(f7, g8_19) + MUL64(f8, g7_19) + MUL64(f9, g6_19);
+  uint64_t h6 = MUL64(f0, g6) + MUL64(f1_2, g5) + MUL64(f2, g4) + MUL64(f3_2, g3) + MUL64(f4, g2) +
+                MUL64(f5_2, g1) + MUL64(f6, g0) + MUL64(f7_2, g9_19) + MUL64(f8, g8_19) + MUL64(f9_2, g7_19);
+  uint64_t h7 = MUL64(f0, g7) + MUL64(f1, g6) + MUL64(f2, g5) + MUL64(f3, g4) + MUL64(f4, g3) +
+                MUL64(f5, g2) + MUL64(f6, g1) + MUL64(f7, g0) + MUL64(f8, g9_19) + MUL64(f9, g8_19);
+  uint64_t h8 = MUL64(f0, g8) + MUL64(f1_2, g7) + MUL64(f2, g6) + MUL64(f3_2, g5) + MUL64(f4, g4) +
+                MUL64(f5_2, g3) + MUL64(f6, g2) + MUL64(f7_2, g1) + MUL64(f8, g0) + MUL64(f9_2, g9_19);
+  uint64_t h9 = MUL64(f0, g9) + MUL64(f1, g8) + MUL64(f2, g7) + MUL64(f3, g6) + MUL64(f4, g5) +
+                MUL64(f5, g4) + MUL64(f6, g3) + MUL64(f7, g2) + MUL64(f8, g1) + MUL64(f9, g0);
+  fe_reduce_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+FE_FN void fe_sq(fe& h, const fe& f) {
+  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
+  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
+  const uint32_t f0_2 = 2u * f0, f1_2 = 2u * f1, f2_2 = 2u * f2, f3_2 = 2u * f3, f4_2 = 2u * f4;
+  const uint32_t f5_2 = 2u * f5, f6_2 = 2u * f6, f7_2 = 2u * f7;
+  const uint32_t f5_38 = 38u * f5, f6_19 = 19u * f6, f7_38 = 38u * f7, f8_19 = 19u * f8, f9_38 = 38u * f9;
+
+  uint64_t h0 = MUL64(f0, f0) + MUL64(f1_2, f9_38) + MUL64(f2_2, f8_19) + MUL64(f3_2, f7_38) +
+                MUL64(f4_2, f6_19) + MUL64(f5, f5_38);
+  uint64_t h1 = MUL64(f0_2, f1) + MUL64(f2, f9_38) + MUL64(f3_2, f8_19) + MUL64(f4, f7_38) + MUL64(f5_2, f6_19);
+  uint64_t h2 = MUL64(f0_2, f2) + MUL64(f1_2, f1) + MUL64(f3_2, f9_38) + MUL64(f4_2, f8_19) +
+                MUL64(f5_2, f7_38) + MUL64(f6, f6_19);
+  uint64_t h3 = MUL64(f0_2, f3) + MUL64(f1_2, f2) + MUL64(f4, f9_38) + MUL64(f5_2, f8_19) + MUL64(f6, f7_38);
+  uint64_t h4 = MUL64(f0_2, f4) + MUL64(f1_2, f3_2) + MUL64(f2, f2) + MUL64(f5_2, f9_38) +
+                MUL64(f6_2, f8_19) + MUL64(f7, f7_38);
+  uint64_t h5 = MUL64(f0_2, f5) + MUL64(f1_2, f4) + MUL64(f2_2, f3) + MUL64(f6, f9_38) + MUL64(f7_2, f8_19);
+  uint64_t h6 = MUL64(f0_2, f6) + MUL64(f1_2, f5_2) + MUL64(f2_2, f4) + MUL64(f3_2, f3) +
+                MUL64(f7_2, f9_38) + MUL64(f8, f8_19);
+  uint64_t h7 = MUL64(f0_2, f7) + MUL64(f1_2, f6) + MUL64(f2_2, f5) + MUL64(f3_2, f4) + MUL64(f8, f9_38);
+  uint64_t h8 = MUL64(f0_2, f8) + MUL64(f1_2, f7_2) + MUL64(f2_2, f6) + MUL64(f3_2, f5_2) +
+                MUL64(f4, f4) + MUL64(f9, f9_38);
+  uint64_t h9 = MUL64(f0_2, f9) + MUL64(f1_2, f8) + MUL64(f2_2, f7) + MUL64(f3_2, f6) + MUL64(f4_2, f5);
+  fe_reduce_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+}
+
+FE_FN void fe_sqn(fe& h, const fe& f, int n) {
+  fe_sq(h, f);
+  for (int i = 1; i < n; ++i) fe_sq(h, h);
+}
+
+// z^(2^250 - 1) and z^11 (shared by invert and pow22523)
+FE_FN void fe_pow250(fe& out, fe& z11, const fe& z) {
+  fe t0, t1, z9, z2_5_0, z2_10_0, z2_20_0, z2_50_0;
+  fe_sq(t1, z);                 // z^2
+  fe_sq(t0, t1); fe_sq(t0, t0); // z^8
+  fe_mul(z9, t0, z);            // z^9
+  fe_mul(z11, z9, t1);          // z^11
+  fe_sq(t0, z11);               // z^22
+  fe_mul(z2_5_0, t0, z9);       // z^31 = z^(2^5-1)
+  fe_sqn(t0, z2_5_0, 5); fe_mul(z2_10_0, t0, z2_5_0);
+  fe_sqn(t0, z2_10_0, 10); fe_mul(z2_20_0, t0, z2_10_0);
+  fe_sqn(t0, z2_20_0, 20); fe_mul(t1, t0, z2_20_0);
+  fe_sqn(t0, t1, 10); fe_mul(z2_50_0, t0, z2_10_0);
+  fe_sqn(t0, z2_50_0, 50); fe_mul(t1, t0, z2_50_0);      // 2^100 - 1
+  fe_sqn(t0, t1, 100); fe_mul(t1, t0, t1);               // 2^200 - 1
+  fe_sqn(t0, t1, 50); fe_mul(out, t0, z2_50_0);          // 2^250 - 1
+}
+
+FE_FN void fe_invert(fe& out, const fe& z) {
+  fe t, z11;
+  fe_pow250(t, z11, z);
+  fe_sqn(t, t, 5);
+  fe_mul(out, t, z11);  // z^(2^255 - 21) = z^(p-2)
+}
+
+FE_FN void fe_pow22523(fe& out, const fe& z) {
+  fe t, z11;
+  fe_pow250(t, z11, z);
+  fe_sqn(t, t, 2);
+  fe_mul(out, t, z);    // z^(2^252 - 3) = z^((p-5)/8)
+}
+
+// Fully reduce to the canonical representative < p, as 8 little-endian u32 words.
+FE_FN void fe_to_words(uint32_t w[8], const fe& f) {
+  fe t = f;
+  fe_carry(t);
+  fe_carry(t);
+  // q = 1 iff t >= p
+  uint32_t q = (t.v[0] + 19u) >> 26;
+#pragma unroll
+  for (int i = 1; i < 10; ++i) q = (t.v[i] + q) >> ((i & 1) ? 25 : 26);
+  t.v[0] += 19u * q;
+  uint32_t c;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int sh = (i & 1) ? 25 : 26;
+    c = t.v[i] >> sh; t.v[i] &= (i & 1) ? M25 : M26; t.v[i + 1] += c;
+  }
+  t.v[9] &= M25;
+  // pack: limb i starts at bit offsets 0,26,51,77,102,128,153,179,204,230
+  w[0] = t.v[0] | (t.v[1] << 26);
+  w[1] = (t.v[1] >> 6) | (t.v[2] << 19);
+  w[2] = (t.v[2] >> 13) | (t.v[3] << 13);
+  w[3] = (t.v[3] >> 19) | (t.v[4] << 6);
+  w[4] = t.v[5] | (t.v[6] << 25);
+  w[5] = (t.v[6] >> 7) | (t.v[7] << 19);
+  w[6] = (t.v[7] >> 13) | (t.v[8] << 12);
+  w[7] = (t.v[8] >> 20) | (t.v[9] << 6);
+}
+
+// Load 8 LE u32 words (bit 255 ignored, value NOT reduced: dalek from_bytes)
+FE_FN void fe_from_words(fe& h, const uint32_t w[8]) {
+  h.v[0] = w[0] & M26;
+  h.v[1] = ((w[0] >> 26) | (w[1] << 6)) & M25;
+  h.v[2] = ((w[1] >> 19) | (w[2] << 13)) & M26;
+  h.v[3] = ((w[2] >> 13) | (w[3] << 19)) & M25;
+  h.v[4] = (w[3] >> 6) & M26;
+  h.v[5] = w[4] & M25;
+  h.v[6] = ((w[4] >> 25) | (w[5] << 7)) & M26;
+  h.v[7] = ((w[5] >> 19) | (w[6] << 13)) & M25;
+  h.v[8] = ((w[6] >> 12) | (w[7] << 20)) & M26;
+  h.v[9] = (w[7] >> 6) & M25;
+}
+
+FE_FN bool fe_is_zero(const fe& f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= w[i];
+  return o == 0;
+}
+
+FE_FN bool fe_is_negative(const fe& f) {
+  uint32_t w[8];
+  fe_to_words(w, f);
+  return w[0] & 1;
+}
+
+FE_FN bool fe_eq(const fe& a, const fe& b) {
+  fe d;
+  fe t = b;
+  fe_carry(t);
+  fe_sub(d, a, t);
+  return fe_is_zero(d);
+}
+
+FE_FN void fe_cmov(fe& h, const fe& f, bool c) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) h.v[i] = c ? f.v[i] : h.v[i];
+}
+
+}  // namespace pbft

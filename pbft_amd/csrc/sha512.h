@@ -1,0 +1,147 @@
+// SHA-512 (FIPS 180-4) for one lane, specialised for the Ed25519 challenge
+// hash k = SHA-512(R || A || M) of ed25519-dalek 1.0.1 verify_strict (sha2 0.9.9,
+// Cargo.lock:2784-2787).  R and A are 32 bytes each (4 big-endian words);
+// M is fetched from HBM as aligned dwords and re-aligned per lane, so the
+// message layout in memory can have any byte stride.
+#pragma once
+#include "fe25519.h"
+
+namespace pbft {
+
+__host__ __device__ __forceinline__ uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+__host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+#define SHA512_K_TABLE                                                                                       \
+  {0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,               \
+   0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,               \
+   0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,               \
+   0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,               \
+   0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,               \
+   0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,               \
+   0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,               \
+   0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,               \
+   0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,               \
+   0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,               \
+   0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,               \
+   0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,               \
+   0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,               \
+   0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,               \
+   0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,               \
+   0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,               \
+   0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,               \
+   0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,               \
+   0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,               \
+   0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL}
+
+__host__ __device__ __forceinline__ void sha512_init(uint64_t H[8]) {
+  H[0] = 0x6a09e667f3bcc908ULL; H[1] = 0xbb67ae8584caa73bULL; H[2] = 0x3c6ef372fe94f82bULL;
+  H[3] = 0xa54ff53a5f1d36f1ULL; H[4] = 0x510e527fade682d1ULL; H[5] = 0x9b05688c2b3e6c1fULL;
+  H[6] = 0x1f83d9abfb41bd6bULL; H[7] = 0x5be0cd19137e2179ULL;
+}
+
+// One compression; W holds the 16 big-endian message words of the block.
+__host__ __device__ __forceinline__ void sha512_compress(uint64_t H[8], uint64_t W[16]) {
+  const uint64_t K[80] = SHA512_K_TABLE;
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+  for (int t = 0; t < 80; ++t) {
+    uint64_t w;
+    if (t < 16) {
+      w = W[t];
+    } else {
+      const uint64_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
+      const uint64_t s0 = ror64(w15, 1) ^ ror64(w15, 8) ^ (w15 >> 7);
+      const uint64_t s1 = ror64(w2, 19) ^ ror64(w2, 61) ^ (w2 >> 6);
+      w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
+      W[t & 15] = w;
+    }
+    const uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
+    const uint64_t ch = (e & f) ^ (~e & g);
+    const uint64_t T1 = h + S1 + ch + K[t] + w;
+    const uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
+    const uint64_t mj = (a & b) ^ (c & (a ^ b));
+    const uint64_t T2 = S0 + mj;
+    h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + T2;
+  }
+  H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+}
+
+// 4 message bytes starting at an arbitrary byte address (little-endian u32).
+// Reads the two aligned dwords that cover them.
+__host__ __device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* q = (const uint32_t*)(a & ~(uintptr_t)3);
+  const uint32_t sh = (uint32_t)(a & 3) * 8u;
+  const uint32_t lo = q[0];
+  const uint32_t hi = sh ? q[1] : 0u;
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+}
+
+// Big-endian 64-bit word j (j >= 0) of the padded stream M || 0x80 || 0...,
+// without the length field.  LEN < 0 means the length is the runtime `len`.
+__host__ __device__ __forceinline__ uint64_t msg_word(const uint8_t* m, int len, int j) {
+  const int o = 8 * j;
+  uint32_t w0 = 0, w1 = 0;
+  if (o < len) w0 = load_u32_unaligned(m + o);
+  if (o + 4 < len) w1 = load_u32_unaligned(m + o + 4);
+  // mask bytes >= len and insert the 0x80 terminator at byte `len`
+  const int r0 = len - o, r1 = len - o - 4;
+  if (r0 < 4) w0 = (r0 <= 0) ? 0u : (w0 & ((1u << (8 * r0)) - 1u));
+  if (r0 >= 0 && r0 < 4) w0 |= 0x80u << (8 * r0);
+  if (r1 < 4) w1 = (r1 <= 0) ? 0u : (w1 & ((1u << (8 * r1)) - 1u));
+  if (r1 >= 0 && r1 < 4) w1 |= 0x80u << (8 * r1);
+  return ((uint64_t)bswap32(w0) << 32) | bswap32(w1);
+}
+
+// SHA-512(pre || M) where pre is NPRE (32 or 64) bytes held in registers as
+// little-endian words and M is fetched from memory.  out: 16 LE words of the
+// digest read as a little-endian 512-bit integer (Scalar::from_hash input).
+template <int NPRE, int LEN>
+__host__ __device__ __forceinline__ void sha512_pre(uint32_t out[16], const uint32_t pre[NPRE / 4],
+                                                    const uint8_t* m, int len_rt) {
+  static_assert(NPRE == 32 || NPRE == 64, "prefix is 32 or 64 bytes");
+  constexpr int NW = NPRE / 8;  // prefix words (64-bit)
+  const int len = LEN >= 0 ? LEN : len_rt;
+  uint64_t H[8];
+  sha512_init(H);
+  const int total = NPRE + len;
+  const int nblocks = (total + 17 + 127) / 128;
+  uint64_t W[16];
+#pragma unroll
+  for (int t = 0; t < NW; ++t) W[t] = ((uint64_t)bswap32(pre[2 * t]) << 32) | bswap32(pre[2 * t + 1]);
+#pragma unroll
+  for (int t = NW; t < 16; ++t) W[t] = msg_word(m, len, t - NW);
+  if (nblocks == 1) {
+    W[14] = 0;
+    W[15] = (uint64_t)total * 8u;
+  }
+  sha512_compress(H, W);
+  for (int b = 1; b < nblocks; ++b) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) W[t] = msg_word(m, len, 16 * b - NW + t);
+    if (b == nblocks - 1) {
+      W[14] = 0;
+      W[15] = (uint64_t)total * 8u;
+    }
+    sha512_compress(H, W);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    out[2 * i] = bswap32((uint32_t)(H[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)H[i]);
+  }
+}
+
+// k-hash: SHA-512(R || A || M), r and a as 8 LE words each.
+template <int LEN>
+__host__ __device__ __forceinline__ void sha512_ram(uint32_t out[16], const uint32_t r[8], const uint32_t a[8],
+                                                    const uint8_t* m, int len_rt) {
+  uint32_t pre[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) { pre[i] = r[i]; pre[8 + i] = a[i]; }
+  sha512_pre<64, LEN>(out, pre, m, len_rt);
+}
+
+}  // namespace pbft

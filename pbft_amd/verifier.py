@@ -1,0 +1,170 @@
+"""BatchVerifier: host-side view of the GPU verifier (BASELINE.json north_star).
+
+Mirrors the trait the reference would bind:
+
+    trait BatchVerifier {
+        fn submit(&mut self, b: &SigBatch) -> Ticket;
+        fn poll(&mut self, t: Ticket) -> Option<Bitmap>;
+        fn verify(&mut self, b: &SigBatch) -> Bitmap;   // blocking
+    }
+
+It replaces the per-message validators validate_prepare
+(src/behavior.rs:159-175) and validate_commit (src/behavior.rs:184-195), whose
+signature checks are TODOs (src/behavior.rs:127, :185).  Invalid signatures are
+bit 0 in the returned bitmap, never an exception (the reference panics via
+.unwrap() at src/behavior.rs:345, :371; the build drops the message instead).
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import PbftError, check, load
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data if a is not None and a.size else 0
+
+
+@dataclass
+class SigBatch:
+    """Struct-of-arrays batch of one (view, seq) round window (or several)."""
+
+    R: np.ndarray        # (N, 32) uint8
+    S: np.ndarray        # (N, 32) uint8
+    key_idx: np.ndarray  # (N,) uint16, index into the installed key set
+    msg: np.ndarray      # (N, stride) uint8, first msg_len bytes signed
+    msg_len: int
+
+    def __post_init__(self):
+        self.R = np.ascontiguousarray(self.R, dtype=np.uint8).reshape(-1, 32)
+        self.S = np.ascontiguousarray(self.S, dtype=np.uint8).reshape(-1, 32)
+        self.key_idx = np.ascontiguousarray(self.key_idx, dtype=np.uint16).reshape(-1)
+        n = len(self.R)
+        if len(self.S) != n or len(self.key_idx) != n:
+            raise ValueError("R, S and key_idx must have the same length")
+        m = np.ascontiguousarray(self.msg, dtype=np.uint8)
+        if m.ndim == 1:
+            m = m.reshape(n, -1) if n else m.reshape(0, max(self.msg_len, 1))
+        if m.shape[0] != n or m.shape[1] < self.msg_len:
+            raise ValueError("msg must be (N, stride >= msg_len)")
+        self.msg = m
+
+    def __len__(self) -> int:
+        return len(self.R)
+
+
+def bitmap_to_bool(bitmap: np.ndarray, n: int) -> np.ndarray:
+    """LSB-first u64 words -> bool[n]."""
+    bits = np.unpackbits(bitmap.view(np.uint8), bitorder="little")
+    return bits[:n].astype(bool)
+
+
+class GpuBatchVerifier:
+    """One HIP context (one GPU).  Not thread-safe: one per host thread."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load()
+        self._ctx = ctypes.c_void_p()
+        check(self._lib.pbft_verify_ctx_create(device, ctypes.byref(self._ctx)))
+        self.device = device
+        self.n_keys = 0
+        self._pending = None
+
+    # -- key set (libp2p identity keys, src/main.rs:39-40) ------------------
+    def set_keys(self, keys: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+        ok = np.zeros(len(keys), dtype=np.uint8)
+        check(self._lib.pbft_verify_set_keys(self._ctx, _ptr(keys), len(keys), _ptr(ok)))
+        self.n_keys = len(keys)
+        return ok.astype(bool)
+
+    # -- BatchVerifier -------------------------------------------------------
+    def verify(self, b: SigBatch) -> np.ndarray:
+        """Blocking; returns the ceil(N/64) u64 bitmap words."""
+        n = len(b)
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_batch(self._ctx, _ptr(b.R), _ptr(b.S), _ptr(b.key_idx), _ptr(b.msg),
+                                          b.msg_len, b.msg.shape[1], n, _ptr(out)))
+        return out
+
+    def submit(self, b: SigBatch) -> int:
+        n = len(b)
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_batch_async(self._ctx, _ptr(b.R), _ptr(b.S), _ptr(b.key_idx), _ptr(b.msg),
+                                                b.msg_len, b.msg.shape[1], n, _ptr(out)))
+        self._pending = (b, out)  # keep host buffers alive until poll/wait
+        return id(out)
+
+    def poll(self, ticket: int):
+        if self._pending is None or id(self._pending[1]) != ticket:
+            raise PbftError(-1, "unknown ticket")
+        if check(self._lib.pbft_verify_poll(self._ctx)) == 1:
+            out = self._pending[1]
+            self._pending = None
+            return out
+        return None
+
+    def wait(self, ticket: int) -> np.ndarray:
+        if self._pending is None or id(self._pending[1]) != ticket:
+            raise PbftError(-1, "unknown ticket")
+        check(self._lib.pbft_verify_wait(self._ctx))
+        out = self._pending[1]
+        self._pending = None
+        return out
+
+    def verify_device(self, d_R: int, d_S: int, d_key_idx: int, d_msg: int, msg_len: int, msg_stride: int,
+                      n: int, d_bitmap: int, stream: int = 0) -> None:
+        """Enqueue on device-resident buffers (raw device pointers)."""
+        check(self._lib.pbft_verify_batch_device(self._ctx, d_R, d_S, d_key_idx, d_msg, msg_len, msg_stride, n,
+                                                 d_bitmap, stream or None))
+
+    def last_kernel_ms(self) -> float:
+        return float(self._lib.pbft_last_kernel_ms(self._ctx))
+
+    # -- request digests (src/message.rs:209-212) and signing ---------------
+    def _pack(self, items):
+        lens = np.array([len(x) for x in items], dtype=np.uint32)
+        offs = np.zeros(len(items), dtype=np.uint64)
+        if len(items):
+            offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        data = np.frombuffer(b"".join(items) + bytes(16), dtype=np.uint8).copy()
+        return data, offs, lens
+
+    def blake2b512(self, items) -> np.ndarray:
+        data, offs, lens = self._pack(items)
+        out = np.zeros((len(items), 64), dtype=np.uint8)
+        check(self._lib.pbft_digest_blake2b512(self._ctx, _ptr(data), _ptr(offs), _ptr(lens), len(items), _ptr(out)))
+        return out
+
+    def sha256(self, items) -> np.ndarray:
+        data, offs, lens = self._pack(items)
+        out = np.zeros((len(items), 32), dtype=np.uint8)
+        check(self._lib.pbft_digest_sha256(self._ctx, _ptr(data), _ptr(offs), _ptr(lens), len(items), _ptr(out)))
+        return out
+
+    def sign(self, seeds: np.ndarray, seed_idx: np.ndarray, msg: np.ndarray, msg_len: int):
+        """RFC 8032 signatures; returns (R, S, public_keys)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint8).reshape(-1, 32)
+        seed_idx = np.ascontiguousarray(seed_idx, dtype=np.uint16).reshape(-1)
+        n = len(seed_idx)
+        msg = np.ascontiguousarray(msg, dtype=np.uint8).reshape(n, -1) if n else np.zeros((0, 1), np.uint8)
+        R = np.zeros((n, 32), dtype=np.uint8)
+        S = np.zeros((n, 32), dtype=np.uint8)
+        pub = np.zeros((len(seeds), 32), dtype=np.uint8)
+        check(self._lib.pbft_sign_batch(self._ctx, _ptr(seeds), len(seeds), _ptr(seed_idx), _ptr(msg), msg_len,
+                                        msg.shape[1], n, _ptr(R), _ptr(S), _ptr(pub)))
+        return R, S, pub
+
+    def close(self):
+        if self._ctx:
+            self._lib.pbft_verify_ctx_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

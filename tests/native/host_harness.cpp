@@ -1,0 +1,147 @@
+// TEST INFRASTRUCTURE: the product's __host__ __device__ arithmetic
+// (pbft_amd/csrc/*.h) compiled for the HOST, so tests/test_host_harness.py can
+// check fields, hashing, scalar reduction, comb tables and the full per-lane
+// verify against the oracle in a container without a GPU.  Never loaded by the
+// product path (pbft_amd/ loads only libpbft_verify.so, which needs a GPU).
+#include "../../pbft_amd/csrc/verify_core.h"
+#include <vector>
+#include <cstring>
+
+using namespace pbft;
+
+static void words_from_bytes(uint32_t w[8], const uint8_t* b) {
+  for (int i = 0; i < 8; ++i) w[i] = b[4 * i] | (b[4 * i + 1] << 8) | (b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+static void bytes_from_words(uint8_t* b, const uint32_t w[8]) {
+  for (int i = 0; i < 8; ++i) for (int j = 0; j < 4; ++j) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
+}
+
+template <int W>
+static void build_table(const ge& P0, uint32_t* out) {
+  for (int pos = 0; pos < comb<W>::P; ++pos)
+    for (int j = 0; j < comb<W>::E; ++j) {
+      niels n;
+      comb_entry<W>(n, P0, pos, j);
+      store_niels(out + ((size_t)pos * comb<W>::E + j) * 32, n);
+    }
+}
+
+extern "C" {
+
+void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
+  uint32_t wa[8], wb[8], wo[8];
+  words_from_bytes(wa, a); words_from_bytes(wb, b);
+  fe fa, fb, fo;
+  fe_from_words(fa, wa); fe_from_words(fb, wb);
+  switch (op) {
+    case 0: fe_mul(fo, fa, fb); break;
+    case 1: fe_sq(fo, fa); break;
+    case 2: fe_invert(fo, fa); break;
+    case 3: fe_pow22523(fo, fa); break;
+    case 4: { fe t; fe_add(t, fa, fb); fe_mul(fo, t, t); break; }     // (a+b)^2 via mul of unreduced
+    case 5: { fe t; fe_sub(t, fa, fb); fe_mul(fo, t, fb); break; }    // (a-b)*b
+    case 6: { fe t; fe_add(t, fa, fb); fe_sq(fo, t); break; }         // (a+b)^2 via sq of unreduced
+    default: fo = fa;
+  }
+  fe_to_words(wo, fo);
+  bytes_from_words(out, wo);
+}
+
+void hh_sha512_ram(const uint8_t* r, const uint8_t* a, const uint8_t* m, int len, uint8_t* out64) {
+  uint32_t wr[8], wa[8], h[16];
+  words_from_bytes(wr, r); words_from_bytes(wa, a);
+  sha512_ram<-1>(h, wr, wa, m, len);
+  for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
+void hh_reduce512(const uint8_t* x64, uint8_t* out32) {
+  uint32_t x[16], o[8];
+  for (int i = 0; i < 16; ++i) x[i] = x64[4 * i] | (x64[4 * i + 1] << 8) | (x64[4 * i + 2] << 16) | ((uint32_t)x64[4 * i + 3] << 24);
+  sc_reduce512(o, x);
+  bytes_from_words(out32, o);
+}
+
+// decompress + small-order (returns 0 bad encoding, 1 ok, 2 small order)
+int hh_decompress(const uint8_t* enc, uint8_t* out_compressed) {
+  uint32_t w[8];
+  words_from_bytes(w, enc);
+  ge p;
+  if (!ge_decompress(p, w)) return 0;
+  fe zi, x, y;
+  fe_invert(zi, p.Z); fe_mul(x, p.X, zi); fe_mul(y, p.Y, zi);
+  uint32_t xw[8], yw[8];
+  fe_to_words(xw, x); fe_to_words(yw, y);
+  yw[7] |= (xw[0] & 1u) << 31;
+  bytes_from_words(out_compressed, yw);
+  return ge_is_small_order(p) ? 2 : 1;
+}
+
+static int table_words(int w) {
+  switch (w) { case 4: return (int)comb<4>::TABLE_WORDS; case 5: return (int)comb<5>::TABLE_WORDS;
+               case 6: return (int)comb<6>::TABLE_WORDS; case 8: return (int)comb<8>::TABLE_WORDS; }
+  return -1;
+}
+int hh_table_words(int w) { return table_words(w); }
+
+// comb table of (negate ? -P : P) for the point encoded by enc; returns 0 on bad encoding
+int hh_build_table(int w, const uint8_t* enc, int negate, uint32_t* out) {
+  uint32_t e[8];
+  words_from_bytes(e, enc);
+  ge P;
+  if (!ge_decompress(P, e)) return 0;
+  if (negate) { ge t; ge_neg(t, P); P = t; }
+  switch (w) {
+    case 4: build_table<4>(P, out); break;
+    case 5: build_table<5>(P, out); break;
+    case 6: build_table<6>(P, out); break;
+    case 8: build_table<8>(P, out); break;
+    default: return -1;
+  }
+  return 1;
+}
+
+// SoA batch verify on the host with tables from hh_build_table (w = 4 or 8 both sides)
+int hh_verify_batch(int w, const uint32_t* tabB, const uint32_t* tabA_all, const uint8_t* keys,
+                    const uint8_t* key_ok, uint32_t n_keys, const uint8_t* R, const uint8_t* S,
+                    const uint16_t* key_idx, const uint8_t* msg, uint32_t msg_len, uint32_t msg_stride,
+                    uint64_t N, uint8_t* accept) {
+  const int tw = table_words(w);
+  for (uint64_t i = 0; i < N; ++i) {
+    uint32_t r[8], s[8], a[8];
+    words_from_bytes(r, R + 32 * i); words_from_bytes(s, S + 32 * i);
+    uint32_t ki = key_idx[i];
+    bool kok = ki < n_keys && key_ok[ki];
+    if (ki >= n_keys) ki = 0;
+    words_from_bytes(a, keys + 32 * (size_t)ki);
+    const uint32_t* tA = tabA_all + (size_t)ki * tw;
+    bool ok;
+    if (w == 4) ok = verify_lane<4, 4, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
+    else if (w == 8) ok = verify_lane<8, 8, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
+    else return -1;
+    accept[i] = ok;
+  }
+  return 0;
+}
+
+}  // extern "C"
+
+extern "C" int hh_comb2(int w, const uint32_t* tabB, const uint32_t* tabA, const uint8_t* s32, const uint8_t* k32,
+                        uint8_t* out_compressed) {
+  if (w != 4) return -1;
+  uint32_t s[8], k[8];
+  words_from_bytes(s, s32); words_from_bytes(k, k32);
+  ge P; ge_identity(P);
+  digit_stream<4> ds; ds.init(s);
+  digit_stream<4> dk; dk.init(k);
+  for (int i = 0; i < comb<4>::P; ++i) {
+    int d = ds.next(); int ad = d < 0 ? -d : d; niels q;
+    load_niels(q, tabB + ((size_t)i * comb<4>::E + ad) * 32); ge_madd_signed(P, P, q, d < 0);
+    d = dk.next(); ad = d < 0 ? -d : d;
+    load_niels(q, tabA + ((size_t)i * comb<4>::E + ad) * 32); ge_madd_signed(P, P, q, d < 0);
+  }
+  fe zi, x, y; fe_invert(zi, P.Z); fe_mul(x, P.X, zi); fe_mul(y, P.Y, zi);
+  uint32_t xw[8], yw[8]; fe_to_words(xw, x); fe_to_words(yw, y);
+  yw[7] |= (xw[0] & 1u) << 31;
+  bytes_from_words(out_compressed, yw);
+  return 0;
+}
