@@ -5,7 +5,7 @@
 #include <cstdio>
 #include <cstdint>
 
-#define ITERS 4096
+#define ITERS 32768
 #define CH 8
 
 __global__ void k_mad64(uint64_t* out, uint32_t seed) {
