@@ -38,6 +38,15 @@ def load() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: PyTorch-ROCm bundles its own libamdhip64.so.7.
+    # Importing torch first makes this library bind to that same runtime (same
+    # SONAME), so torch tensors / streams and our contexts share one HIP
+    # instance.  Loading ours first would pull /opt/rocm's copy and leave torch
+    # unable to initialise.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise PbftError(-5, f"{LIB_PATH} not built: run python -c 'import __graft_entry__ as g; g.build()'")
     lib = ctypes.CDLL(LIB_PATH)

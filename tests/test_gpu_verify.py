@@ -1,18 +1,28 @@
-"""GPU parity: the HIP verifier's bitmap vs the oracle, bit-exact.
+"""GPU parity: the HIP kernels vs the oracle, bit-exact (run with -m gpu on an MI355X).
 
-Oracle = oracle/ed25519_ref.py (expected bits committed in tests/golden) and
-oracle/ed25519_oracle.c for seeded batches too large for pure Python.
+Checked through the C ABI (pbft_amd binds libpbft_verify.so with ctypes):
+  * committed golden vectors (18 adversarial classes, 11 message lengths);
+  * seeded config-#3 round (n = 64 keys, 2^16 signatures, 1 % adversarial) vs
+    the C oracle (oracle/ed25519_oracle.c), and the full-size config-#4 round
+    (2^20) through size-independent properties + a popcount/checksum vs the oracle;
+  * RFC 8032 signing vs the oracle signer; Blake2b-512 / SHA-256 vs hashlib;
+  * API edges: N = 0, 1, 63, 65, out-of-range key index, async submit/poll,
+    device-resident entry point with odd strides.
 """
 import ctypes
 import hashlib
+import json
 import os
+import random
 
 import numpy as np
 import pytest
 
-from conftest import ROOT, golden_batches
+from conftest import GOLDEN, ROOT, golden_batches
 
 pytestmark = pytest.mark.gpu
+L = 2**252 + 27742317777372353535851937790883648493
+KAT = json.load(open(os.path.join(GOLDEN, "kat.json")))
 
 
 @pytest.fixture(scope="module")
@@ -23,17 +33,221 @@ def gv():
     v.close()
 
 
-def test_golden_bitmaps_bit_exact(gv, golden):
+@pytest.fixture(scope="module")
+def coracle():
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    vp = ctypes.c_void_p
+    lib.oracle_verify_batch.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                        ctypes.c_uint64, vp, ctypes.c_int]
+    lib.oracle_sign_batch.argtypes = [vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, vp, vp,
+                                      ctypes.c_int]
+    lib.oracle_public_key.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    return lib
+
+
+def oracle_bits(coracle, keys, R, S, key_idx, msg, msg_len):
+    n = len(R)
+    out = np.zeros(n, dtype=np.uint8)
+    msg = np.ascontiguousarray(msg)
+    rc = coracle.oracle_verify_batch(keys.ctypes.data, len(keys), R.ctypes.data, S.ctypes.data, key_idx.ctypes.data,
+                                     msg.ctypes.data, msg_len, msg.shape[1], n, out.ctypes.data,
+                                     min(32, os.cpu_count() or 1))
+    assert rc == 0
+    return out.astype(bool)
+
+
+def seeds_for(n, tag=0):
+    return np.stack([np.frombuffer(hashlib.sha512(b"pbft-key" + tag.to_bytes(8, "little") +
+                                                  i.to_bytes(8, "little")).digest()[:32], dtype=np.uint8)
+                     for i in range(n)])
+
+
+def round_batch(gv, n_keys, n_seq, seq0=1, tag=0):
+    """A synthetic PBFT round: every replica signs Prepare + Commit per seq (GPU signer)."""
+    seeds = seeds_for(n_keys, tag)
+    msgs = []
+    for s in range(seq0, seq0 + n_seq):
+        d = hashlib.blake2b(b"op-" + str(s).encode(), digest_size=64).digest()
+        for kind in (1, 2):
+            env = b"PBFT" + bytes([kind]) + (1).to_bytes(8, "little") + s.to_bytes(8, "little") + d
+            msgs.extend([env] * n_keys)
+    msg = np.frombuffer(b"".join(msgs), dtype=np.uint8).reshape(-1, 85).copy()
+    key_idx = np.tile(np.arange(n_keys, dtype=np.uint16), 2 * n_seq)
+    R, S, pub = gv.sign(seeds, key_idx, msg, 85)
+    return seeds, pub, R, S, key_idx, msg
+
+
+def adversarial(rng, pub, R, S, key_idx, msg, frac=0.01):
+    """Mutate a seeded `frac` of lanes across the §8(d) adversarial classes."""
+    R, S, key_idx, msg = R.copy(), S.copy(), key_idx.copy(), msg.copy()
+    n = len(R)
+    idx = rng.choice(n, size=max(11, int(n * frac)), replace=False)
+    so = [bytes.fromhex(h) for h in KAT["small_order_encodings"]]
+    nc = [bytes.fromhex(h) for h in KAT["noncanonical_decodable_encodings"]]
+    # an encoding that does not decode (y^2 - 1)/(d y^2 + 1) non-square: y = 2 is one
+    noc = (2).to_bytes(32, "little")
+    for j, i in enumerate(idx):
+        c = j % 11
+        if c == 0:
+            msg[i, rng.integers(85)] ^= 1 << rng.integers(8)
+        elif c == 1:
+            R[i, rng.integers(32)] ^= 1 << rng.integers(8)
+        elif c == 2:
+            S[i, rng.integers(31)] ^= 1 << rng.integers(8)
+        elif c == 3:
+            s = int.from_bytes(S[i].tobytes(), "little") + L
+            S[i] = np.frombuffer(s.to_bytes(32, "little"), dtype=np.uint8)
+        elif c == 4:
+            S[i, 31] |= 0x80
+        elif c == 5:
+            R[i] = np.frombuffer(noc, dtype=np.uint8)
+        elif c == 6:
+            R[i] = np.frombuffer(nc[j % len(nc)], dtype=np.uint8)
+        elif c == 7:
+            R[i] = np.frombuffer(so[j % len(so)], dtype=np.uint8)
+        elif c == 8:
+            key_idx[i] = (key_idx[i] + 1) % len(pub)
+        elif c == 9:
+            R[i] = 0
+            S[i] = 0
+        else:
+            key_idx[i] = len(pub) + 3  # out of the installed key set
+    return R, S, key_idx, msg, idx
+
+
+def verify(gv, R, S, key_idx, msg, msg_len):
     from pbft_amd import SigBatch, bitmap_to_bool
+    bm = gv.verify(SigBatch(R, S, key_idx, msg, msg_len))
+    return bitmap_to_bool(bm, len(R)), bm
+
+
+def test_golden_bitmaps_bit_exact(gv, golden):
     for ml, b in golden_batches(golden):
         ok = gv.set_keys(b["keys"])
         assert (ok == b["key_ok"].astype(bool)).all(), ml
-        bm = gv.verify(SigBatch(b["R"], b["S"], b["key_idx"], b["msg"], ml))
-        got = bitmap_to_bool(bm, len(b["R"]))
+        got, bm = verify(gv, b["R"], b["S"], b["key_idx"], b["msg"], ml)
         exp = b["expected"].astype(bool)
         bad = np.nonzero(got != exp)[0]
         assert len(bad) == 0, (ml, bad[:10], b["cls"][bad[:10]])
-        # bits past N are zero
         n = len(b["R"])
         if n % 64:
+            assert int(bm[-1]) >> (n % 64) == 0  # bits past N are zero
+
+
+def test_sign_matches_oracle(gv, coracle):
+    rng = np.random.default_rng(1)
+    for ml in (0, 1, 47, 85, 111, 200):
+        n = 300
+        seeds = rng.integers(0, 256, size=(17, 32), dtype=np.uint8)
+        idx = rng.integers(0, 17, size=n).astype(np.uint16)
+        stride = max(ml, 1)
+        msg = rng.integers(0, 256, size=(n, stride), dtype=np.uint8)
+        R, S, pub = gv.sign(seeds, idx, msg, ml)
+        oR = np.zeros_like(R)
+        oS = np.zeros_like(S)
+        buf = np.zeros(n * stride + 16, dtype=np.uint8)
+        buf[: n * stride] = msg.ravel()
+        assert coracle.oracle_sign_batch(seeds.ctypes.data, idx.ctypes.data, buf.ctypes.data, ml, stride, n,
+                                         oR.ctypes.data, oS.ctypes.data, 8) == 0
+        assert (R == oR).all() and (S == oS).all(), ml
+        for j in range(17):
+            pk = ctypes.create_string_buffer(32)
+            coracle.oracle_public_key(pk, seeds[j].tobytes())
+            assert pk.raw == pub[j].tobytes()
+
+
+def test_config3_round_with_adversarial(gv, coracle):
+    """n = 64 replicas (f = 21), 2^16 signatures, 1 % adversarial (BASELINE configs[2])."""
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 512, tag=3)
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(3)
+    R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
+    got, _ = verify(gv, R2, S2, K2, M2, 85)
+    exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert not got[idx].any() and got.sum() == len(R) - len(idx)
+
+
+def test_config4_full_size_properties(gv, coracle):
+    """2^20 signatures (BASELINE configs[3] round): size-independent properties + oracle checksum."""
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 256, 2048, tag=4)
+    assert gv.set_keys(pub).all()
+    got, bm = verify(gv, R, S, key_idx, msg, 85)
+    assert got.all()                                    # every honest signature accepted
+    rng = np.random.default_rng(4)
+    R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg, frac=0.001)
+    got2, bm2 = verify(gv, R2, S2, K2, M2, 85)
+    assert set(np.nonzero(~got2)[0].tolist()) == set(idx.tolist())   # exactly the mutated lanes
+    got3, bm3 = verify(gv, R2, S2, K2, M2, 85)
+    assert (bm3 == bm2).all()                           # idempotent
+    # the oracle agrees on a 2^14 slice containing mutated lanes
+    sl = slice(int(idx.min()) // 64 * 64, int(idx.min()) // 64 * 64 + 16384)
+    exp = oracle_bits(coracle, pub, R2[sl], S2[sl], K2[sl], M2[sl], 85)
+    assert (got2[sl] == exp).all()
+
+
+def test_api_edges_and_async(gv, coracle, golden):
+    from pbft_amd import SigBatch, bitmap_to_bool
+    b = dict(golden_batches(golden))[85]
+    gv.set_keys(b["keys"])
+    exp = b["expected"].astype(bool)
+    for n in (1, 2, 63, 64, 65, 127, 200):
+        got, bm = verify(gv, b["R"][:n], b["S"][:n], b["key_idx"][:n], b["msg"][:n], 85)
+        assert (got == exp[:n]).all(), n
+        assert len(bm) == (n + 63) // 64
+        if n % 64:
             assert int(bm[-1]) >> (n % 64) == 0
+    empty = gv.verify(SigBatch(b["R"][:0], b["S"][:0], b["key_idx"][:0], b["msg"][:0], 85))
+    assert len(empty) == 0
+    # async: submit, poll until done, equals sync
+    t = gv.submit(SigBatch(b["R"], b["S"], b["key_idx"], b["msg"], 85))
+    out = None
+    while out is None:
+        out = gv.poll(t)
+    assert (bitmap_to_bool(out, len(exp)) == exp).all()
+    # odd message stride (envelope embedded in wider records, unaligned)
+    n = len(exp)
+    wide = np.zeros((n, 93), dtype=np.uint8)
+    wide[:, 3:88] = b["msg"]
+    got, _ = verify(gv, b["R"], b["S"], b["key_idx"], wide[:, 3:].copy(), 85)
+    assert (got == exp).all()
+
+
+def test_device_entry_point(gv, golden):
+    import torch
+    from pbft_amd import bitmap_to_bool
+    b = dict(golden_batches(golden))[85]
+    gv.set_keys(b["keys"])
+    dev = torch.device("cuda", 0)
+    n = len(b["R"])
+    for stride in (85, 87, 128):
+        buf = np.zeros(n * stride + 64, dtype=np.uint8)
+        buf[: n * stride].reshape(n, stride)[:, :85] = b["msg"]
+        dR = torch.from_numpy(b["R"].copy()).to(dev)
+        dS = torch.from_numpy(b["S"].copy()).to(dev)
+        dK = torch.from_numpy(b["key_idx"].view(np.int16).copy()).to(dev)
+        dM = torch.from_numpy(buf).to(dev)
+        dB = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+        st = torch.cuda.Stream(dev)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(st):
+            gv.verify_device(dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(), 85, stride, n,
+                             dB.data_ptr(), st.cuda_stream)
+        st.synchronize()
+        got = bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n)
+        assert (got == b["expected"].astype(bool)).all(), stride
+        assert gv.last_kernel_ms() > 0
+
+
+def test_digests_match_hashlib(gv):
+    rng = random.Random(5)
+    items = [b"", b"abc", b"testOperation"] + [rng.randbytes(rng.choice([1, 55, 56, 63, 64, 65, 111, 112, 127, 128,
+                                                                          129, 255, 256, 1000]))
+                                                for _ in range(500)]
+    b2 = gv.blake2b512(items)
+    s2 = gv.sha256(items)
+    for i, it in enumerate(items):
+        assert b2[i].tobytes() == hashlib.blake2b(it, digest_size=64).digest(), (i, len(it))
+        assert s2[i].tobytes() == hashlib.sha256(it).digest(), (i, len(it))
+    # the reference README's request (README.md:42) digest, src/message.rs:209-212
+    assert b2[2].tobytes().hex() == KAT["digest"]["blake2b512_hex"]

@@ -1,0 +1,128 @@
+"""The product's __host__ __device__ arithmetic compiled for the host (tests/native/host_harness.cpp).
+
+These run without a GPU: the exact field / SHA-512 / Barrett / decompress /
+comb-table / verify_lane code that the HIP kernels execute is checked against
+the oracle, so arithmetic bugs are caught before a GPU run.  The GPU tests
+(test_gpu_*.py) then check the compiled gfx950 kernels bit-exactly.
+"""
+import ctypes
+import hashlib
+import os
+import random
+
+import numpy as np
+import pytest
+
+import ed25519_ref as E
+from conftest import ROOT, golden_batches
+
+P = E.P
+
+
+@pytest.fixture(scope="module")
+def hh():
+    path = os.path.join(ROOT, "tests", "native", "libhost_harness.so")
+    if not os.path.exists(path):
+        pytest.skip("host harness not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    lib.hh_build_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int, vp]
+    lib.hh_verify_batch.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32,
+                                    ctypes.c_uint32, ctypes.c_uint64, vp]
+    lib.hh_comb2.argtypes = [ctypes.c_int, vp, vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    return lib
+
+
+def _fe(hh, op, a, b):
+    out = ctypes.create_string_buffer(32)
+    hh.hh_fe_op(op, a.to_bytes(32, "little"), b.to_bytes(32, "little"), out)
+    return int.from_bytes(out.raw, "little")
+
+
+def test_field_ops(hh):
+    rnd = random.Random(7)
+    edge = [0, 1, 2, 18, 19, P - 1, P, P + 1, P + 18, 2**255 - 1, 2**255 - 2, 2**254, 2**26 - 1, 2**51]
+    vals = edge + [rnd.randrange(2**255) for _ in range(600)]
+    for i, a in enumerate(vals):
+        b = vals[(i * 7 + 3) % len(vals)]
+        assert _fe(hh, 0, a, b) == a * b % P
+        assert _fe(hh, 1, a, b) == a * a % P
+        assert _fe(hh, 4, a, b) == (a + b) ** 2 % P
+        assert _fe(hh, 5, a, b) == (a - b) * b % P
+        assert _fe(hh, 6, a, b) == (a + b) ** 2 % P
+    for a in vals[:60]:
+        assert _fe(hh, 2, a, 0) == pow(a, P - 2, P)
+        assert _fe(hh, 3, a, 0) == pow(a, (P - 5) // 8, P)
+
+
+@pytest.mark.parametrize("ln", [0, 1, 47, 48, 63, 64, 85, 111, 112, 175, 176, 239, 240, 300, 1023])
+def test_sha512_ram(hh, ln):
+    rnd = random.Random(ln)
+    r, a, m = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(ln)
+    buf = m + bytes(16)
+    out = ctypes.create_string_buffer(64)
+    hh.hh_sha512_ram(r, a, buf, ln, out)
+    assert out.raw == hashlib.sha512(r + a + m).digest()
+
+
+def test_reduce512(hh):
+    rnd = random.Random(11)
+    L = E.L
+    vals = [0, 1, L - 1, L, L + 1, 2 * L, 3 * L - 1, 2**512 - 1, 2**256, 2**253] + [rnd.randrange(2**512)
+                                                                                     for _ in range(3000)]
+    for x in vals:
+        out = ctypes.create_string_buffer(32)
+        hh.hh_reduce512(x.to_bytes(64, "little"), out)
+        assert int.from_bytes(out.raw, "little") == x % L
+
+
+def test_decompress(hh, golden):
+    rnd = random.Random(5)
+    import json
+    kat = json.load(open(os.path.join(ROOT, "tests", "golden", "kat.json")))
+    encs = [bytes.fromhex(h) for h in kat["small_order_encodings"] + kat["noncanonical_decodable_encodings"]]
+    encs += [rnd.randbytes(32) for _ in range(300)] + [E.compress(E.BASE)]
+    for enc in encs:
+        out = ctypes.create_string_buffer(32)
+        rc = hh.hh_decompress(enc, out)
+        p = E.decompress(enc)
+        if p is None:
+            assert rc == 0
+        else:
+            assert rc == (2 if E.is_small_order(p) else 1)
+            assert out.raw == E.compress(p)
+
+
+def test_comb_tables_and_mul(hh):
+    tb = np.zeros(hh.hh_table_words(4), dtype=np.uint32)
+    ta = np.zeros_like(tb)
+    assert hh.hh_build_table(4, E.compress(E.BASE), 0, tb.ctypes.data) == 1
+    A = E.pt_mul(987654321, E.BASE)
+    assert hh.hh_build_table(4, E.compress(A), 1, ta.ctypes.data) == 1
+    rnd = random.Random(9)
+    out = ctypes.create_string_buffer(32)
+    cases = [(0, 0), (1, 0), (0, 1), (8, 0), (0x88, 0x99), (E.L - 1, E.L - 1), (2**252, 3)]
+    cases += [(rnd.randrange(E.L), rnd.randrange(E.L)) for _ in range(20)]
+    for s, k in cases:
+        hh.hh_comb2(4, tb.ctypes.data, ta.ctypes.data, s.to_bytes(32, "little"), k.to_bytes(32, "little"), out)
+        assert out.raw == E.compress(E.pt_add(E.pt_mul(s, E.BASE), E.pt_mul(k, E.pt_neg(A)))), (s, k)
+
+
+def test_verify_lane_golden(hh, golden):
+    W = 4
+    tw = hh.hh_table_words(W)
+    tabB = np.zeros(tw, dtype=np.uint32)
+    assert hh.hh_build_table(W, E.compress(E.BASE), 0, tabB.ctypes.data) == 1
+    for ml, b in golden_batches(golden):
+        keys, kok = b["keys"], b["key_ok"]
+        tabA = np.zeros((len(keys), tw), dtype=np.uint32)
+        for i in range(len(keys)):
+            hh.hh_build_table(W, keys[i].tobytes(), 1, tabA[i].ctypes.data)
+        n, stride = len(b["R"]), b["msg"].shape[1]
+        mbuf = np.zeros(n * stride + 16, dtype=np.uint8)
+        mbuf[: n * stride] = b["msg"].ravel()
+        acc = np.zeros(n, dtype=np.uint8)
+        assert hh.hh_verify_batch(W, tabB.ctypes.data, tabA.ctypes.data, keys.ctypes.data, kok.ctypes.data, len(keys),
+                                  b["R"].ctypes.data, b["S"].ctypes.data, b["key_idx"].ctypes.data, mbuf.ctypes.data,
+                                  ml, stride, n, acc.ctypes.data) == 0
+        assert (acc == b["expected"]).all(), (ml, np.nonzero(acc != b["expected"])[0][:10])
