@@ -21,5 +21,5 @@ WA = 8
 _P = lambda w: (254 + w - 1) // w  # noqa: E731
 COMB_MADDS = _P(WB) + _P(WA)
 PRODUCTS_PER_VERIFY = COMB_MADDS * 7 * 100 + (254 * 55 + 11 * 100) + 2 * 100 + (81 + 44)
-VALU_MAD_PEAK_PER_S = 27.62e12
-VALU_OP_PEAK_PER_S = 35.9e12  # 32-bit VOP3 integer ops (v_add3_u32 / v_alignbit_b32), measured
+VALU_MAD_PEAK_PER_S = 30.25e12
+VALU_OP_PEAK_PER_S = 37.2e12  # 32-bit VOP3 integer ops (v_add3_u32 / v_alignbit_b32), measured
