@@ -85,6 +85,11 @@ int pbft_verify_batch_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d
                              const uint8_t *d_msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                              uint64_t *d_bitmap, void *stream);
 
+/* Pre-size the verify workspace (121 bytes of HBM per signature) for batches
+ * of up to max_n signatures, so that later launches allocate nothing (required
+ * before capturing pbft_verify_batch_device into a hipGraph). */
+int pbft_verify_reserve(pbft_ctx *ctx, uint64_t max_n);
+
 /* Request digests over N variable-length byte strings packed in `data`:
  * item i is data[offsets[i] .. offsets[i] + lens[i]).  out: N x 64 (Blake2b-512)
  * or N x 32 (SHA-256) bytes.  Blocking, host buffers. */

@@ -10,13 +10,13 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libpbft_verify.so")
+LIB_PATH = os.environ.get("PBFT_VERIFY_LIB") or os.path.join(_HERE, "libpbft_verify.so")  # override: A/B builds
 
 # every symbol include/pbft_verify.h declares
 EXPORTS = (
     "pbft_verify_ctx_create", "pbft_verify_ctx_destroy", "pbft_verify_set_keys",
     "pbft_verify_batch", "pbft_verify_batch_async", "pbft_verify_poll", "pbft_verify_wait",
-    "pbft_verify_batch_device", "pbft_digest_blake2b512", "pbft_digest_sha256",
+    "pbft_verify_batch_device", "pbft_verify_reserve", "pbft_digest_blake2b512", "pbft_digest_sha256",
     "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms",
 )
 
@@ -61,6 +61,7 @@ def load() -> ctypes.CDLL:
         "pbft_verify_poll": (i32, [vp]),
         "pbft_verify_wait": (i32, [vp]),
         "pbft_verify_batch_device": (i32, [vp, vp, vp, vp, vp, u32, u32, u64, vp, vp]),
+        "pbft_verify_reserve": (i32, [vp, u64]),
         "pbft_digest_blake2b512": (i32, [vp, u8p, vp, vp, u64, u8p]),
         "pbft_digest_sha256": (i32, [vp, u8p, vp, vp, u64, u8p]),
         "pbft_sign_batch": (i32, [vp, u8p, u32, vp, u8p, u32, u32, u64, u8p, u8p, u8p]),

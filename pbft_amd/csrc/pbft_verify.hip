@@ -14,6 +14,7 @@
 #include <string.h>
 
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/pbft_verify.h"
@@ -22,17 +23,18 @@
 
 using namespace pbft;
 
-#ifndef PBFT_WB
-#define PBFT_WB 8
-#endif
-#ifndef PBFT_WA
-#define PBFT_WA 8
-#endif
 #define PBFT_ENVELOPE_LEN 85
 #define BLOCK 256
 
-static constexpr int WB = PBFT_WB;
-static constexpr int WA = PBFT_WA;
+// Comb windows.  The base-point table uses 16-bit windows (16 positions x
+// 32769 entries x 128 B = 67 MB, resident in HBM and largely in the 256 MB
+// MALL).  Each replica key gets a 16-bit table too (67 MB/key) while the key
+// set fits PBFT_KEY_TABLE_BUDGET_MB (default 64 GiB of the 288 GB HBM), else
+// 8-bit tables (0.5 MB/key).  Fewer windows = fewer mixed additions: 16 + 16
+// instead of 32 + 32 ("Comb windows").
+static constexpr int WB = 16;
+static constexpr int WA_BIG = 16;
+static constexpr int WA_SMALL = 8;
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_last_error;
@@ -53,12 +55,38 @@ static int set_err(int code, const char* what) {
 
 // ------------------------------------------------------------------ kernels
 
-// Comb tables for a set of points given by encoding (negate: table of -P).
-// One thread per (key, position, entry).  key_ok[key] = decodes && !small order.
+// Comb tables for a set of points given by encoding (negate: tables of -P).
+// Pass 1, one thread per (key, position): decompress, key_ok, and the
+// position's base point 2^(W*pos) * (+-P) by W*pos doublings.
 template <int W>
-__global__ void __launch_bounds__(BLOCK) build_comb_kernel(const uint32_t* __restrict__ enc, uint32_t n_keys,
-                                                           int negate, uint32_t* __restrict__ tables,
-                                                           uint8_t* __restrict__ key_ok) {
+__global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __restrict__ enc, uint32_t n_keys,
+                                                          int negate, ge* __restrict__ bases,
+                                                          uint8_t* __restrict__ dec_ok, uint8_t* __restrict__ key_ok) {
+  constexpr int P = comb<W>::P;
+  const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= (uint64_t)P * n_keys) return;
+  const uint32_t key = (uint32_t)(tid / P);
+  const int pos = (int)(tid % P);
+  uint32_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
+  ge A;
+  const bool dec = ge_decompress(A, w);
+  if (pos == 0) {
+    dec_ok[key] = dec ? 1 : 0;
+    if (key_ok) key_ok[key] = (dec && !ge_is_small_order(A)) ? 1 : 0;
+  }
+  if (!dec) ge_identity(A);
+  if (negate) { ge t; ge_neg(t, A); A = t; }
+  for (int i = 0; i < W * pos; ++i) ge_dbl(A, A);
+  bases[tid] = A;
+}
+
+// Pass 2, one thread per (key, position, entry j): j * base in affine Niels form.
+template <int W>
+__global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict__ bases,
+                                                           const uint8_t* __restrict__ dec_ok, uint32_t n_keys,
+                                                           uint32_t* __restrict__ tables) {
   constexpr int P = comb<W>::P, E = comb<W>::E;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t per_key = (uint64_t)P * E;
@@ -66,20 +94,41 @@ __global__ void __launch_bounds__(BLOCK) build_comb_kernel(const uint32_t* __res
   const uint32_t key = (uint32_t)(tid / per_key);
   const uint32_t rem = (uint32_t)(tid % per_key);
   const int pos = rem / E, j = rem % E;
-  uint32_t w[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
-  ge A;
-  const bool dec = ge_decompress(A, w);
-  if (rem == 0 && key_ok) key_ok[key] = (dec && !ge_is_small_order(A)) ? 1 : 0;
   niels n;
-  if (!dec) {
+  if (j == 0 || !dec_ok[key]) {
     niels_identity(n);
   } else {
-    if (negate) { ge t; ge_neg(t, A); A = t; }
-    comb_entry<W>(n, A, pos, j);
+    const ge Q = bases[(size_t)key * P + pos];
+    ge acc = Q;
+    const int top = 31 - __builtin_clz((unsigned)j);
+    for (int b = top - 1; b >= 0; --b) {
+      ge_dbl(acc, acc);
+      if ((j >> b) & 1) { ge t; ge_add(t, acc, Q); acc = t; }
+    }
+    ge_to_niels(n, acc);
   }
   store_niels(tables + (size_t)key * comb<W>::TABLE_WORDS + (size_t)rem * 32, n);
+}
+
+template <int W>
+static int build_tables(const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables, uint8_t* d_key_ok,
+                        hipStream_t st) {
+  ge* d_bases = nullptr;
+  uint8_t* d_dec = nullptr;
+  HIP_TRY(hipMalloc(&d_bases, sizeof(ge) * (size_t)comb<W>::P * n));
+  HIP_TRY(hipMalloc(&d_dec, n));
+  const uint64_t t1 = (uint64_t)comb<W>::P * n;
+  hipLaunchKernelGGL(comb_base_kernel<W>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
+                     negate, d_bases, d_dec, d_key_ok);
+  HIP_TRY(hipGetLastError());
+  const uint64_t t2 = (uint64_t)comb<W>::P * comb<W>::E * n;
+  hipLaunchKernelGGL(comb_entry_kernel<W>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
+                     d_dec, n, d_tables);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(st));
+  HIP_TRY(hipFree(d_bases));
+  HIP_TRY(hipFree(d_dec));
+  return PBFT_OK;
 }
 
 __device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
@@ -89,17 +138,71 @@ __device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
   w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
 }
 
-// One signature per lane; wave ballot -> one bitmap word per wavefront.
-template <int LEN>
-__global__ void __launch_bounds__(BLOCK) verify_kernel(const uint8_t* __restrict__ R, const uint8_t* __restrict__ S,
-                                                       const uint16_t* __restrict__ key_idx,
-                                                       const uint8_t* __restrict__ msg, uint32_t msg_len,
-                                                       uint32_t msg_stride, uint64_t N,
-                                                       const uint32_t* __restrict__ tabB,
-                                                       const uint32_t* __restrict__ tabA,
-                                                       const uint32_t* __restrict__ keys,
-                                                       const uint8_t* __restrict__ key_ok, uint32_t n_keys,
-                                                       uint64_t* __restrict__ bitmap) {
+// ---- verify, device form ----------------------------------------------------
+// Same arithmetic as verify_lane (verify_core.h), split into two kernels by
+// register footprint:
+//
+//  comb_kernel   (one signature per lane, ~190 VGPRs)
+//    k = SHA-512(R || A || M) mod L; s < L; signed digits of s and k written to
+//    LDS in step order; R' = sum_i T_B[i][s_i] + T_{-A}[i][k_i] with every
+//    step's 128-B table entry fetched by LDS-DMA (global_load_lds_dwordx4,
+//    per-lane source address) one step AHEAD, so the random HBM/MALL gathers
+//    hide under the previous mixed addition.  Writes R' = (X:Y:Z) limb-major
+//    ([limb][N], coalesced) and one flag byte (s < L and key usable).
+//  finish_kernel (M = FIN_M signatures per lane, small footprint)
+//    Montgomery batch inversion of the M Z's (1 inversion + 3(M-1) muls
+//    instead of M inversions), affine x, y, canonical compare with R,
+//    small-order test on y, ballot -> one bitmap word per (wave, m).
+//
+// Step order of the comb: B_0, A_0, B_1, A_1, ... while both scalars have
+// positions, then the remaining positions of the longer one.
+typedef __attribute__((address_space(3))) void lds_void;
+#ifndef FIN_M
+#define FIN_M 16
+#endif
+#ifndef FIN_WAVES_PER_EU
+#define FIN_WAVES_PER_EU 1
+#endif
+
+template <int WB_, int WA_>
+struct steps {
+  static constexpr int PB = comb<WB_>::P, PA = comb<WA_>::P;
+  static constexpr int PMIN = PB < PA ? PB : PA;
+  static constexpr int N = PB + PA;
+  // table and position of step j (wave-uniform)
+  __device__ static __forceinline__ void at(int j, bool& isA, int& pos) {
+    if (j < 2 * PMIN) { isA = j & 1; pos = j >> 1; }
+    else { isA = PA > PB; pos = j - PMIN; }
+  }
+};
+
+__device__ __forceinline__ void dma_entry(const uint32_t* src, uint4* ebuf) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    __builtin_amdgcn_global_load_lds(src + 4 * q, (lds_void*)(ebuf + 64 * q), 16, 0, 0);
+}
+
+template <int WA_>
+constexpr size_t comb_lds_per_wave() {
+  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 128;
+}
+
+#ifndef PBFT_COMB_WAVES_PER_EU
+#define PBFT_COMB_WAVES_PER_EU 2
+#endif
+template <int LEN, int WA>
+__global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint16_t* __restrict__ key_idx,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags) {
+  using ST = steps<WB, WA>;
+  constexpr int EB = comb<WB>::E, EA = comb<WA>::E;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint8_t* wl = lds + (size_t)wave * comb_lds_per_wave<WA>();
+  uint4* ebuf = (uint4*)wl;
+  int16_t* dig = (int16_t*)(wl + 8 * 1024);
   const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < N;
   const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
@@ -110,13 +213,153 @@ __global__ void __launch_bounds__(BLOCK) verify_kernel(const uint8_t* __restrict
   bool kok = ki < n_keys;
   if (!kok) ki = 0;
   kok = kok && key_ok[ki];
-  const uint4* kp = (const uint4*)(keys + 8 * ki);
-  const uint4 k0 = kp[0], k1 = kp[1];
-  a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
-  const bool ok = verify_lane<WB, WA, LEN>(r, s, a, kok, msg + (size_t)msg_stride * ii, (int)msg_len, tabB,
-                                          tabA + (size_t)ki * comb<WA>::TABLE_WORDS);
-  const uint64_t vote = __ballot(live && ok);
-  if ((threadIdx.x & 63) == 0 && live) bitmap[i >> 6] = vote;
+  {
+    const uint4* kp = (const uint4*)(keys + 8 * ki);
+    const uint4 k0 = kp[0], k1 = kp[1];
+    a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+  }
+  const uint32_t* tA = tabA + (size_t)ki * comb<WA>::TABLE_WORDS;
+  const bool s_ok = sc_lt_L(s);
+  {
+    uint32_t h[16], k[8];
+    sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * ii, (int)msg_len);
+    sc_reduce512(k, h);
+    digit_stream<WB> ds;
+    ds.init(s);
+    digit_stream<WA> dk;
+    dk.init(k);
+    int j = 0;
+#pragma unroll
+    for (int p = 0; p < (ST::PB > ST::PA ? ST::PB : ST::PA); ++p) {
+      if (p < ST::PB) dig[(j++) * 64 + lane] = (int16_t)ds.next();
+      if (p < ST::PA) dig[(j++) * 64 + lane] = (int16_t)dk.next();
+    }
+  }
+  auto entry_ptr = [&](int j, int d) -> const uint32_t* {
+    bool isA;
+    int pos;
+    ST::at(j, isA, pos);
+    const int ad = d < 0 ? -d : d;
+    return isA ? tA + ((size_t)pos * EA + ad) * 32 : tabB + ((size_t)pos * EB + ad) * 32;
+  };
+  ge P;
+  ge_identity(P);
+  dma_entry(entry_ptr(0, dig[lane]), ebuf);
+  for (int j = 0; j < ST::N; ++j) {
+    const int d = dig[j * 64 + lane];
+    niels q;
+    {
+      uint32_t w[32];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 v = ebuf[64 * c + lane];
+        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+      }
+#pragma unroll
+      for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
+    }
+    if (j + 1 < ST::N) {
+      const int dn = dig[(j + 1) * 64 + lane];
+      // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      dma_entry(entry_ptr(j + 1, dn), ebuf);
+    }
+    ge_madd_signed(P, P, q, d < 0);
+  }
+  if (live) {
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      xyz[(size_t)t * N + i] = P.X.v[t];
+      xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
+      xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
+    }
+    flags[i] = (s_ok && kok) ? 1 : 0;
+  }
+}
+
+__device__ __forceinline__ void load_fe(fe& f, const uint32_t* __restrict__ base, uint64_t N, uint64_t i) {
+#pragma unroll
+  for (int t = 0; t < 10; ++t) f.v[t] = base[(size_t)t * N + i];
+}
+
+// Compile-time unrolled helpers (keep the prefix-product array in VGPRs: a
+// runtime-indexed array would be placed in scratch, cdna guide §5.4 rule 20).
+template <int M>
+struct fin_unroll {
+  template <class F>
+  __device__ static __forceinline__ void up(F&& f) {
+    fin_unroll<M - 1>::up(f);
+    f(std::integral_constant<int, M - 1>());
+  }
+  template <class F>
+  __device__ static __forceinline__ void down(F&& f) {
+    f(std::integral_constant<int, M - 1>());
+    fin_unroll<M - 1>::down(f);
+  }
+};
+template <>
+struct fin_unroll<0> {
+  template <class F>
+  __device__ static __forceinline__ void up(F&&) {}
+  template <class F>
+  __device__ static __forceinline__ void down(F&&) {}
+};
+
+// M signatures per lane: lane l of wave w handles i = (w * M + m) * 64 + l.
+__global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const uint8_t* __restrict__ R,
+                                                       const uint32_t* __restrict__ xyz,
+                                                       const uint8_t* __restrict__ flags, uint64_t N,
+                                                       uint64_t* __restrict__ bitmap) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  const uint64_t base = wave * FIN_M * 64 + lane;
+  if (wave * FIN_M * 64 >= N) return;
+  const uint32_t* Xb = xyz;
+  const uint32_t* Yb = xyz + 10 * N;
+  const uint32_t* Zb = xyz + 20 * N;
+  // prefix products of Z (lanes past N contribute 1)
+  fe pre[FIN_M];
+  fin_unroll<FIN_M>::up([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    const uint64_t i = base + (uint64_t)m * 64;
+    fe z;
+    if (i < N) load_fe(z, Zb, N, i); else fe_one(z);
+    if constexpr (m == 0) pre[0] = z;
+    else fe_mul(pre[m], pre[m - 1], z);
+  });
+  fe inv;
+  fe_invert(inv, pre[FIN_M - 1]);
+  fin_unroll<FIN_M>::down([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    const uint64_t i = base + (uint64_t)m * 64;
+    const bool live = i < N;
+    const uint64_t ii = live ? i : 0;
+    fe zi;
+    if constexpr (m > 0) {
+      fe_mul(zi, inv, pre[m - 1]);   // 1 / Z_m
+      fe z;
+      if (live) load_fe(z, Zb, N, ii); else fe_one(z);
+      fe_mul(inv, inv, z);           // 1 / (Z_0 ... Z_{m-1})
+    } else {
+      zi = inv;
+    }
+    fe X, Y, x, y;
+    load_fe(X, Xb, N, ii);
+    load_fe(Y, Yb, N, ii);
+    fe_mul(x, X, zi);
+    fe_mul(y, Y, zi);
+    uint32_t xw[8], yw[8], r[8], ry[8];
+    fe_to_words(xw, x);
+    fe_to_words(yw, y);
+    load32(r, R + 32 * ii);
+    canon_y(ry, r);
+    bool eq = (xw[0] & 1u) == (r[7] >> 31);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) eq = eq && yw[t] == ry[t];
+    const bool ok = live && flags[ii] && eq && !y_is_small_order(yw);
+    const uint64_t vote = __ballot(ok);
+    if (lane == 0 && live) bitmap[(wave * FIN_M + m)] = vote;
+  });
 }
 
 // RFC 8032 signing, one signature per lane (replicas sign their own
@@ -176,11 +419,15 @@ struct pbft_ctx {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
+  int wa = 0;  // comb window of the installed key tables (WA_BIG or WA_SMALL)
   // staging for the host-buffer API
   uint8_t* d_stage = nullptr;
   size_t stage_cap = 0;
   uint64_t* d_bitmap = nullptr;
   size_t bitmap_cap = 0;
+  // verify workspace: R' limbs [30][N] u32 + flags[N]
+  uint8_t* d_work = nullptr;
+  size_t work_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
   bool in_flight = false;
   uint64_t* async_out = nullptr;
@@ -210,18 +457,47 @@ static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
   return PBFT_OK;
 }
 
+// Grow the verify workspace (never inside a stream capture: call
+// pbft_verify_reserve first when capturing launches into a graph).
+static int ensure_work(pbft_ctx* c, uint64_t N) {
+  const size_t need = 121 * (size_t)N + 256;
+  if (need <= c->work_cap) return PBFT_OK;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->d_work) HIP_TRY(hipFree(c->d_work));
+  c->d_work = nullptr;
+  c->work_cap = 0;
+  if (hipMalloc(&c->d_work, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
+  c->work_cap = need;
+  return PBFT_OK;
+}
+
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
+  int rc = ensure_work(c, N);
+  if (rc) return rc;
   HIP_TRY(hipEventRecord(c->ev0, st));
-  if (msg_len == PBFT_ENVELOPE_LEN)
-    hipLaunchKernelGGL(verify_kernel<PBFT_ENVELOPE_LEN>, dim3((unsigned)blocks), dim3(BLOCK), 0, st, dR, dS, dK, dM,
-                       msg_len, msg_stride, N, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, dB);
-  else
-    hipLaunchKernelGGL(verify_kernel<-1>, dim3((unsigned)blocks), dim3(BLOCK), 0, st, dR, dS, dK, dM, msg_len,
-                       msg_stride, N, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, dB);
+  const dim3 g((unsigned)blocks), b(BLOCK);
+  uint32_t* xyz = (uint32_t*)c->d_work;
+  uint8_t* flags = c->d_work + 120 * N;
+#define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                          \
+  hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * comb_lds_per_wave<WA_>(), st, dR, dS, dK, \
+                     dM, msg_len, msg_stride, N, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz,  \
+                     flags)
+  if (msg_len == PBFT_ENVELOPE_LEN) {
+    if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
+    else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
+  } else {
+    if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(-1, WA_BIG);
+    else PBFT_LAUNCH_COMB(-1, WA_SMALL);
+  }
+#undef PBFT_LAUNCH_COMB
+  HIP_TRY(hipGetLastError());
+  const uint64_t fin_waves = (N + 64 * FIN_M - 1) / (64 * FIN_M);
+  const uint64_t fin_blocks = (fin_waves * 64 + BLOCK - 1) / BLOCK;
+  hipLaunchKernelGGL(finish_kernel, dim3((unsigned)fin_blocks), dim3(BLOCK), 0, st, dR, xyz, flags, N, dB);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   return PBFT_OK;
@@ -261,8 +537,10 @@ const char* pbft_last_error(void) { return g_last_error.c_str(); }
 
 const char* pbft_build_info(void) {
   static char buf[160];
-  snprintf(buf, sizeof buf, "pbft_verify gfx950 WB=%d WA=%d block=%d entry=128B tabB=%zuB tabA/key=%zuB", WB, WA,
-           BLOCK, comb<WB>::TABLE_WORDS * 4, comb<WA>::TABLE_WORDS * 4);
+  snprintf(buf, sizeof buf,
+           "pbft_verify gfx950 WB=%d WA=%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB", WB, WA_BIG,
+           WA_SMALL, BLOCK, comb<WB>::TABLE_WORDS * 4, comb<WA_BIG>::TABLE_WORDS * 4,
+           comb<WA_SMALL>::TABLE_WORDS * 4);
   return buf;
 }
 
@@ -293,11 +571,8 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipMalloc(&d_benc, 32));
   HIP_TRY(hipMalloc(&c->d_tabB, comb<WB>::TABLE_WORDS * 4));
   HIP_TRY(hipMemcpyAsync(d_benc, benc, 32, hipMemcpyHostToDevice, c->stream));
-  const uint64_t threads = (uint64_t)comb<WB>::P * comb<WB>::E;
-  hipLaunchKernelGGL(build_comb_kernel<WB>, dim3((unsigned)((threads + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                     c->stream, d_benc, 1u, 0, c->d_tabB, (uint8_t*)nullptr);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  int rc = build_tables<WB>(d_benc, 1u, 0, c->d_tabB, nullptr, c->stream);
+  if (rc) return rc;
   HIP_TRY(hipFree(d_benc));
   *out = c;
   return PBFT_OK;
@@ -305,15 +580,16 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
 
 int pbft_verify_ctx_destroy(pbft_ctx* c) {
   if (!c) return PBFT_OK;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  hipFree(c->d_tabB); hipFree(c->d_tabA); hipFree(c->d_keys); hipFree(c->d_key_ok);
-  hipFree(c->d_stage); hipFree(c->d_bitmap);
-  if (c->h_bitmap) hipHostFree(c->h_bitmap);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
-  if (c->ev_done) hipEventDestroy(c->ev_done);
-  if (c->stream) hipStreamDestroy(c->stream);
+  // teardown: errors are ignored (nothing useful to report from a destructor)
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(c->d_tabB); (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
+  (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work);
+  if (c->h_bitmap) (void)hipHostFree(c->h_bitmap);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
+  if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PBFT_OK;
 }
@@ -324,17 +600,25 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  hipFree(c->d_tabA); hipFree(c->d_keys); hipFree(c->d_key_ok);
+  (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
   c->d_tabA = nullptr; c->d_keys = nullptr; c->d_key_ok = nullptr; c->n_keys = 0;
-  const size_t tab_bytes = comb<WA>::TABLE_WORDS * 4 * (size_t)n;
+  // 16-bit key windows while the key set fits the budget, else 8-bit
+  size_t budget_mb = 65536;
+  if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
+  size_t free_b = 0, total_b = 0;
+  HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  const size_t big = comb<WA_BIG>::TABLE_WORDS * 4 * (size_t)n;
+  const bool use_big = big <= budget_mb * (size_t)1048576 && big + ((size_t)4 << 30) < free_b;
+  const int wa = use_big ? WA_BIG : WA_SMALL;
+  const size_t tab_bytes = (use_big ? comb<WA_BIG>::TABLE_WORDS : comb<WA_SMALL>::TABLE_WORDS) * 4 * (size_t)n;
   if (hipMalloc(&c->d_tabA, tab_bytes) != hipSuccess) return set_err(PBFT_ENOMEM, "key table alloc");
   HIP_TRY(hipMalloc(&c->d_keys, 32 * (size_t)n));
   HIP_TRY(hipMalloc(&c->d_key_ok, n));
   HIP_TRY(hipMemcpyAsync(c->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  const uint64_t threads = (uint64_t)comb<WA>::P * comb<WA>::E * n;
-  hipLaunchKernelGGL(build_comb_kernel<WA>, dim3((unsigned)((threads + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
-                     c->stream, c->d_keys, n, 1, c->d_tabA, c->d_key_ok);
-  HIP_TRY(hipGetLastError());
+  int rc = use_big ? build_tables<WA_BIG>(c->d_keys, n, 1, c->d_tabA, c->d_key_ok, c->stream)
+                   : build_tables<WA_SMALL>(c->d_keys, n, 1, c->d_tabA, c->d_key_ok, c->stream);
+  if (rc) return rc;
+  c->wa = wa;
   if (key_ok) HIP_TRY(hipMemcpyAsync(key_ok, c->d_key_ok, n, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->n_keys = n;
@@ -370,7 +654,7 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
 static int finish_async(pbft_ctx* c) {
   memcpy(c->async_out, c->h_bitmap, c->async_words * 8);
   c->in_flight = false;
-  hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+  (void)hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
   return PBFT_OK;
 }
 
@@ -504,10 +788,16 @@ int pbft_sign_batch(pbft_ctx* c, const uint8_t* seeds, uint32_t n_seeds, const u
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(pub, c->d_stage + offP, 32 * (size_t)n_seeds, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    hipFree(d_i2);
-    hipFree(d_r2);
+    (void)hipFree(d_i2);
+    (void)hipFree(d_r2);
   }
   return PBFT_OK;
+}
+
+int pbft_verify_reserve(pbft_ctx* c, uint64_t max_n) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  HIP_TRY(hipSetDevice(c->device));
+  return ensure_work(c, max_n);
 }
 
 float pbft_last_kernel_ms(pbft_ctx* c) {

@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of verify_kernel builds in ONE process (cdna guide §5.4 rule 24).
+
+usage: python tools/ab.py lib1.so lib2.so ... [--rounds 8 --iters 10 --budget-mb X]
+Each lib gets its own context on the same synthetic 2^20-signature round.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--replicas", type=int, default=256)
+    ap.add_argument("--seqs", type=int, default=2048)
+    a = ap.parse_args()
+    import torch
+    import bench
+    from pbft_amd import GpuBatchVerifier, bitmap_to_bool
+    torch.cuda.set_device(0)
+    seeds = bench.key_seeds(a.replicas)
+    msg, key_idx = bench.envelopes(1, a.seqs, a.replicas)
+    n = len(msg)
+    v0 = GpuBatchVerifier(0)
+    R, S, pub = v0.sign(seeds, key_idx, msg, 85)
+    v0.close()
+    dev = torch.device("cuda", 0)
+    dR, dS = torch.from_numpy(R).to(dev), torch.from_numpy(S).to(dev)
+    dK = torch.from_numpy(key_idx.view(np.int16)).to(dev)
+    mp = np.zeros(n * 85 + 64, dtype=np.uint8)
+    mp[: n * 85] = msg.reshape(-1)
+    dM = torch.from_numpy(mp).to(dev)
+    dB = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    st = torch.cuda.Stream(dev)
+    ctxs = []
+    for p in a.libs:
+        lib = ctypes.CDLL(os.path.abspath(p))
+        vp = ctypes.c_void_p
+        lib.pbft_verify_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        lib.pbft_verify_set_keys.argtypes = [vp, vp, ctypes.c_uint32, vp]
+        lib.pbft_verify_batch_device.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                                 ctypes.c_uint64, vp, vp]
+        lib.pbft_build_info.restype = ctypes.c_char_p
+        c = vp()
+        assert lib.pbft_verify_ctx_create(0, ctypes.byref(c)) == 0
+        ok = np.zeros(len(pub), np.uint8)
+        assert lib.pbft_verify_set_keys(c, pub.ctypes.data, len(pub), ok.ctypes.data) == 0
+        ctxs.append((p, lib, c))
+    res = {p: [] for p in a.libs}
+    for r in range(a.rounds):
+        for p, lib, c in ctxs:
+            dB.zero_()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.iters):
+                assert lib.pbft_verify_batch_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(),
+                                                    85, 85, n, dB.data_ptr(), st.cuda_stream) == 0
+            e1.record(st)
+            st.synchronize()
+            res[p].append(e0.elapsed_time(e1) / a.iters)
+            if "abl" not in os.path.basename(p):
+                assert bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n).all(), p
+    for p, lib, c in ctxs:
+        t = np.array(res[p])
+        print(f"{os.path.basename(p):32s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
+              f"-> {n / np.median(t) * 1e3 / 1e6:.1f} M verifies/s   [{lib.pbft_build_info().decode()}]")
+
+
+if __name__ == "__main__":
+    main()

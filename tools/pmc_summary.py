@@ -12,10 +12,11 @@ import sys
 d = sys.argv[1]
 n = int(sys.argv[2]) if len(sys.argv) > 2 else 1 << 20
 ms = float(sys.argv[3]) if len(sys.argv) > 3 else None
+KERNEL = os.environ.get("KERNEL", "comb_kernel")
 vals = collections.defaultdict(list)
 for f in sorted(glob.glob(os.path.join(d, "*.csv"))):
     for r in csv.DictReader(open(f)):
-        if "verify_kernel" in r.get("Kernel_Name", ""):
+        if KERNEL in r.get("Kernel_Name", ""):
             vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
 m = {k: sum(v) / len(v) for k, v in vals.items()}
 out = []
