@@ -120,6 +120,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
+    from pbft_amd.dist import allgather_bitmap
     from pbft_amd.roofline import PRODUCTS_PER_VERIFY, VALU_MAD_PEAK_PER_S
 
     n_rep, n_seq = args.replicas, args.seqs
@@ -155,7 +156,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if ws > 1:
-            dist.all_gather_into_tensor(d_all, d_B)
+            allgather_bitmap(d_B, ws, d_all)
 
     for _ in range(args.warmup):
         step()
@@ -221,7 +222,7 @@ def main():
                        "parallelism": f"shard-by-index x{ws}" + (" + RCCL all-gather of bitmaps" if ws > 1 else "")},
             "roofline": {"bound": "valu", "achieved": products / 1e12, "peak": VALU_MAD_PEAK_PER_S / 1e12,
                          "unit": "T products/s (v_mad_u64_u32)", "frac": products / VALU_MAD_PEAK_PER_S,
-                         "traffic": None, "kernel": "verify_kernel<85>", "kernel_avg_ms": kern_avg,
+                         "traffic": None, "kernel": "comb_kernel<85,16> + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
                          "products_per_verify": PRODUCTS_PER_VERIFY},
             "p50_ms_4k_round": float(np.median(lat)) if lat else None,
             "p99_ms_4k_round": float(np.percentile(lat, 99)) if lat else None,

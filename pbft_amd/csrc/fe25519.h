@@ -87,6 +87,41 @@ FE_FN void fe_reduce_wide(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t
   h.v[8] = (uint32_t)h8; h.v[9] = (uint32_t)h9;
 }
 
+#ifndef PBFT_FE_MUL_COLUMN_ORDER
+// Operand-scanning order: the 10 column accumulators are updated round-robin,
+// so consecutive v_mad_u64_u32 never depend on each other (10-way ILP per lane;
+// the dependent-mad latency is ~17 cycles on gfx950, tools/microbench/mad_latency.hip).
+FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
+  uint32_t g19[10], fx[10];
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    g19[i] = 19u * g.v[i];
+    fx[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+  }
+  uint64_t acc[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) acc[k] = MUL64(f.v[0], g.v[k]);
+#pragma unroll
+  for (int i = 1; i < 10; ++i) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+      const int j = k - i;  // g index; j < 0 wraps with x19
+      // odd*odd limb products carry an extra factor 2 (radix 2^25.5)
+      const uint32_t fi = ((i & 1) && (j & 1)) ? fx[i] : f.v[i];
+      const uint32_t gj = j >= 0 ? g.v[j] : g19[j + 10];
+#if defined(__HIP_DEVICE_COMPILE__) && defined(PBFT_ASM_MAD)
+      // issue order pinned: the machine scheduler otherwise regroups the mads
+      // into 4-5 dependent chains
+      uint64_t cc;
+      asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[k]), "=s"(cc) : "v"(fi), "v"(gj));
+#else
+      acc[k] += MUL64(fi, gj);
+#endif
+    }
+  }
+  fe_reduce_wide(h, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], acc[8], acc[9]);
+}
+#else
 FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
@@ -118,6 +153,8 @@ FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
                 MUL64(f5, g4) + MUL64(f6, g3) + MUL64(f7, g2) + MUL64(f8, g1) + MUL64(f9, g0);
   fe_reduce_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
 }
+
+#endif
 
 FE_FN void fe_sq(fe& h, const fe& f) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
