@@ -32,7 +32,10 @@ using namespace pbft;
 // set fits PBFT_KEY_TABLE_BUDGET_MB (default 64 GiB of the 288 GB HBM), else
 // 8-bit tables (0.5 MB/key).  Fewer windows = fewer mixed additions: 16 + 16
 // instead of 32 + 32 ("Comb windows").
-static constexpr int WB = 16;
+#ifndef PBFT_WB
+#define PBFT_WB 16
+#endif
+static constexpr int WB = PBFT_WB;
 static constexpr int WA_BIG = 16;
 static constexpr int WA_SMALL = 8;
 
@@ -82,32 +85,75 @@ __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __rest
   bases[tid] = A;
 }
 
-// Pass 2, one thread per (key, position, entry j): j * base in affine Niels form.
+// Pass 2, one thread per (key, position, run of TAB_RUN consecutive entries):
+// j0 * base by double-and-add, then each next entry by one addition of base;
+// the run's TAB_RUN Z coordinates are inverted together (Montgomery's trick:
+// 1 inversion + 3 muls each), so an entry costs ~15 field multiplications
+// instead of one inversion (~265).  Entry 0 of every position is the identity.
+#define TAB_RUN 16
 template <int W>
 __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict__ bases,
                                                            const uint8_t* __restrict__ dec_ok, uint32_t n_keys,
                                                            uint32_t* __restrict__ tables) {
   constexpr int P = comb<W>::P, E = comb<W>::E;
+  constexpr uint32_t RUNS = ((1u << (W - 1)) + TAB_RUN - 1) / TAB_RUN;  // entries 1 .. 2^(W-1)
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t per_key = (uint64_t)P * E;
+  const uint64_t per_key = (uint64_t)P * RUNS;
   if (tid >= per_key * n_keys) return;
   const uint32_t key = (uint32_t)(tid / per_key);
   const uint32_t rem = (uint32_t)(tid % per_key);
-  const int pos = rem / E, j = rem % E;
-  niels n;
-  if (j == 0 || !dec_ok[key]) {
-    niels_identity(n);
-  } else {
-    const ge Q = bases[(size_t)key * P + pos];
-    ge acc = Q;
-    const int top = 31 - __builtin_clz((unsigned)j);
-    for (int b = top - 1; b >= 0; --b) {
-      ge_dbl(acc, acc);
-      if ((j >> b) & 1) { ge t; ge_add(t, acc, Q); acc = t; }
-    }
-    ge_to_niels(n, acc);
+  const int pos = rem / RUNS;
+  const uint32_t run = rem % RUNS;
+  uint32_t* out = tables + (size_t)key * comb<W>::TABLE_WORDS + (size_t)pos * E * 32;
+  if (run == 0) {
+    niels id;
+    niels_identity(id);
+    store_niels(out, id);
   }
-  store_niels(tables + (size_t)key * comb<W>::TABLE_WORDS + (size_t)rem * 32, n);
+  const uint32_t j0 = 1 + run * TAB_RUN;
+  const uint32_t cnt = min((uint32_t)TAB_RUN, (1u << (W - 1)) + 1 - j0);
+  if (!dec_ok[key]) {
+    niels id;
+    niels_identity(id);
+    for (uint32_t t = 0; t < cnt; ++t) store_niels(out + (size_t)(j0 + t) * 32, id);
+    return;
+  }
+  const ge Q = bases[(size_t)key * P + pos];
+  // acc = j0 * Q
+  ge acc = Q;
+  const int top = 31 - __builtin_clz(j0);
+  for (int bb = top - 1; bb >= 0; --bb) {
+    ge_dbl(acc, acc);
+    if ((j0 >> bb) & 1) { ge t; ge_add(t, acc, Q); acc = t; }
+  }
+  // the run's points (private arrays: scratch is fine for a one-time build)
+  fe X[TAB_RUN], Y[TAB_RUN], Z[TAB_RUN], pre[TAB_RUN];
+  for (uint32_t t = 0; t < cnt; ++t) {
+    X[t] = acc.X; Y[t] = acc.Y; Z[t] = acc.Z;
+    if (t == 0) pre[0] = acc.Z; else fe_mul(pre[t], pre[t - 1], acc.Z);
+    if (t + 1 < cnt) { ge nx; ge_add(nx, acc, Q); acc = nx; }
+  }
+  fe inv;
+  fe_invert(inv, pre[cnt - 1]);
+  fe k2d;
+  fe_const_2d(k2d);
+  for (int t = (int)cnt - 1; t >= 0; --t) {
+    fe zi;
+    if (t > 0) { fe_mul(zi, inv, pre[t - 1]); fe_mul(inv, inv, Z[t]); } else { zi = inv; }
+    fe x, y;
+    fe_mul(x, X[t], zi);
+    fe_mul(y, Y[t], zi);
+    niels n;
+    fe_add(n.ypx, y, x);
+    fe_sub(n.ymx, y, x);
+    fe_mul(n.xy2d, x, y);
+    fe_mul(n.xy2d, n.xy2d, k2d);
+    uint32_t w[8];
+    fe_to_words(w, n.ypx); fe_from_words(n.ypx, w);
+    fe_to_words(w, n.ymx); fe_from_words(n.ymx, w);
+    fe_to_words(w, n.xy2d); fe_from_words(n.xy2d, w);
+    store_niels(out + (size_t)(j0 + t) * 32, n);
+  }
 }
 
 template <int W>
@@ -121,7 +167,7 @@ static int build_tables(const uint32_t* d_enc, uint32_t n, int negate, uint32_t*
   hipLaunchKernelGGL(comb_base_kernel<W>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
                      negate, d_bases, d_dec, d_key_ok);
   HIP_TRY(hipGetLastError());
-  const uint64_t t2 = (uint64_t)comb<W>::P * comb<W>::E * n;
+  const uint64_t t2 = (uint64_t)comb<W>::P * (((1u << (W - 1)) + TAB_RUN - 1) / TAB_RUN) * n;
   hipLaunchKernelGGL(comb_entry_kernel<W>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
                      d_dec, n, d_tables);
   HIP_TRY(hipGetLastError());
@@ -184,7 +230,7 @@ __device__ __forceinline__ void dma_entry(const uint32_t* src, uint4* ebuf) {
 
 template <int WA_>
 constexpr size_t comb_lds_per_wave() {
-  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 128;
+  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 256;
 }
 
 #ifndef PBFT_COMB_WAVES_PER_EU
@@ -202,7 +248,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* wl = lds + (size_t)wave * comb_lds_per_wave<WA>();
   uint4* ebuf = (uint4*)wl;
-  int16_t* dig = (int16_t*)(wl + 8 * 1024);
+  int32_t* dig = (int32_t*)(wl + 8 * 1024);
   const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < N;
   const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
@@ -231,8 +277,8 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     int j = 0;
 #pragma unroll
     for (int p = 0; p < (ST::PB > ST::PA ? ST::PB : ST::PA); ++p) {
-      if (p < ST::PB) dig[(j++) * 64 + lane] = (int16_t)ds.next();
-      if (p < ST::PA) dig[(j++) * 64 + lane] = (int16_t)dk.next();
+      if (p < ST::PB) dig[(j++) * 64 + lane] = ds.next();
+      if (p < ST::PA) dig[(j++) * 64 + lane] = dk.next();
     }
   }
   auto entry_ptr = [&](int j, int d) -> const uint32_t* {

@@ -8,7 +8,24 @@
 
 namespace pbft {
 
-__host__ __device__ __forceinline__ uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate: two v_alignbit_b32 on gfx950 (the generic form lowers to
+// 2 x 64-bit shifts + 2 ORs).  n is a compile-time constant at every call site.
+__host__ __device__ __forceinline__ uint64_t ror64(uint64_t x, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t nlo, nhi;
+  if (n < 32) {
+    nlo = __builtin_amdgcn_alignbit(hi, lo, n);
+    nhi = __builtin_amdgcn_alignbit(lo, hi, n);
+  } else {
+    nlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+    nhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+  }
+  return ((uint64_t)nhi << 32) | nlo;
+#else
+  return (x >> n) | (x << (64 - n));
+#endif
+}
 __host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
 }
@@ -41,29 +58,45 @@ __host__ __device__ __forceinline__ void sha512_init(uint64_t H[8]) {
   H[6] = 0x1f83d9abfb41bd6bULL; H[7] = 0x5be0cd19137e2179ULL;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+__constant__ static const uint64_t SHA512_K[80] = SHA512_K_TABLE;
+#endif
+
 // One compression; W holds the 16 big-endian message words of the block.
+// The 80 rounds run as 5 iterations of a 16-round unrolled body: the message
+// schedule indices (t mod 16) and the a..h renaming (16 = 0 mod 8) stay
+// compile-time constants while the code stays ~5x smaller than a full unroll
+// (instruction-cache footprint); K[t] is a wave-uniform scalar load.
+__host__ __device__ __forceinline__ void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
+                                                      uint64_t& e, uint64_t& f, uint64_t& g, uint64_t& h,
+                                                      uint64_t k, uint64_t w) {
+  const uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
+  const uint64_t ch = (e & f) ^ (~e & g);
+  const uint64_t T1 = h + S1 + ch + k + w;
+  const uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
+  const uint64_t mj = (a & b) ^ (c & (a ^ b));
+  h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
+}
+
 __host__ __device__ __forceinline__ void sha512_compress(uint64_t H[8], uint64_t W[16]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t* K = SHA512_K;
+#else
   const uint64_t K[80] = SHA512_K_TABLE;
+#endif
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
 #pragma unroll
-  for (int t = 0; t < 80; ++t) {
-    uint64_t w;
-    if (t < 16) {
-      w = W[t];
-    } else {
-      const uint64_t w15 = W[(t - 15) & 15], w2 = W[(t - 2) & 15];
+  for (int j = 0; j < 16; ++j) sha512_round(a, b, c, d, e, f, g, h, K[j], W[j]);
+#pragma nounroll
+  for (int t0 = 16; t0 < 80; t0 += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
       const uint64_t s0 = ror64(w15, 1) ^ ror64(w15, 8) ^ (w15 >> 7);
       const uint64_t s1 = ror64(w2, 19) ^ ror64(w2, 61) ^ (w2 >> 6);
-      w = W[t & 15] + s0 + W[(t - 7) & 15] + s1;
-      W[t & 15] = w;
+      W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+      sha512_round(a, b, c, d, e, f, g, h, K[t0 + j], W[j]);
     }
-    const uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
-    const uint64_t ch = (e & f) ^ (~e & g);
-    const uint64_t T1 = h + S1 + ch + K[t] + w;
-    const uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
-    const uint64_t mj = (a & b) ^ (c & (a ^ b));
-    const uint64_t T2 = S0 + mj;
-    h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + T2;
   }
   H[0] += a; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
 }
