@@ -228,9 +228,43 @@ __device__ __forceinline__ void dma_entry(const uint32_t* src, uint4* ebuf) {
     __builtin_amdgcn_global_load_lds(src + 4 * q, (lds_void*)(ebuf + 64 * q), 16, 0, 0);
 }
 
+// Line-coalesced gather ("transposed" DMA).  A table entry is one 128-B line.
+// Lane-per-entry DMA (dma_entry above) makes every wave-instruction touch 64
+// different lines with 16 B each, the access shape the memory pipeline serves
+// worst; here instruction i fetches the 8 entries of lanes 8i..8i+7 WHOLE: lane
+// L reads 16-B chunk c = (L & 7) ^ (L >> 3) of the entry of lane 8i + (L >> 3),
+// so each instruction covers 8 full lines.  The DMA lands lane L of instruction
+// i at LDS byte 1024 i + 16 L, i.e. entry e occupies bytes [128 e, 128 e + 128)
+// with chunk c at position c ^ (e & 7) -- the XOR swizzle spreads the owner
+// lanes' ds_read_b128 over all banks.  idx is the entry index in 128-B units
+// from `base` (the entry's owner lane holds it; 8 ds_bpermute per step).
+__device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t idx, int lane, uint8_t* ebuf) {
+  const int k = lane >> 3;
+  const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t e = (uint32_t)__shfl((int)idx, 8 * q + k);
+    __builtin_amdgcn_global_load_lds(base + (size_t)e * 128 + coff, (lds_void*)(ebuf + 1024 * q), 16, 0, 0);
+  }
+}
+#ifndef PBFT_LINE_DMA
+#define PBFT_LINE_DMA 1
+#endif
+
+// Signed comb digits live in LDS in step order.  For W <= 16 a digit is in
+// [-2^(W-1), 2^(W-1) - 1] and fits int16 (halves the per-wave LDS: 8 KB entry
+// buffer + 4 KB digits, so LDS no longer caps occupancy below the VGPR limit).
+#ifndef PBFT_LAUNDER
+#define PBFT_LAUNDER 1
+#endif
+#ifndef PBFT_DIG16
+#define PBFT_DIG16 1
+#endif
+template <int WA_>
+using dig_t = typename std::conditional<(PBFT_DIG16 && WB <= 16 && WA_ <= 16), int16_t, int32_t>::type;
 template <int WA_>
 constexpr size_t comb_lds_per_wave() {
-  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 256;
+  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 64 * sizeof(dig_t<WA_>);
 }
 
 #ifndef PBFT_COMB_WAVES_PER_EU
@@ -248,7 +282,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   uint8_t* wl = lds + (size_t)wave * comb_lds_per_wave<WA>();
   uint4* ebuf = (uint4*)wl;
-  int32_t* dig = (int32_t*)(wl + 8 * 1024);
+  dig_t<WA>* dig = (dig_t<WA>*)(wl + 8 * 1024);
   const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   const bool live = i < N;
   const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
@@ -264,7 +298,9 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint4 k0 = kp[0], k1 = kp[1];
     a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
   }
+#if !PBFT_LINE_DMA
   const uint32_t* tA = tabA + (size_t)ki * comb<WA>::TABLE_WORDS;
+#endif
   const bool s_ok = sc_lt_L(s);
   {
     uint32_t h[16], k[8];
@@ -277,10 +313,56 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     int j = 0;
 #pragma unroll
     for (int p = 0; p < (ST::PB > ST::PA ? ST::PB : ST::PA); ++p) {
-      if (p < ST::PB) dig[(j++) * 64 + lane] = ds.next();
-      if (p < ST::PA) dig[(j++) * 64 + lane] = dk.next();
+      if (p < ST::PB) dig[(j++) * 64 + lane] = (dig_t<WA>)ds.next();
+      if (p < ST::PA) dig[(j++) * 64 + lane] = (dig_t<WA>)dk.next();
     }
   }
+#if PBFT_LINE_DMA
+  // entry index of step j in 128-B units from the step's (wave-uniform) table base
+  const uint32_t keybase = ki * (uint32_t)(comb<WA>::P * EA);
+  auto entry_idx = [&](int j, int d, const uint8_t*& base) -> uint32_t {
+    bool isA;
+    int pos;
+    ST::at(j, isA, pos);
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    base = (const uint8_t*)(isA ? tabA : tabB);
+#if PBFT_ABL_FETCH0
+    return (uint32_t)pos * (isA ? EA : EB) + 1u;
+#else
+    return isA ? keybase + (uint32_t)pos * EA + ad : (uint32_t)pos * EB + ad;
+#endif
+  };
+  uint8_t* eb8 = (uint8_t*)ebuf;
+  const uint32_t rd0 = 128u * lane + 16u * (lane & 7);  // chunk c of my entry at rd0 ^ (16 c)
+  ge P;
+  ge_identity(P);
+  {
+    const uint8_t* base;
+    const uint32_t e0 = entry_idx(0, dig[lane], base);
+    dma_entry_lines(base, e0, lane, eb8);
+  }
+  for (int j = 0; j < ST::N; ++j) {
+    const int d = dig[j * 64 + lane];
+    niels q;
+    {
+      uint32_t w[32];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const uint4 v = *(const uint4*)(eb8 + (rd0 ^ (16u * c)));
+        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+      }
+#pragma unroll
+      for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
+    }
+    if (j + 1 < ST::N) {
+      const int dn = dig[(j + 1) * 64 + lane];
+      const uint8_t* base;
+      const uint32_t en = entry_idx(j + 1, dn, base);
+      // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      dma_entry_lines(base, en, lane, eb8);
+    }
+#else
   auto entry_ptr = [&](int j, int d) -> const uint32_t* {
     bool isA;
     int pos;
@@ -310,7 +392,22 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       dma_entry(entry_ptr(j + 1, dn), ebuf);
     }
+#endif
+#if PBFT_ABL_NOMADD  // ablation: gathers only, no group arithmetic
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= q.ypx.v[t]; P.Y.v[t] ^= q.ymx.v[t]; P.Z.v[t] += q.xy2d.v[t] + d; }
+#else
     ge_madd_signed(P, P, q, d < 0);
+#endif
+#if PBFT_LAUNDER
+    // Keep the loop-carried limbs opaque 32-bit values: otherwise LLVM carries
+    // them as the i64 columns they were reduced from and every product with a
+    // P limb becomes a 64x32 multiply (2 mads + moves).
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      asm("" : "+v"(P.X.v[t]), "+v"(P.Y.v[t]), "+v"(P.Z.v[t]), "+v"(P.T.v[t]));
+    }
+#endif
   }
   if (live) {
 #pragma unroll
@@ -654,7 +751,9 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
   const size_t big = comb<WA_BIG>::TABLE_WORDS * 4 * (size_t)n;
-  const bool use_big = big <= budget_mb * (size_t)1048576 && big + ((size_t)4 << 30) < free_b;
+  // (the line-gather addresses key-table entries with 32-bit indices: n * P * E < 2^32)
+  const bool idx_fits = (uint64_t)n * comb<WA_BIG>::P * comb<WA_BIG>::E < (1ull << 32);
+  const bool use_big = idx_fits && big <= budget_mb * (size_t)1048576 && big + ((size_t)4 << 30) < free_b;
   const int wa = use_big ? WA_BIG : WA_SMALL;
   const size_t tab_bytes = (use_big ? comb<WA_BIG>::TABLE_WORDS : comb<WA_SMALL>::TABLE_WORDS) * 4 * (size_t)n;
   if (hipMalloc(&c->d_tabA, tab_bytes) != hipSuccess) return set_err(PBFT_ENOMEM, "key table alloc");

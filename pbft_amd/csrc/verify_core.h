@@ -56,14 +56,35 @@ FE_FN void load_niels(niels& n, const uint32_t* src) {
 #endif
 }
 
-// r = p + sign * q  (sign from neg), 7 multiplies + selects
-FE_FN void ge_madd_signed(ge& r, const ge& p, const niels& q, bool neg) {
-  fe a, b, c, d, t, qa, qb;
+// Conditional swap of two limb vectors by a lane mask m (0 or ~0): three
+// full-rate VOP2 ops per limb pair.  A per-lane `cond ? a : b` compiles to
+// v_cndmask_b32_e32 reading VCC, which issues at ~22 cycles per wave on gfx950
+// (tools/microbench/valu_mix.hip, profiles/r01_valu_mix.txt) versus ~2.2 for
+// v_xor/v_and; m is made opaque so LLVM cannot turn this back into selects.
+FE_FN void fe_cswap_mask(fe& x, fe& y, uint32_t m) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
-    qa.v[i] = neg ? q.ypx.v[i] : q.ymx.v[i];
-    qb.v[i] = neg ? q.ymx.v[i] : q.ypx.v[i];
+    const uint32_t t = (x.v[i] ^ y.v[i]) & m;
+    x.v[i] ^= t;
+    y.v[i] ^= t;
   }
+}
+
+FE_FN uint32_t lane_mask(bool c) {
+  uint32_t m = 0u - (uint32_t)c;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(m));
+#endif
+  return m;
+}
+
+// r = p + sign * q  (sign from neg), 7 multiplies + masked swaps
+FE_FN void ge_madd_signed(ge& r, const ge& p, const niels& q, bool neg) {
+  fe a, b, c, d, t, qa, qb;
+  const uint32_t m = lane_mask(neg);
+  qa = q.ymx;
+  qb = q.ypx;
+  fe_cswap_mask(qa, qb, m);
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, qa);
   fe_add(t, p.Y, p.X);
@@ -74,11 +95,9 @@ FE_FN void ge_madd_signed(ge& r, const ge& p, const niels& q, bool neg) {
   fe_sub(e, b, a);
   fe_sub(dmc, d, c);
   fe_add(dpc, d, c);
-#pragma unroll
-  for (int i = 0; i < 10; ++i) {
-    f.v[i] = neg ? dpc.v[i] : dmc.v[i];
-    g.v[i] = neg ? dmc.v[i] : dpc.v[i];
-  }
+  f = dmc;
+  g = dpc;
+  fe_cswap_mask(f, g, m);
   fe_add(h, b, a);
   // Operand order keeps the 19-premultiplied (second) operand below 2^27.3 for
   // either sign: d - c (up to 2^28) is always a first operand.  Z3 = F*G is

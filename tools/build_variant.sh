@@ -1,0 +1,11 @@
+#!/bin/bash
+# Build a variant of the verifier library for in-process A/B timing (tools/ab.py).
+# usage: tools/build_variant.sh NAME [hipcc -D flags...]   -> build/ab/libpbft_NAME.so
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/ab
+name=$1; shift
+[ -f build/replica.o ] || g++ -O2 -std=c++17 -fPIC -c -o build/replica.o pbft_amd/csrc/host/replica.cpp
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" -o build/ab/libpbft_$name.so \
+  pbft_amd/csrc/pbft_verify.hip -x none build/replica.o
+echo built build/ab/libpbft_$name.so
