@@ -36,7 +36,6 @@ N_REPLICAS = 256
 SEQS_PER_GPU = 2048
 ENVELOPE = 85
 # algorithmic 32x32->64 products per verify for the comb algorithm
-PRODUCTS_PER_VERIFY = None  # filled from pbft_amd.roofline
 SEED = 0x5EED0000 + 4
 
 
@@ -98,6 +97,20 @@ def cpu_baseline(keys, R, S, key_idx, msg, budget_s: float = 12.0):
                       f"{dt:.1f} s, {cores} threads of oracle/ed25519_oracle.c"}
 
 
+def pmc_traffic(wb: int, wa: int, n: int) -> dict:
+    """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
+    same command, tools/gpu_pmc_cur.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
+    p = os.path.join(ROOT, "profiles", "r01_pmc_comb", "derived.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return {}
+    if d.get("sigs_per_launch") != n or f"WB={wb}" not in d.get("launch", "") or f"<85,{wa}>" not in d.get("launch", ""):
+        return {}
+    return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"], "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
+            "source": "profiles/r01_pmc_comb/derived.json (PMC passes, not this run)"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -121,7 +134,11 @@ def main():
 
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
     from pbft_amd.dist import allgather_bitmap
-    from pbft_amd.roofline import PRODUCTS_PER_VERIFY, VALU_MAD_PEAK_PER_S
+    from pbft_amd import _lib
+    from pbft_amd.roofline import (INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_per_verify,
+                                   windows_from_build_info)
+    wb, wa = windows_from_build_info(_lib.load().pbft_build_info().decode())
+    PRODUCTS_PER_VERIFY = products_per_verify(wb, wa)
 
     n_rep, n_seq = args.replicas, args.seqs
     seeds = key_seeds(n_rep)
@@ -204,6 +221,7 @@ def main():
         value = total / dt
         products = PRODUCTS_PER_VERIFY * n / (kern_avg * 1e-3)
         cpu = None if args.no_cpu else cpu_baseline(pub, R, S, key_idx, msg)
+        pmc = pmc_traffic(wb, wa, n)
         line = {
             "metric": "Ed25519 verifies/sec per node (1M-signature PBFT rounds)",
             "value": value,
@@ -222,7 +240,10 @@ def main():
                        "parallelism": f"shard-by-index x{ws}" + (" + RCCL all-gather of bitmaps" if ws > 1 else "")},
             "roofline": {"bound": "valu", "achieved": products / 1e12, "peak": VALU_MAD_PEAK_PER_S / 1e12,
                          "unit": "T products/s (v_mad_u64_u32)", "frac": products / VALU_MAD_PEAK_PER_S,
-                         "traffic": None, "kernel": "comb_kernel<85,16> + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
+                         "traffic": pmc.get("traffic_bytes_per_launch"),
+                         "traffic_source": pmc.get("source"),
+                         "valu_busy_pct": pmc.get("valu_busy_pct"),
+                         "gather_bytes_algorithmic": (gather_bytes_per_verify(wb, wa) + INPUT_BYTES) * n, "kernel": f"comb_kernel<85,{wa}> (WB={wb}) + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
                          "products_per_verify": PRODUCTS_PER_VERIFY},
             "p50_ms_4k_round": float(np.median(lat)) if lat else None,
             "p99_ms_4k_round": float(np.percentile(lat, 99)) if lat else None,

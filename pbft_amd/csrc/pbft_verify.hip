@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -26,14 +27,15 @@ using namespace pbft;
 #define PBFT_ENVELOPE_LEN 85
 #define BLOCK 256
 
-// Comb windows.  The base-point table uses 16-bit windows (16 positions x
-// 32769 entries x 128 B = 67 MB, resident in HBM and largely in the 256 MB
-// MALL).  Each replica key gets a 16-bit table too (67 MB/key) while the key
-// set fits PBFT_KEY_TABLE_BUDGET_MB (default 64 GiB of the 288 GB HBM), else
-// 8-bit tables (0.5 MB/key).  Fewer windows = fewer mixed additions: 16 + 16
-// instead of 32 + 32 ("Comb windows").
+// Comb windows.  The base-point table uses 24-bit signed windows: 11 positions x
+// (2^23 + 1) entries x 128 B = 11.8 GB, one copy per device shared by all
+// contexts -- HBM capacity traded for arithmetic on a path that is VALU and
+// gather bound (11 instead of 16 mixed additions for [s]B).  Each replica key
+// gets a 16-bit table (16 positions, 67 MB/key) while the key set fits
+// PBFT_KEY_TABLE_BUDGET_MB (default 64 GiB of the 288 GB HBM), else 8-bit
+// tables (0.5 MB/key).  DESIGN.md, "Comb windows".
 #ifndef PBFT_WB
-#define PBFT_WB 16
+#define PBFT_WB 24
 #endif
 static constexpr int WB = PBFT_WB;
 static constexpr int WA_BIG = 16;
@@ -188,13 +190,16 @@ __device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
 // Same arithmetic as verify_lane (verify_core.h), split into two kernels by
 // register footprint:
 //
-//  comb_kernel   (one signature per lane, ~190 VGPRs)
-//    k = SHA-512(R || A || M) mod L; s < L; signed digits of s and k written to
-//    LDS in step order; R' = sum_i T_B[i][s_i] + T_{-A}[i][k_i] with every
-//    step's 128-B table entry fetched by LDS-DMA (global_load_lds_dwordx4,
-//    per-lane source address) one step AHEAD, so the random HBM/MALL gathers
-//    hide under the previous mixed addition.  Writes R' = (X:Y:Z) limb-major
-//    ([limb][N], coalesced) and one flag byte (s < L and key usable).
+//  comb_kernel   (one signature per lane, <= 128 VGPRs, 8 KB LDS per wave:
+//                 4 waves per SIMD)
+//    k = SHA-512(R || A || M) mod L; s < L; signed radix-2^W digits of s and k
+//    turned into one table-entry index per comb step (stored [step][Npad] in
+//    the HBM workspace, coalesced) plus a 32-bit sign mask held in a VGPR;
+//    R' = sum_i T_B[i][s_i] + T_{-A}[i][k_i], every step's 128-B table entry
+//    gathered one step AHEAD by line-coalesced LDS-DMA (dma_entry_lines), so
+//    the random HBM gathers hide under the previous mixed addition.  Writes
+//    R' = (X:Y:Z) limb-major ([limb][N], coalesced) and one flag byte
+//    (s < L and key usable).
 //  finish_kernel (M = FIN_M signatures per lane, small footprint)
 //    Montgomery batch inversion of the M Z's (1 inversion + 3(M-1) muls
 //    instead of M inversions), affine x, y, canonical compare with R,
@@ -203,6 +208,17 @@ __device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
 // Step order of the comb: B_0, A_0, B_1, A_1, ... while both scalars have
 // positions, then the remaining positions of the longer one.
 typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-B LDS read from a 32-bit LDS byte address (ds_read_b128)
+__device__ __forceinline__ u32x4 lds_read16(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+  return *(lds_u32x4*)(uintptr_t)addr;
+#else
+  (void)addr;
+  return u32x4{0, 0, 0, 0};
+#endif
+}
 #ifndef FIN_M
 #define FIN_M 16
 #endif
@@ -215,189 +231,142 @@ struct steps {
   static constexpr int PB = comb<WB_>::P, PA = comb<WA_>::P;
   static constexpr int PMIN = PB < PA ? PB : PA;
   static constexpr int N = PB + PA;
+  static_assert(N <= 64, "sign mask holds one bit per step");
+  using mask_t = typename std::conditional<(N <= 32), uint32_t, uint64_t>::type;
   // table and position of step j (wave-uniform)
-  __device__ static __forceinline__ void at(int j, bool& isA, int& pos) {
-    if (j < 2 * PMIN) { isA = j & 1; pos = j >> 1; }
-    else { isA = PA > PB; pos = j - PMIN; }
-  }
+  __host__ __device__ static constexpr bool is_a(int j) { return j < 2 * PMIN ? (j & 1) : (PA > PB); }
+  __host__ __device__ static constexpr int pos(int j) { return j < 2 * PMIN ? (j >> 1) : j - PMIN; }
 };
 
-__device__ __forceinline__ void dma_entry(const uint32_t* src, uint4* ebuf) {
-#pragma unroll
-  for (int q = 0; q < 8; ++q)
-    __builtin_amdgcn_global_load_lds(src + 4 * q, (lds_void*)(ebuf + 64 * q), 16, 0, 0);
-}
-
 // Line-coalesced gather ("transposed" DMA).  A table entry is one 128-B line.
-// Lane-per-entry DMA (dma_entry above) makes every wave-instruction touch 64
-// different lines with 16 B each, the access shape the memory pipeline serves
-// worst; here instruction i fetches the 8 entries of lanes 8i..8i+7 WHOLE: lane
-// L reads 16-B chunk c = (L & 7) ^ (L >> 3) of the entry of lane 8i + (L >> 3),
-// so each instruction covers 8 full lines.  The DMA lands lane L of instruction
-// i at LDS byte 1024 i + 16 L, i.e. entry e occupies bytes [128 e, 128 e + 128)
-// with chunk c at position c ^ (e & 7) -- the XOR swizzle spreads the owner
-// lanes' ds_read_b128 over all banks.  idx is the entry index in 128-B units
-// from `base` (the entry's owner lane holds it; 8 ds_bpermute per step).
-__device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t idx, int lane, uint8_t* ebuf) {
+// Lane-per-entry DMA (each lane fetching its own entry in 8 x 16 B) makes
+// every wave-instruction touch 64 different lines 16 B at a time, the access
+// shape the memory pipeline serves worst (profiles/r01_ab_log.md: the kernel
+// ran as fast without its arithmetic).  Here instruction q fetches the 8
+// entries of lanes 8q..8q+7 WHOLE: lane L reads 16-B chunk c = (L & 7) ^ (L >> 3)
+// of the entry of lane 8q + (L >> 3), so each instruction covers 8 full lines.
+// The DMA lands lane L of instruction q at LDS byte 1024 q + 16 L, i.e. entry e
+// occupies bytes [128 e, 128 e + 128) with chunk c at position c ^ (e & 7) --
+// the XOR swizzle spreads the owner lanes' ds_read_b128 over all banks.
+// idx (entry index in 128-B units from `base`) is fetched from its owner lane
+// with ds_bpermute (one base address + immediate offsets 32 q).
+__device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t idx, int lane, uint32_t ebuf_lds) {
   const int k = lane >> 3;
   const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
+  const int baddr = k << 2;
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const uint32_t e = (uint32_t)__shfl((int)idx, 8 * q + k);
-    __builtin_amdgcn_global_load_lds(base + (size_t)e * 128 + coff, (lds_void*)(ebuf + 1024 * q), 16, 0, 0);
+    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)idx);
+    __builtin_amdgcn_global_load_lds(base + (size_t)e * 128 + coff,
+                                     (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
   }
 }
-#ifndef PBFT_LINE_DMA
-#define PBFT_LINE_DMA 1
-#endif
 
-// Signed comb digits live in LDS in step order.  For W <= 16 a digit is in
-// [-2^(W-1), 2^(W-1) - 1] and fits int16 (halves the per-wave LDS: 8 KB entry
-// buffer + 4 KB digits, so LDS no longer caps occupancy below the VGPR limit).
 #ifndef PBFT_LAUNDER
 #define PBFT_LAUNDER 1
 #endif
-#ifndef PBFT_DIG16
-#define PBFT_DIG16 1
-#endif
-template <int WA_>
-using dig_t = typename std::conditional<(PBFT_DIG16 && WB <= 16 && WA_ <= 16), int16_t, int32_t>::type;
-template <int WA_>
-constexpr size_t comb_lds_per_wave() {
-  return 8 * 1024 + (size_t)steps<WB, WA_>::N * 64 * sizeof(dig_t<WA_>);
-}
-
 #ifndef PBFT_COMB_WAVES_PER_EU
-#define PBFT_COMB_WAVES_PER_EU 2
+#define PBFT_COMB_WAVES_PER_EU 4
 #endif
+static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
+
 template <int LEN, int WA>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint16_t* __restrict__ key_idx,
-    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
-    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags) {
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
+    uint32_t* __restrict__ eidx) {
   using ST = steps<WB, WA>;
   constexpr int EB = comb<WB>::E, EA = comb<WA>::E;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint8_t* wl = lds + (size_t)wave * comb_lds_per_wave<WA>();
-  uint4* ebuf = (uint4*)wl;
-  dig_t<WA>* dig = (dig_t<WA>*)(wl + 8 * 1024);
-  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  // wave-uniform LDS base of this wave's entry buffer (SGPR: the DMA's M0)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;  // < Npad
   const bool live = i < N;
   const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
-  uint32_t r[8], s[8], a[8];
-  load32(r, R + 32 * ii);
-  load32(s, S + 32 * ii);
-  uint32_t ki = key_idx[ii];
-  bool kok = ki < n_keys;
-  if (!kok) ki = 0;
-  kok = kok && key_ok[ki];
+  typename ST::mask_t sgn = 0;        // bit j: digit of step j is negative
+  bool s_ok, kok;
   {
-    const uint4* kp = (const uint4*)(keys + 8 * ki);
-    const uint4 k0 = kp[0], k1 = kp[1];
-    a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
-  }
-#if !PBFT_LINE_DMA
-  const uint32_t* tA = tabA + (size_t)ki * comb<WA>::TABLE_WORDS;
-#endif
-  const bool s_ok = sc_lt_L(s);
-  {
+    uint32_t r[8], s[8], a[8];
+    load32(r, R + 32 * ii);
+    load32(s, S + 32 * ii);
+    uint32_t ki = key_idx[ii];
+    kok = ki < n_keys;
+    if (!kok) ki = 0;
+    kok = kok && key_ok[ki];
+    {
+      const uint4* kp = (const uint4*)(keys + 8 * ki);
+      const uint4 k0 = kp[0], k1 = kp[1];
+      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+    }
+    s_ok = sc_lt_L(s);
     uint32_t h[16], k[8];
+#if PBFT_ABL_NOSHA  // ablation: no challenge hash (k from R and A directly)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) h[t] = r[t & 7] ^ a[(t + 3) & 7];
+#else
     sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * ii, (int)msg_len);
+#endif
     sc_reduce512(k, h);
+    // per-step entry index (128-B units from the step's table base) and sign
+    const uint32_t keybase = ki * (uint32_t)(comb<WA>::P * EA);
     digit_stream<WB> ds;
     ds.init(s);
     digit_stream<WA> dk;
     dk.init(k);
-    int j = 0;
 #pragma unroll
-    for (int p = 0; p < (ST::PB > ST::PA ? ST::PB : ST::PA); ++p) {
-      if (p < ST::PB) dig[(j++) * 64 + lane] = (dig_t<WA>)ds.next();
-      if (p < ST::PA) dig[(j++) * 64 + lane] = (dig_t<WA>)dk.next();
+    for (int j = 0; j < ST::N; ++j) {
+      const bool isA = ST::is_a(j);
+      const int d = isA ? dk.next() : ds.next();
+      const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+      sgn |= (typename ST::mask_t)(d < 0 ? 1u : 0u) << j;
+#if PBFT_ABL_FETCH0  // ablation: every lane gathers entry 1 of its position (L2-resident)
+      const uint32_t e = (uint32_t)ST::pos(j) * (isA ? EA : EB) + 1u;
+#else
+      const uint32_t e = isA ? keybase + (uint32_t)ST::pos(j) * EA + ad : (uint32_t)ST::pos(j) * EB + ad;
+#endif
+      eidx[(size_t)j * Npad + i] = e;
     }
   }
-#if PBFT_LINE_DMA
-  // entry index of step j in 128-B units from the step's (wave-uniform) table base
-  const uint32_t keybase = ki * (uint32_t)(comb<WA>::P * EA);
-  auto entry_idx = [&](int j, int d, const uint8_t*& base) -> uint32_t {
-    bool isA;
-    int pos;
-    ST::at(j, isA, pos);
-    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-    base = (const uint8_t*)(isA ? tabA : tabB);
-#if PBFT_ABL_FETCH0
-    return (uint32_t)pos * (isA ? EA : EB) + 1u;
-#else
-    return isA ? keybase + (uint32_t)pos * EA + ad : (uint32_t)pos * EB + ad;
-#endif
-  };
-  uint8_t* eb8 = (uint8_t*)ebuf;
-  const uint32_t rd0 = 128u * lane + 16u * (lane & 7);  // chunk c of my entry at rd0 ^ (16 c)
+  const uint8_t* tB = (const uint8_t*)tabB;
+  const uint8_t* tA = (const uint8_t*)tabA;
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // chunk c of my entry at rd0 ^ (16 c)
   ge P;
   ge_identity(P);
-  {
-    const uint8_t* base;
-    const uint32_t e0 = entry_idx(0, dig[lane], base);
-    dma_entry_lines(base, e0, lane, eb8);
-  }
+  // (each lane re-reads only the indices it wrote itself: no barrier needed)
+  dma_entry_lines(ST::is_a(0) ? tA : tB, eidx[i], lane, ebuf);
+  uint32_t nidx = eidx[Npad + i];
   for (int j = 0; j < ST::N; ++j) {
-    const int d = dig[j * 64 + lane];
+    // The entry's DMA must have landed: the ds_reads below use integer LDS
+    // addresses, so the compiler cannot see that they alias the DMA's writes.
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    asm volatile("" ::: "memory");
     niels q;
     {
       uint32_t w[32];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const uint4 v = *(const uint4*)(eb8 + (rd0 ^ (16u * c)));
+        const u32x4 v = lds_read16(rd0 ^ (16u * c));
         w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
       }
 #pragma unroll
       for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
     }
     if (j + 1 < ST::N) {
-      const int dn = dig[(j + 1) * 64 + lane];
-      const uint8_t* base;
-      const uint32_t en = entry_idx(j + 1, dn, base);
       // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      dma_entry_lines(base, en, lane, eb8);
+      dma_entry_lines(ST::is_a(j + 1) ? tA : tB, nidx, lane, ebuf);
+      if (j + 2 < ST::N) nidx = eidx[(size_t)(j + 2) * Npad + i];
     }
-#else
-  auto entry_ptr = [&](int j, int d) -> const uint32_t* {
-    bool isA;
-    int pos;
-    ST::at(j, isA, pos);
-    const int ad = d < 0 ? -d : d;
-    return isA ? tA + ((size_t)pos * EA + ad) * 32 : tabB + ((size_t)pos * EB + ad) * 32;
-  };
-  ge P;
-  ge_identity(P);
-  dma_entry(entry_ptr(0, dig[lane]), ebuf);
-  for (int j = 0; j < ST::N; ++j) {
-    const int d = dig[j * 64 + lane];
-    niels q;
-    {
-      uint32_t w[32];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const uint4 v = ebuf[64 * c + lane];
-        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-      }
-#pragma unroll
-      for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
-    }
-    if (j + 1 < ST::N) {
-      const int dn = dig[(j + 1) * 64 + lane];
-      // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      dma_entry(entry_ptr(j + 1, dn), ebuf);
-    }
-#endif
+    const bool neg = (uint32_t)(sgn >> j) & 1u;
 #if PBFT_ABL_NOMADD  // ablation: gathers only, no group arithmetic
 #pragma unroll
-    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= q.ypx.v[t]; P.Y.v[t] ^= q.ymx.v[t]; P.Z.v[t] += q.xy2d.v[t] + d; }
+    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= q.ypx.v[t]; P.Y.v[t] ^= q.ymx.v[t]; P.Z.v[t] += q.xy2d.v[t] + neg; }
 #else
-    ge_madd_signed(P, P, q, d < 0);
+    ge_madd_signed(P, P, q, neg);
 #endif
 #if PBFT_LAUNDER
     // Keep the loop-carried limbs opaque 32-bit values: otherwise LLVM carries
@@ -602,8 +571,16 @@ static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
 
 // Grow the verify workspace (never inside a stream capture: call
 // pbft_verify_reserve first when capturing launches into a graph).
+// Workspace per launch of N signatures (Npad = N rounded up to BLOCK):
+//   xyz   [30][N] u32   R' limbs, comb -> finish            120 B/sig
+//   flags [N] u8                                              1 B/sig
+//   eidx  [steps][Npad] u32  per-step table entry indices    4 x steps B/sig
+static constexpr int MAX_STEPS = steps<WB, WA_SMALL>::N > steps<WB, WA_BIG>::N ? steps<WB, WA_SMALL>::N
+                                                                              : steps<WB, WA_BIG>::N;
+static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static int ensure_work(pbft_ctx* c, uint64_t N) {
-  const size_t need = 121 * (size_t)N + 256;
+  const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
+  const size_t need = eidx_offset(N) + 4 * (size_t)MAX_STEPS * Npad + 256;
   if (need <= c->work_cap) return PBFT_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->d_work) HIP_TRY(hipFree(c->d_work));
@@ -625,10 +602,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   const dim3 g((unsigned)blocks), b(BLOCK);
   uint32_t* xyz = (uint32_t*)c->d_work;
   uint8_t* flags = c->d_work + 120 * N;
-#define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                          \
-  hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * comb_lds_per_wave<WA_>(), st, dR, dS, dK, \
-                     dM, msg_len, msg_stride, N, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz,  \
-                     flags)
+  uint32_t* eidx = (uint32_t*)(c->d_work + eidx_offset(N));
+  const uint64_t Npad = blocks * BLOCK;
+#define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
+  hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS, dK, dM, msg_len, \
+                     msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
   if (msg_len == PBFT_ENVELOPE_LEN) {
     if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
     else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
@@ -674,6 +652,46 @@ static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
                        msg_len, msg_stride, N, c->d_bitmap, c->stream);
 }
 
+// The base-point comb table is a constant of the curve: one copy per device,
+// shared by every context on it (reference-counted; at WB = 24 it is 11.8 GB).
+static std::mutex g_tabB_mu;
+static uint32_t* g_tabB[64] = {};
+static int g_tabB_refs[64] = {};
+
+static int acquire_base_table(int device, hipStream_t st, uint32_t** out) {
+  std::lock_guard<std::mutex> lk(g_tabB_mu);
+  if (device < 0 || device >= 64) return set_err(PBFT_ENODEV, "device ordinal >= 64");
+  if (!g_tabB[device]) {
+    // base point B = (x, 4/5), x even
+    const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
+                              0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
+    uint32_t* d_benc = nullptr;
+    uint32_t* tab = nullptr;
+    HIP_TRY(hipMalloc(&d_benc, 32));
+    if (hipMalloc(&tab, comb<WB>::TABLE_WORDS * 4) != hipSuccess) {
+      (void)hipFree(d_benc);
+      return set_err(PBFT_ENOMEM, "base-point table alloc");
+    }
+    HIP_TRY(hipMemcpyAsync(d_benc, benc, 32, hipMemcpyHostToDevice, st));
+    int rc = build_tables<WB>(d_benc, 1u, 0, tab, nullptr, st);
+    (void)hipFree(d_benc);
+    if (rc) { (void)hipFree(tab); return rc; }
+    g_tabB[device] = tab;
+  }
+  ++g_tabB_refs[device];
+  *out = g_tabB[device];
+  return PBFT_OK;
+}
+
+static void release_base_table(int device) {
+  std::lock_guard<std::mutex> lk(g_tabB_mu);
+  if (device < 0 || device >= 64 || g_tabB_refs[device] == 0) return;
+  if (--g_tabB_refs[device] == 0) {
+    (void)hipFree(g_tabB[device]);
+    g_tabB[device] = nullptr;
+  }
+}
+
 extern "C" {
 
 const char* pbft_last_error(void) { return g_last_error.c_str(); }
@@ -707,16 +725,13 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
-  // base point B = (x, 4/5), x even
-  const uint32_t benc[8] = {0x66666658u, 0x66666666u, 0x66666666u, 0x66666666u,
-                            0x66666666u, 0x66666666u, 0x66666666u, 0x66666666u};
-  uint32_t* d_benc = nullptr;
-  HIP_TRY(hipMalloc(&d_benc, 32));
-  HIP_TRY(hipMalloc(&c->d_tabB, comb<WB>::TABLE_WORDS * 4));
-  HIP_TRY(hipMemcpyAsync(d_benc, benc, 32, hipMemcpyHostToDevice, c->stream));
-  int rc = build_tables<WB>(d_benc, 1u, 0, c->d_tabB, nullptr, c->stream);
-  if (rc) return rc;
-  HIP_TRY(hipFree(d_benc));
+  int rc = acquire_base_table(device, c->stream, &c->d_tabB);
+  if (rc) {
+    (void)hipEventDestroy(c->ev0); (void)hipEventDestroy(c->ev1); (void)hipEventDestroy(c->ev_done);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return rc;
+  }
   *out = c;
   return PBFT_OK;
 }
@@ -726,7 +741,8 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   // teardown: errors are ignored (nothing useful to report from a destructor)
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(c->d_tabB); (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
+  release_base_table(c->device);
+  (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
   (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work);
   if (c->h_bitmap) (void)hipHostFree(c->h_bitmap);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
