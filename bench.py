@@ -111,6 +111,57 @@ def pmc_traffic(wb: int, wa: int, n: int) -> dict:
             "source": "profiles/r01_pmc_comb/derived.json (PMC passes, not this run)"}
 
 
+def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int = 4096, n_ctx: int = 4,
+                   duration_s: float = 1.0):
+    """BASELINE config #5 on this GPU: 4096-signature batches arriving at a fixed offered rate, each submitted
+    through the host-buffer API (H2D copies + kernels + bitmap D2H) on one of n_ctx contexts (own HIP streams,
+    shared tables: pbft_verify_ctx_clone).  Latency = bitmap ready (host poll) - scheduled arrival.
+    offered_sigs_per_s = inf measures back-to-back pipelined throughput instead."""
+    from pbft_amd import SigBatch
+    ctxs = [v.clone() for _ in range(n_ctx)]
+    nb = max(1, len(R) // batch)
+    batches = [SigBatch(R[i * batch:(i + 1) * batch], S[i * batch:(i + 1) * batch],
+                        key_idx[i * batch:(i + 1) * batch], msg[i * batch:(i + 1) * batch], ENVELOPE)
+               for i in range(min(nb, 64))]
+    for c in ctxs:  # warm: workspace / staging allocation
+        c.wait(c.submit(batches[0]))
+    period = batch / offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else 0.0
+    pending = [None] * n_ctx  # (ticket, scheduled time)
+    lat, done = [], 0
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        now = time.perf_counter()
+        for ci, p in enumerate(pending):
+            if p is not None and ctxs[ci].poll(p[0]) is not None:
+                t = time.perf_counter()
+                lat.append((t - p[1]) * 1e3)
+                pending[ci] = None
+                done += 1
+        if now - t0 >= duration_s:
+            if all(p is None for p in pending):
+                break
+            continue
+        t_sched = t0 + k * period
+        if now >= t_sched:
+            ci = k % n_ctx
+            if pending[ci] is not None:  # backlog: this stream is still busy
+                b = ctxs[ci].wait(pending[ci][0])
+                lat.append((time.perf_counter() - pending[ci][1]) * 1e3)
+                done += 1
+            pending[ci] = (ctxs[ci].submit(batches[k % len(batches)]), t_sched if period else time.perf_counter())
+            k += 1
+    wall = time.perf_counter() - t0
+    for c in ctxs:
+        c.close()
+    lat = np.array(lat)
+    return {"batch": batch, "streams": n_ctx,
+            "offered_sigs_per_s": offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else None,
+            "achieved_sigs_per_s": done * batch / wall, "batches": int(done),
+            "p50_ms": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)),
+            "path": "host buffers: H2D + comb + finish + D2H per batch"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -220,6 +271,11 @@ def main():
         total = n * ws * args.steps
         value = total / dt
         products = PRODUCTS_PER_VERIFY * n / (kern_avg * 1e-3)
+        stream = None
+        if args.latency_iters > 0:
+            # config #5: 2^24 sigs/s offered to an 8-GPU node = 2^21 per GPU; and back-to-back 4k batches
+            stream = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21)),
+                      "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
         cpu = None if args.no_cpu else cpu_baseline(pub, R, S, key_idx, msg)
         pmc = pmc_traffic(wb, wa, n)
         line = {
@@ -247,6 +303,7 @@ def main():
                          "products_per_verify": PRODUCTS_PER_VERIFY},
             "p50_ms_4k_round": float(np.median(lat)) if lat else None,
             "p99_ms_4k_round": float(np.percentile(lat, 99)) if lat else None,
+            "stream_4k": stream,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

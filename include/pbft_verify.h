@@ -61,6 +61,13 @@ int pbft_verify_ctx_destroy(pbft_ctx *ctx);
  * rejects (bad encoding or small order).  Replaces any previous key set. */
 int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *key_ok);
 
+/* A second context on the same device that shares the parent's base-point
+ * table and its CURRENT key set (reference-counted; a later set_keys on either
+ * context replaces only that context's key set), with its own HIP stream,
+ * staging and workspace: one context per host thread / in-flight stream for
+ * pipelined serving of small batches (BASELINE config #5). */
+int pbft_verify_ctx_clone(pbft_ctx *parent, pbft_ctx **out);
+
 /* Blocking batch verify from host buffers (PCIe copies included).
  * R[N][32], S[N][32], key_idx[N] (index into the key set), msg[N][msg_stride]
  * of which the first msg_len bytes are the signed message.  bitmap_out has
@@ -85,7 +92,7 @@ int pbft_verify_batch_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d
                              const uint8_t *d_msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                              uint64_t *d_bitmap, void *stream);
 
-/* Pre-size the verify workspace (121 bytes of HBM per signature) for batches
+/* Pre-size the verify workspace (~230 bytes of HBM per signature) for batches
  * of up to max_n signatures, so that later launches allocate nothing (required
  * before capturing pbft_verify_batch_device into a hipGraph). */
 int pbft_verify_reserve(pbft_ctx *ctx, uint64_t max_n);

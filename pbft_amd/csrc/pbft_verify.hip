@@ -13,6 +13,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -523,15 +524,41 @@ __global__ void __launch_bounds__(BLOCK) digest_kernel(const uint8_t* __restrict
 }
 
 // ------------------------------------------------------------------ context
+// A replica key set on one device: raw encodings, key_ok bytes and the -A comb
+// tables.  Reference-counted so that contexts cloned for extra streams
+// (pbft_verify_ctx_clone) serve batches from the same tables.
+struct keyset {
+  std::atomic<int> refs{1};
+  uint32_t* d_tabA = nullptr;
+  uint32_t* d_keys = nullptr;
+  uint8_t* d_key_ok = nullptr;
+  uint32_t n = 0;
+  int wa = 0;
+};
+static void keyset_release(keyset* k) {
+  if (k && --k->refs == 0) {
+    (void)hipFree(k->d_tabA); (void)hipFree(k->d_keys); (void)hipFree(k->d_key_ok);
+    delete k;
+  }
+}
+
 struct pbft_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
   uint32_t* d_tabB = nullptr;
+  keyset* ks = nullptr;
+  // cached from ks (null / 0 without a key set)
   uint32_t* d_tabA = nullptr;
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
   int wa = 0;  // comb window of the installed key tables (WA_BIG or WA_SMALL)
+  void adopt(keyset* k) {
+    keyset_release(ks);
+    ks = k;
+    d_tabA = k ? k->d_tabA : nullptr; d_keys = k ? k->d_keys : nullptr; d_key_ok = k ? k->d_key_ok : nullptr;
+    n_keys = k ? k->n : 0; wa = k ? k->wa : 0;
+  }
   // staging for the host-buffer API
   uint8_t* d_stage = nullptr;
   size_t stage_cap = 0;
@@ -742,7 +769,7 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   release_base_table(c->device);
-  (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
+  c->adopt(nullptr);
   (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work);
   if (c->h_bitmap) (void)hipHostFree(c->h_bitmap);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -759,8 +786,7 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  (void)hipFree(c->d_tabA); (void)hipFree(c->d_keys); (void)hipFree(c->d_key_ok);
-  c->d_tabA = nullptr; c->d_keys = nullptr; c->d_key_ok = nullptr; c->n_keys = 0;
+  c->adopt(nullptr);
   // 16-bit key windows while the key set fits the budget, else 8-bit
   size_t budget_mb = 65536;
   if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
@@ -770,19 +796,43 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   // (the line-gather addresses key-table entries with 32-bit indices: n * P * E < 2^32)
   const bool idx_fits = (uint64_t)n * comb<WA_BIG>::P * comb<WA_BIG>::E < (1ull << 32);
   const bool use_big = idx_fits && big <= budget_mb * (size_t)1048576 && big + ((size_t)4 << 30) < free_b;
-  const int wa = use_big ? WA_BIG : WA_SMALL;
   const size_t tab_bytes = (use_big ? comb<WA_BIG>::TABLE_WORDS : comb<WA_SMALL>::TABLE_WORDS) * 4 * (size_t)n;
-  if (hipMalloc(&c->d_tabA, tab_bytes) != hipSuccess) return set_err(PBFT_ENOMEM, "key table alloc");
-  HIP_TRY(hipMalloc(&c->d_keys, 32 * (size_t)n));
-  HIP_TRY(hipMalloc(&c->d_key_ok, n));
-  HIP_TRY(hipMemcpyAsync(c->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  int rc = use_big ? build_tables<WA_BIG>(c->d_keys, n, 1, c->d_tabA, c->d_key_ok, c->stream)
-                   : build_tables<WA_SMALL>(c->d_keys, n, 1, c->d_tabA, c->d_key_ok, c->stream);
+  keyset* k = new keyset();
+  k->wa = use_big ? WA_BIG : WA_SMALL;
+  k->n = n;
+  if (hipMalloc(&k->d_tabA, tab_bytes) != hipSuccess || hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess ||
+      hipMalloc(&k->d_key_ok, n) != hipSuccess) {
+    keyset_release(k);
+    return set_err(PBFT_ENOMEM, "key table alloc");
+  }
+  int rc = PBFT_OK;
+  if (hipMemcpyAsync(k->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = set_err(PBFT_EHIP, "key upload");
+  if (!rc)
+    rc = use_big ? build_tables<WA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+                 : build_tables<WA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
+  if (!rc && key_ok && hipMemcpyAsync(key_ok, k->d_key_ok, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    rc = set_err(PBFT_EHIP, "key_ok download");
+  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
+  if (rc) {
+    keyset_release(k);
+    return rc;
+  }
+  c->adopt(k);
+  return PBFT_OK;
+}
+
+int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
+  if (!parent || !out) return set_err(PBFT_EINVAL, "null argument");
+  *out = nullptr;
+  pbft_ctx* c = nullptr;
+  int rc = pbft_verify_ctx_create(parent->device, &c);
   if (rc) return rc;
-  c->wa = wa;
-  if (key_ok) HIP_TRY(hipMemcpyAsync(key_ok, c->d_key_ok, n, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  c->n_keys = n;
+  if (parent->ks) {
+    ++parent->ks->refs;
+    c->adopt(parent->ks);
+  }
+  *out = c;
   return PBFT_OK;
 }
 

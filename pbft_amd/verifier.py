@@ -65,13 +65,21 @@ def bitmap_to_bool(bitmap: np.ndarray, n: int) -> np.ndarray:
 class GpuBatchVerifier:
     """One HIP context (one GPU).  Not thread-safe: one per host thread."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, _parent: "GpuBatchVerifier | None" = None):
         self._lib = load()
         self._ctx = ctypes.c_void_p()
-        check(self._lib.pbft_verify_ctx_create(device, ctypes.byref(self._ctx)))
+        if _parent is None:
+            check(self._lib.pbft_verify_ctx_create(device, ctypes.byref(self._ctx)))
+            self.n_keys = 0
+        else:
+            check(self._lib.pbft_verify_ctx_clone(_parent._ctx, ctypes.byref(self._ctx)))
+            device, self.n_keys = _parent.device, _parent.n_keys
         self.device = device
-        self.n_keys = 0
         self._pending = None
+
+    def clone(self) -> "GpuBatchVerifier":
+        """Another context (own HIP stream and workspace) sharing this one's tables and key set."""
+        return GpuBatchVerifier(_parent=self)
 
     # -- key set (libp2p identity keys, src/main.rs:39-40) ------------------
     def set_keys(self, keys: np.ndarray) -> np.ndarray:

@@ -251,3 +251,28 @@ def test_digests_match_hashlib(gv):
         assert s2[i].tobytes() == hashlib.sha256(it).digest(), (i, len(it))
     # the reference README's request (README.md:42) digest, src/message.rs:209-212
     assert b2[2].tobytes().hex() == KAT["digest"]["blake2b512_hex"]
+
+
+def test_ctx_clone_shares_tables_and_snapshots_keys(gv, golden):
+    """pbft_verify_ctx_clone: a second stream on the same tables; the clone keeps the key set it was made with."""
+    from pbft_amd import SigBatch, bitmap_to_bool
+    bs = dict(golden_batches(golden))
+    b85, b0 = bs[85], bs[0]
+    gv.set_keys(b85["keys"])
+    c = gv.clone()
+    try:
+        exp = b85["expected"].astype(bool)
+        batch = SigBatch(b85["R"], b85["S"], b85["key_idx"], b85["msg"], 85)
+        # both contexts in flight at once (two HIP streams), same answer
+        t1, t2 = gv.submit(batch), c.submit(batch)
+        o2, o1 = c.wait(t2), gv.wait(t1)
+        assert (bitmap_to_bool(o1, len(exp)) == exp).all()
+        assert (bitmap_to_bool(o2, len(exp)) == exp).all()
+        # replacing the parent's key set leaves the clone's snapshot in place
+        gv.set_keys(b0["keys"])
+        got0, _ = verify(gv, b0["R"], b0["S"], b0["key_idx"], b0["msg"], 0)
+        assert (got0 == b0["expected"].astype(bool)).all()
+        got85 = bitmap_to_bool(c.verify(batch), len(exp))
+        assert (got85 == exp).all()
+    finally:
+        c.close()
