@@ -18,6 +18,10 @@ EXPORTS = (
     "pbft_verify_batch", "pbft_verify_batch_async", "pbft_verify_poll", "pbft_verify_wait",
     "pbft_verify_batch_device", "pbft_verify_reserve", "pbft_digest_blake2b512", "pbft_digest_sha256",
     "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms",
+    # include/pbft_wire.h
+    "pbft_uvi_encode", "pbft_uvi_decode", "pbft_wire_encode_json", "pbft_wire_encode_frame",
+    "pbft_wire_decode_json", "pbft_wire_decode_votes", "pbft_records_pack", "pbft_verify_records_device",
+    "pbft_verify_records",
 )
 
 ERRORS = {0: "PBFT_OK", -1: "PBFT_EINVAL", -2: "PBFT_EHIP", -3: "PBFT_ENOKEYS",
@@ -69,6 +73,16 @@ def load() -> ctypes.CDLL:
         "pbft_last_error": (ctypes.c_char_p, []),
         "pbft_build_info": (ctypes.c_char_p, []),
         "pbft_last_kernel_ms": (ctypes.c_float, [vp]),
+        "pbft_uvi_encode": (ctypes.c_size_t, [u64, u8p]),
+        "pbft_uvi_decode": (i32, [u8p, ctypes.c_size_t, vp, vp]),
+        "pbft_wire_encode_json": (i32, [vp, vp, ctypes.c_size_t, vp]),
+        "pbft_wire_encode_frame": (i32, [vp, vp, ctypes.c_size_t, vp]),
+        "pbft_wire_decode_json": (i32, [vp, ctypes.c_size_t, vp, vp, ctypes.c_size_t]),
+        "pbft_wire_decode_votes": (i32, [u8p, ctypes.c_size_t, u32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                         vp, vp, vp]),
+        "pbft_records_pack": (i32, [vp, vp, vp, vp, u32, u64, vp]),
+        "pbft_verify_records_device": (i32, [vp, vp, u64, vp, vp]),
+        "pbft_verify_records": (i32, [vp, vp, u64, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

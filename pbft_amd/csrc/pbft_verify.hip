@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/pbft_verify.h"
+#include "../../include/pbft_wire.h"
 #include "digest_kernels.h"
 #include "verify_core.h"
 
@@ -273,7 +274,8 @@ static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
 
 template <int LEN, int WA>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
-    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint16_t* __restrict__ key_idx,
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
+    uint32_t rs_stride, uint32_t k_stride,
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
@@ -292,9 +294,9 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   bool s_ok, kok;
   {
     uint32_t r[8], s[8], a[8];
-    load32(r, R + 32 * ii);
-    load32(s, S + 32 * ii);
-    uint32_t ki = key_idx[ii];
+    load32(r, R + (size_t)rs_stride * ii);
+    load32(s, S + (size_t)rs_stride * ii);
+    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
     kok = ki < n_keys;
     if (!kok) ki = 0;
     kok = kok && key_ok[ki];
@@ -420,6 +422,7 @@ struct fin_unroll<0> {
 
 // M signatures per lane: lane l of wave w handles i = (w * M + m) * 64 + l.
 __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const uint8_t* __restrict__ R,
+                                                       uint32_t rs_stride,
                                                        const uint32_t* __restrict__ xyz,
                                                        const uint8_t* __restrict__ flags, uint64_t N,
                                                        uint64_t* __restrict__ bitmap) {
@@ -464,7 +467,7 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
     uint32_t xw[8], yw[8], r[8], ry[8];
     fe_to_words(xw, x);
     fe_to_words(yw, y);
-    load32(r, R + 32 * ii);
+    load32(r, R + (size_t)rs_stride * ii);
     canon_y(ry, r);
     bool eq = (xw[0] & 1u) == (r[7] >> 31);
 #pragma unroll
@@ -619,7 +622,8 @@ static int ensure_work(pbft_ctx* c, uint64_t N) {
 }
 
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
-                         uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st) {
+                         uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
+                         uint32_t rs_stride = 32, uint32_t k_stride = 2) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
@@ -632,8 +636,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   uint32_t* eidx = (uint32_t*)(c->d_work + eidx_offset(N));
   const uint64_t Npad = blocks * BLOCK;
 #define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
-  hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS, dK, dM, msg_len, \
-                     msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
+  hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS,             \
+                     (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
   if (msg_len == PBFT_ENVELOPE_LEN) {
     if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
     else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
@@ -645,7 +649,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   HIP_TRY(hipGetLastError());
   const uint64_t fin_waves = (N + 64 * FIN_M - 1) / (64 * FIN_M);
   const uint64_t fin_blocks = (fin_waves * 64 + BLOCK - 1) / BLOCK;
-  hipLaunchKernelGGL(finish_kernel, dim3((unsigned)fin_blocks), dim3(BLOCK), 0, st, dR, xyz, flags, N, dB);
+  hipLaunchKernelGGL(finish_kernel, dim3((unsigned)fin_blocks), dim3(BLOCK), 0, st, dR, rs_stride, xyz, flags, N,
+                     dB);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev1, st));
   return PBFT_OK;
@@ -895,6 +900,37 @@ int pbft_verify_batch_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, 
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
   return launch_verify(c, dR, dS, dK, dM, msg_len, msg_stride, N, dB, st);
+}
+
+// Binary wire records (include/pbft_wire.h): R at +0, S at +32, envelope at +64,
+// key index at +150, stride 160 -- read in place by the same kernels.
+int pbft_verify_records_device(pbft_ctx* c, const uint8_t* d_rec, uint64_t N, uint64_t* dB, void* stream) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (N && (!d_rec || !dB)) return set_err(PBFT_EINVAL, "bad batch arguments");
+  if (((uintptr_t)d_rec & 15) != 0) return set_err(PBFT_EINVAL, "records must be 16-byte aligned");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  return launch_verify(c, d_rec, d_rec + 32, (const uint16_t*)(d_rec + 150), d_rec + 64, PBFT_ENVELOPE_LEN,
+                       PBFT_RECORD_BYTES, N, dB, st, PBFT_RECORD_BYTES, PBFT_RECORD_BYTES);
+}
+
+int pbft_verify_records(pbft_ctx* c, const uint8_t* rec, uint64_t N, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (N && (!rec || !out)) return set_err(PBFT_EINVAL, "bad batch arguments");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  if (N == 0) return PBFT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t words = (N + 63) / 64;
+  int rc = ensure_stage(c, PBFT_RECORD_BYTES * N + 256, words);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->d_stage, rec, PBFT_RECORD_BYTES * N, hipMemcpyHostToDevice, c->stream));
+  rc = pbft_verify_records_device(c, c->d_stage, N, c->d_bitmap, c->stream);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(out, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return PBFT_OK;
 }
 
 static int run_digest(pbft_ctx* c, int kind, const uint8_t* data, const uint64_t* offsets, const uint32_t* lens,

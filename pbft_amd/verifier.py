@@ -129,6 +129,14 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_batch_device(self._ctx, d_R, d_S, d_key_idx, d_msg, msg_len, msg_stride, n,
                                                  d_bitmap, stream or None))
 
+    def verify_records(self, records: np.ndarray) -> np.ndarray:
+        """Blocking verify of (N, 160) binary wire records (include/pbft_wire.h); returns bitmap words."""
+        rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, 160)
+        n = len(rec)
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_records(self._ctx, _ptr(rec), n, _ptr(out)))
+        return out
+
     def last_kernel_ms(self) -> float:
         return float(self._lib.pbft_last_kernel_ms(self._ctx))
 

@@ -5,7 +5,9 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/ab
 name=$1; shift
-[ -f build/replica.o ] || g++ -O2 -std=c++17 -fPIC -c -o build/replica.o pbft_amd/csrc/host/replica.cpp
+for h in replica wire; do
+  [ build/$h.o -nt pbft_amd/csrc/host/$h.cpp ] || g++ -O2 -std=c++17 -fPIC -c -o build/$h.o pbft_amd/csrc/host/$h.cpp
+done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" -o build/ab/libpbft_$name.so \
-  pbft_amd/csrc/pbft_verify.hip -x none build/replica.o
+  pbft_amd/csrc/pbft_verify.hip -x none build/replica.o build/wire.o
 echo built build/ab/libpbft_$name.so

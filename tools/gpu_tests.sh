@@ -1,8 +1,8 @@
 #!/bin/bash
+# GPU parity tests + smoke only
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
-tail -40 gpurun_out/pytest_gpu.log
-exit $rc
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 420 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
