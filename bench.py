@@ -200,6 +200,8 @@ def main():
     R, S, pub = v.sign(seeds, key_idx, msg, ENVELOPE)
     key_ok = v.set_keys(pub)
     assert key_ok.all()
+    wb, wa = v.windows()  # the key window set_keys chose for this key set
+    PRODUCTS_PER_VERIFY = products_per_verify(wb, wa)
 
     dev = torch.device("cuda", local)
     d_R = torch.from_numpy(R).to(dev)

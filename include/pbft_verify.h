@@ -115,6 +115,9 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 /* Diagnostics */
 const char *pbft_last_error(void);
 const char *pbft_build_info(void); /* kernel windows, arch, version */
+/* Comb windows in use: wb (base point, build-time) and wa (the installed key
+ * set's window, chosen by pbft_verify_set_keys; 0 before it), key count. */
+int pbft_verify_ctx_info(pbft_ctx *ctx, uint32_t *wb, uint32_t *wa, uint32_t *n_keys);
 /* Device time of the last verify kernel launched by this context, in ms
  * (HIP events on the launch stream). */
 float pbft_last_kernel_ms(pbft_ctx *ctx);

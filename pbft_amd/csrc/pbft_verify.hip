@@ -29,19 +29,24 @@ using namespace pbft;
 #define PBFT_ENVELOPE_LEN 85
 #define BLOCK 256
 
-// Comb windows.  The base-point table uses 24-bit signed windows: 11 positions x
-// (2^23 + 1) entries x 128 B = 11.8 GB, one copy per device shared by all
-// contexts -- HBM capacity traded for arithmetic on a path that is VALU and
-// gather bound (11 instead of 16 mixed additions for [s]B).  Each replica key
-// gets a 16-bit table (16 positions, 67 MB/key) while the key set fits
-// PBFT_KEY_TABLE_BUDGET_MB (default 64 GiB of the 288 GB HBM), else 8-bit
-// tables (0.5 MB/key).  DESIGN.md, "Comb windows".
+// Comb windows.  The base-point table uses 26-bit signed windows: 10 positions x
+// (2^25 + 1) entries x 128 B = 43 GB, one copy per device shared by all
+// contexts -- HBM capacity traded for arithmetic on a VALU-bound path (10
+// instead of 16 mixed additions for [s]B).  Each replica key gets an 18-bit
+// table (15 positions, 252 MB/key) while the key set fits
+// PBFT_KEY_TABLE_BUDGET_MB (default 96 GiB of the 288 GB HBM), else 16-bit
+// (67 MB/key), else 8-bit (0.5 MB/key).  25 steps per signature at n <= 390.
+// DESIGN.md §3-4; measured in profiles/r01_ab_log.md.
 #ifndef PBFT_WB
-#define PBFT_WB 24
+#define PBFT_WB 26
 #endif
 static constexpr int WB = PBFT_WB;
-static constexpr int WA_BIG = 16;
-static constexpr int WA_SMALL = 8;
+#ifndef PBFT_WA
+#define PBFT_WA 18
+#endif
+static constexpr int WA_BIG = PBFT_WA;  // 15 positions x (2^17 + 1) x 128 B = 252 MB per key
+static constexpr int WA_MID = 16;       // 16 positions x (2^15 + 1) x 128 B =  67 MB per key
+static constexpr int WA_SMALL = 8;      // 32 positions x 129 x 128 B        = 0.5 MB per key
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_last_error;
@@ -555,7 +560,7 @@ struct pbft_ctx {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
-  int wa = 0;  // comb window of the installed key tables (WA_BIG or WA_SMALL)
+  int wa = 0;  // comb window of the installed key tables (WA_BIG, WA_MID or WA_SMALL)
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
@@ -605,8 +610,8 @@ static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
 //   xyz   [30][N] u32   R' limbs, comb -> finish            120 B/sig
 //   flags [N] u8                                              1 B/sig
 //   eidx  [steps][Npad] u32  per-step table entry indices    4 x steps B/sig
-static constexpr int MAX_STEPS = steps<WB, WA_SMALL>::N > steps<WB, WA_BIG>::N ? steps<WB, WA_SMALL>::N
-                                                                              : steps<WB, WA_BIG>::N;
+static constexpr int MAX_STEPS = steps<WB, WA_SMALL>::N;  // the smallest key window has the most steps
+static_assert(steps<WB, WA_SMALL>::N >= steps<WB, WA_MID>::N && steps<WB, WA_MID>::N >= steps<WB, WA_BIG>::N, "");
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static int ensure_work(pbft_ctx* c, uint64_t N) {
   const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
@@ -640,9 +645,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
                      (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
   if (msg_len == PBFT_ENVELOPE_LEN) {
     if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
+    else if (c->wa == WA_MID) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_MID);
     else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
   } else {
     if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(-1, WA_BIG);
+    else if (c->wa == WA_MID) PBFT_LAUNCH_COMB(-1, WA_MID);
     else PBFT_LAUNCH_COMB(-1, WA_SMALL);
   }
 #undef PBFT_LAUNCH_COMB
@@ -731,9 +738,9 @@ const char* pbft_last_error(void) { return g_last_error.c_str(); }
 const char* pbft_build_info(void) {
   static char buf[160];
   snprintf(buf, sizeof buf,
-           "pbft_verify gfx950 WB=%d WA=%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB", WB, WA_BIG,
-           WA_SMALL, BLOCK, comb<WB>::TABLE_WORDS * 4, comb<WA_BIG>::TABLE_WORDS * 4,
-           comb<WA_SMALL>::TABLE_WORDS * 4);
+           "pbft_verify gfx950 WB=%d WA=%d|%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB|%zuB", WB,
+           WA_BIG, WA_MID, WA_SMALL, BLOCK, comb<WB>::TABLE_WORDS * 4, comb<WA_BIG>::TABLE_WORDS * 4,
+           comb<WA_MID>::TABLE_WORDS * 4, comb<WA_SMALL>::TABLE_WORDS * 4);
   return buf;
 }
 
@@ -792,18 +799,30 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->adopt(nullptr);
-  // 16-bit key windows while the key set fits the budget, else 8-bit
-  size_t budget_mb = 65536;
+  // The widest key window whose tables fit the budget (PBFT_KEY_TABLE_BUDGET_MB, default 96 GiB of the
+  // 288 GB HBM) and the free memory: 18-bit (252 MB/key, <= 390 keys by default), 16-bit (67 MB/key), else
+  // 8-bit (0.5 MB/key).  Entry indices are 32-bit (n * P * E < 2^32).
+  size_t budget_mb = 96 * 1024;
   if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  const size_t big = comb<WA_BIG>::TABLE_WORDS * 4 * (size_t)n;
-  // (the line-gather addresses key-table entries with 32-bit indices: n * P * E < 2^32)
-  const bool idx_fits = (uint64_t)n * comb<WA_BIG>::P * comb<WA_BIG>::E < (1ull << 32);
-  const bool use_big = idx_fits && big <= budget_mb * (size_t)1048576 && big + ((size_t)4 << 30) < free_b;
-  const size_t tab_bytes = (use_big ? comb<WA_BIG>::TABLE_WORDS : comb<WA_SMALL>::TABLE_WORDS) * 4 * (size_t)n;
+  auto fits = [&](size_t table_words, uint64_t entries_per_key) {
+    const size_t bytes = table_words * 4 * (size_t)n;
+    return (uint64_t)n * entries_per_key < (1ull << 32) && bytes <= budget_mb * (size_t)1048576 &&
+           bytes + ((size_t)4 << 30) < free_b;
+  };
+  int wa = WA_SMALL;
+  size_t tab_words = comb<WA_SMALL>::TABLE_WORDS;
+  if (fits(comb<WA_BIG>::TABLE_WORDS, (uint64_t)comb<WA_BIG>::P * comb<WA_BIG>::E)) {
+    wa = WA_BIG;
+    tab_words = comb<WA_BIG>::TABLE_WORDS;
+  } else if (fits(comb<WA_MID>::TABLE_WORDS, (uint64_t)comb<WA_MID>::P * comb<WA_MID>::E)) {
+    wa = WA_MID;
+    tab_words = comb<WA_MID>::TABLE_WORDS;
+  }
+  const size_t tab_bytes = tab_words * 4 * (size_t)n;
   keyset* k = new keyset();
-  k->wa = use_big ? WA_BIG : WA_SMALL;
+  k->wa = wa;
   k->n = n;
   if (hipMalloc(&k->d_tabA, tab_bytes) != hipSuccess || hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess ||
       hipMalloc(&k->d_key_ok, n) != hipSuccess) {
@@ -814,8 +833,9 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (hipMemcpyAsync(k->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key upload");
   if (!rc)
-    rc = use_big ? build_tables<WA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
-                 : build_tables<WA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
+    rc = wa == WA_BIG   ? build_tables<WA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+         : wa == WA_MID ? build_tables<WA_MID>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+                        : build_tables<WA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
   if (!rc && key_ok && hipMemcpyAsync(key_ok, k->d_key_ok, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key_ok download");
   if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
@@ -1045,6 +1065,14 @@ int pbft_verify_reserve(pbft_ctx* c, uint64_t max_n) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
   return ensure_work(c, max_n);
+}
+
+int pbft_verify_ctx_info(pbft_ctx* c, uint32_t* wb, uint32_t* wa, uint32_t* n_keys) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (wb) *wb = (uint32_t)WB;
+  if (wa) *wa = (uint32_t)c->wa;
+  if (n_keys) *n_keys = c->n_keys;
+  return PBFT_OK;
 }
 
 float pbft_last_kernel_ms(pbft_ctx* c) {

@@ -9,7 +9,7 @@ products_per_verify(WB, WA) counts the v_mad_u64_u32 products the implemented
 algorithm needs per signature (signed comb windows WB for [s]B and WA for
 [k](-A); Montgomery batch inversion over FIN_M signatures per lane):
   comb       (PB + PA) mixed additions x 7 field muls x 100 products
-             (PB = ceil(254 / WB), PA = ceil(254 / WA); 11 + 16 at 24/16)
+             (PB = ceil(254 / WB), PA = ceil(254 / WA); 10 + 15 at 26/18)
   inversion  (254 squarings x 55 + 11 muls x 100) / FIN_M
   batch      3 muls per signature (prefix, 1/Z_m, running inverse) +
              2 affine muls (x, y), x 100
@@ -42,14 +42,14 @@ def gather_bytes_per_verify(wb: int, wa: int) -> int:
 
 
 def windows_from_build_info(info: str):
-    """(WB, WA_big) from pbft_build_info(), e.g. 'pbft_verify gfx950 WB=24 WA=16|8 ...'."""
+    """(WB, WA_big) from pbft_build_info(), e.g. 'pbft_verify gfx950 WB=26 WA=18|16|8 ...'."""
     m = re.search(r"WB=(\d+) WA=(\d+)", info)
     if not m:
         raise ValueError(f"unexpected build info: {info!r}")
     return int(m.group(1)), int(m.group(2))
 
 
-# defaults of the shipped build (WB = 24, WA = 16)
-WB = 24
-WA = 16
+# defaults of the shipped build (WB = 26, WA = 18 for n <= 390 keys)
+WB = 26
+WA = 18
 PRODUCTS_PER_VERIFY = products_per_verify(WB, WA)

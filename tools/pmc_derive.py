@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""profiles/<run>/derived.json from rocprofv3 --pmc pass CSVs of the verify launch pair (read by bench.py).
+
+usage: python tools/pmc_derive.py PMC_DIR WB WA [n_sigs]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+d, wb, wa = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+n = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
+
+
+def agg(name):
+    vals = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(d, "*.csv")):
+        for r in csv.DictReader(open(f)):
+            if name in r.get("Kernel_Name", ""):
+                vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}
+
+
+out = {"launch": f"comb_kernel<85,{wa}> (WB={wb}) + finish_kernel, one 2^20-signature round", "sigs_per_launch": n}
+tot = 0.0
+for k in ("comb_kernel", "finish_kernel"):
+    m = agg(k)
+    fb, wbytes = 2 * m["FETCH_SIZE"] * 1024, m["WRITE_SIZE"] * 1024
+    out[k] = {"fetch_bytes": fb, "write_bytes": wbytes, "valu_busy_pct": m.get("VALUBusy"),
+              "valu_lane_utilisation_pct": m.get("VALUUtilization"),
+              "valu_insts_per_lane": m["SQ_INSTS_VALU"] / m["SQ_WAVES"], "waves": m["SQ_WAVES"]}
+    tot += fb + wbytes
+out["traffic_bytes_per_launch"] = tot
+out["note"] = ("rocprofv3 --pmc passes (one counter group per run, no tracing) of `python3 bench.py --steps 5 "
+               "--warmup 1 --no-cpu --latency-iters 0` (tools/gpu_pmc_cur.sh); FETCH_SIZE (KB) doubled per the "
+               "gfx950 correction of MI355X_MICROARCH.md's HBM section; WRITE_SIZE taken as is")
+json.dump(out, open(os.path.join(d, "derived.json"), "w"), indent=1)
+print(json.dumps(out, indent=1))
