@@ -342,27 +342,36 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   const uint8_t* tB = (const uint8_t*)tabB;
   const uint8_t* tA = (const uint8_t*)tabA;
   const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // chunk c of my entry at rd0 ^ (16 c)
-  ge P;
-  ge_identity(P);
+  // this lane's entry from the LDS buffer (after its DMA landed: vmcnt(0)); the ds_reads use integer LDS
+  // addresses, so the compiler cannot see that they alias the DMA's writes -- hence the explicit wait
+  auto read_entry = [&](niels& q) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    asm volatile("" ::: "memory");
+    uint32_t w[32];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4 v = lds_read16(rd0 ^ (16u * c));
+      w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
+  };
   // (each lane re-reads only the indices it wrote itself: no barrier needed)
   dma_entry_lines(ST::is_a(0) ? tA : tB, eidx[i], lane, ebuf);
   uint32_t nidx = eidx[Npad + i];
-  for (int j = 0; j < ST::N; ++j) {
-    // The entry's DMA must have landed: the ds_reads below use integer LDS
-    // addresses, so the compiler cannot see that they alias the DMA's writes.
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    asm volatile("" ::: "memory");
+  ge P;
+  {
+    // step 0: P = +-T_B[0][s_0] directly (1 multiplication instead of a 7-multiplication addition)
     niels q;
-    {
-      uint32_t w[32];
-#pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        const u32x4 v = lds_read16(rd0 ^ (16u * c));
-        w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-      }
-#pragma unroll
-      for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
-    }
+    read_entry(q);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): entry in VGPRs before the DMA reuses the buffer
+    dma_entry_lines(ST::is_a(1) ? tA : tB, nidx, lane, ebuf);
+    nidx = eidx[2 * Npad + i];
+    ge_from_niels_signed(P, q, (uint32_t)sgn & 1u);
+  }
+  for (int j = 1; j < ST::N; ++j) {
+    niels q;
+    read_entry(q);
     if (j + 1 < ST::N) {
       // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
