@@ -435,6 +435,9 @@ struct fin_unroll<0> {
 };
 
 // M signatures per lane: lane l of wave w handles i = (w * M + m) * 64 + l.
+// M = FIN_M (16) for large rounds; small batches use fewer signatures per lane
+// so that more waves share the latency-bound inversion chains (launch_verify).
+template <int FM>
 __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const uint8_t* __restrict__ R,
                                                        uint32_t rs_stride,
                                                        const uint32_t* __restrict__ xyz,
@@ -442,14 +445,14 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
                                                        uint64_t* __restrict__ bitmap) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
-  const uint64_t base = wave * FIN_M * 64 + lane;
-  if (wave * FIN_M * 64 >= N) return;
+  const uint64_t base = wave * FM * 64 + lane;
+  if (wave * FM * 64 >= N) return;
   const uint32_t* Xb = xyz;
   const uint32_t* Yb = xyz + 10 * N;
   const uint32_t* Zb = xyz + 20 * N;
   // prefix products of Z (lanes past N contribute 1)
-  fe pre[FIN_M];
-  fin_unroll<FIN_M>::up([&](auto mc) {
+  fe pre[FM];
+  fin_unroll<FM>::up([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
     fe z;
@@ -458,8 +461,8 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
     else fe_mul(pre[m], pre[m - 1], z);
   });
   fe inv;
-  fe_invert(inv, pre[FIN_M - 1]);
-  fin_unroll<FIN_M>::down([&](auto mc) {
+  fe_invert(inv, pre[FM - 1]);
+  fin_unroll<FM>::down([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
     const bool live = i < N;
@@ -488,7 +491,7 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
     for (int t = 0; t < 8; ++t) eq = eq && yw[t] == ry[t];
     const bool ok = live && flags[ii] && eq && !y_is_small_order(yw);
     const uint64_t vote = __ballot(ok);
-    if (lane == 0 && live) bitmap[(wave * FIN_M + m)] = vote;
+    if (lane == 0 && live) bitmap[(wave * FM + m)] = vote;
   });
 }
 
@@ -643,7 +646,9 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
   int rc = ensure_work(c, N);
   if (rc) return rc;
+#if !PBFT_NO_LAUNCH_EVENTS
   HIP_TRY(hipEventRecord(c->ev0, st));
+#endif
   const dim3 g((unsigned)blocks), b(BLOCK);
   uint32_t* xyz = (uint32_t*)c->d_work;
   uint8_t* flags = c->d_work + 120 * N;
@@ -663,12 +668,20 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   }
 #undef PBFT_LAUNCH_COMB
   HIP_TRY(hipGetLastError());
-  const uint64_t fin_waves = (N + 64 * FIN_M - 1) / (64 * FIN_M);
-  const uint64_t fin_blocks = (fin_waves * 64 + BLOCK - 1) / BLOCK;
-  hipLaunchKernelGGL(finish_kernel, dim3((unsigned)fin_blocks), dim3(BLOCK), 0, st, dR, rs_stride, xyz, flags, N,
-                     dB);
+  // signatures per finish lane: as many as keep >= one wave per SIMD (1,024 waves) busy
+  const int fm = N >= (uint64_t)64 * 1024 * FIN_M ? FIN_M : N >= (uint64_t)64 * 1024 * 4 ? 4 : 1;
+#define PBFT_LAUNCH_FIN(M_)                                                                                 \
+  hipLaunchKernelGGL(finish_kernel<M_>, dim3((unsigned)((((N + 64 * M_ - 1) / (64 * M_)) * 64 + BLOCK - 1) / \
+                                                        BLOCK)),                                           \
+                     dim3(BLOCK), 0, st, dR, rs_stride, xyz, flags, N, dB)
+  if (fm == FIN_M) PBFT_LAUNCH_FIN(FIN_M);
+  else if (fm == 4) PBFT_LAUNCH_FIN(4);
+  else PBFT_LAUNCH_FIN(1);
+#undef PBFT_LAUNCH_FIN
   HIP_TRY(hipGetLastError());
+#if !PBFT_NO_LAUNCH_EVENTS
   HIP_TRY(hipEventRecord(c->ev1, st));
+#endif
   return PBFT_OK;
 }
 

@@ -8,7 +8,8 @@ of 128 B, but issues ~2e4 32x32->64 multiply-accumulates.
 products_per_verify(WB, WA) counts the v_mad_u64_u32 products the implemented
 algorithm needs per signature (signed comb windows WB for [s]B and WA for
 [k](-A); Montgomery batch inversion over FIN_M signatures per lane):
-  comb       (PB + PA) mixed additions x 7 field muls x 100 products
+  comb       (PB + PA - 1) mixed additions x 7 field muls x 100 products
+             + 1 mul for the first step, built directly from its table entry
              (PB = ceil(254 / WB), PA = ceil(254 / WA); 10 + 15 at 26/18)
   inversion  (254 squarings x 55 + 11 muls x 100) / FIN_M
   batch      3 muls per signature (prefix, 1/Z_m, running inverse) +
@@ -34,7 +35,7 @@ def positions(w: int) -> int:
 
 
 def products_per_verify(wb: int, wa: int) -> int:
-    return (positions(wb) + positions(wa)) * 7 * 100 + (254 * 55 + 11 * 100) // FIN_M + 5 * 100 + (81 + 44)
+    return ((positions(wb) + positions(wa) - 1) * 7 + 1) * 100 + (254 * 55 + 11 * 100) // FIN_M + 5 * 100 + (81 + 44)
 
 
 def gather_bytes_per_verify(wb: int, wa: int) -> int:

@@ -184,6 +184,11 @@ def test_config4_full_size_properties(gv, coracle):
     sl = slice(int(idx.min()) // 64 * 64, int(idx.min()) // 64 * 64 + 16384)
     exp = oracle_bits(coracle, pub, R2[sl], S2[sl], K2[sl], M2[sl], 85)
     assert (got2[sl] == exp).all()
+    # sub-batch sizes that select the other finish-kernel widths (4 and 1 signatures per lane; the full round
+    # uses 16) and a ragged tail: the same bits as the full-round launch
+    for n in (300_007, 65_536 + 63, 4096):
+        got4, _ = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
+        assert (got4 == got2[:n]).all(), n
 
 
 def test_api_edges_and_async(gv, coracle, golden):

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--replicas", type=int, default=256)
     ap.add_argument("--seqs", type=int, default=2048)
+    ap.add_argument("--per-launch-events", action="store_true", help="also record a torch event pair per launch")
     a = ap.parse_args()
     import torch
     import bench
@@ -63,6 +64,8 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(a.iters):
+                if a.per_launch_events:
+                    torch.cuda.Event(enable_timing=True).record(st)
                 assert lib.pbft_verify_batch_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(),
                                                     85, 85, n, dB.data_ptr(), st.cuda_stream) == 0
             e1.record(st)
