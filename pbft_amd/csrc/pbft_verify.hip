@@ -406,6 +406,159 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   }
 }
 
+// ---- latency mode: SPLIT lanes per signature ---------------------------------
+// For small batches (BASELINE config #5: 4096-signature rounds) one lane per
+// signature leaves most SIMDs idle and the round takes one lane's serial time.
+// comb_split_kernel gives every signature SPLIT = 4 lanes: each lane computes
+// the challenge hash itself (redundantly: it is on the critical path anyway),
+// then the steps j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a
+// step in the last round add the identity entry), and the 4 partial points are
+// summed with two shuffle + extended-addition rounds.  ~2x lower latency per
+// round, ~1.3x the VALU work per signature; used for batches < 2^16 signatures.
+static constexpr int SPLIT = 4;
+#ifndef PBFT_SPLIT_BELOW
+#define PBFT_SPLIT_BELOW 65536
+#endif
+static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_split_kernel
+
+// Line-coalesced gather with per-lane 64-bit entry addresses (the split kernel's
+// lanes of one wave gather from both tables in the same step).
+__device__ __forceinline__ void dma_entry_lines64(const uint8_t* addr, int lane, uint32_t ebuf_lds) {
+  const int k = lane >> 3;
+  const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
+  const int baddr = k << 2;
+  const uint64_t a = (uint64_t)(uintptr_t)addr;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)(a >> 32));
+    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    __builtin_amdgcn_global_load_lds(src + coff, (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+  }
+}
+
+FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
+#pragma unroll
+  for (int t = 0; t < 10; ++t) out.v[t] = (uint32_t)__shfl_xor((int)in.v[t], mask);
+}
+
+template <int LEN, int WA>
+__global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
+    uint32_t rs_stride, uint32_t k_stride,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
+    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
+    const uint8_t** __restrict__ eaddr) {
+  using ST = steps<WB, WA>;
+  constexpr int EB = comb<WB>::E, EA = comb<WA>::E;
+  constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+  const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;  // global lane, < Lpad
+  const uint64_t i = g / SPLIT;
+  const int r = (int)(g % SPLIT);
+  const bool live = i < N;
+  const uint64_t ii = live ? i : 0;
+  uint32_t sgn = 0;  // bit t: digit of local step t is negative
+  bool s_ok, kok;
+  {
+    uint32_t rr[8], s[8], a[8];
+    load32(rr, R + (size_t)rs_stride * ii);
+    load32(s, S + (size_t)rs_stride * ii);
+    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
+    kok = ki < n_keys;
+    if (!kok) ki = 0;
+    kok = kok && key_ok[ki];
+    {
+      const uint4* kp = (const uint4*)(keys + 8 * ki);
+      const uint4 k0 = kp[0], k1 = kp[1];
+      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+    }
+    s_ok = sc_lt_L(s);
+    uint32_t h[16], k[8];
+    sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * ii, (int)msg_len);
+    sc_reduce512(k, h);
+    const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * comb<WA>::TABLE_WORDS * 4;
+    digit_stream<WB> ds;
+    ds.init(s);
+    digit_stream<WA> dk;
+    dk.init(k);
+#pragma unroll
+    for (int j = 0; j < SPLIT * T; ++j) {
+      if (j < ST::N) {
+        const bool isA = ST::is_a(j);
+        const int d = isA ? dk.next() : ds.next();
+        if (j % SPLIT == r) {
+          const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+          sgn |= (d < 0 ? 1u : 0u) << (j / SPLIT);
+          eaddr[(size_t)(j / SPLIT) * Lpad + g] =
+              isA ? tA + ((size_t)ST::pos(j) * EA + ad) * 128 : (const uint8_t*)tabB + ((size_t)ST::pos(j) * EB + ad) * 128;
+        }
+      } else if (j % SPLIT == r) {
+        eaddr[(size_t)(j / SPLIT) * Lpad + g] = (const uint8_t*)tabB;  // entry 0 of position 0: the identity
+      }
+    }
+  }
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);
+  auto read_entry = [&](niels& q) {
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA landed (integer LDS addresses, see comb_kernel)
+    asm volatile("" ::: "memory");
+    uint32_t w[32];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const u32x4 v = lds_read16(rd0 ^ (16u * c));
+      w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
+    }
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
+  };
+  dma_entry_lines64(eaddr[g], lane, ebuf);
+  const uint8_t* nadr = eaddr[Lpad + g];
+  ge P;
+  {
+    niels q;
+    read_entry(q);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    dma_entry_lines64(nadr, lane, ebuf);
+    if (2 < T) nadr = eaddr[2 * Lpad + g];
+    ge_from_niels_signed(P, q, sgn & 1u);
+  }
+  for (int t = 1; t < T; ++t) {
+    niels q;
+    read_entry(q);
+    if (t + 1 < T) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      dma_entry_lines64(nadr, lane, ebuf);
+      if (t + 2 < T) nadr = eaddr[(size_t)(t + 2) * Lpad + g];
+    }
+    ge_madd_signed(P, P, q, (sgn >> t) & 1u);
+#pragma unroll
+    for (int u = 0; u < 10; ++u) asm("" : "+v"(P.X.v[u]), "+v"(P.Y.v[u]), "+v"(P.Z.v[u]), "+v"(P.T.v[u]));
+  }
+  // sum the SPLIT partial points: lanes r ^ 1, then r ^ 2 (extended addition, complete formulas)
+  static_assert(SPLIT == 4, "two combine rounds");
+  auto combine = [&](int m) {
+    ge Q, Sum;
+    fe_shfl_xor(Q.X, P.X, m); fe_shfl_xor(Q.Y, P.Y, m); fe_shfl_xor(Q.Z, P.Z, m); fe_shfl_xor(Q.T, P.T, m);
+    ge_add(Sum, P, Q);
+    P = Sum;
+  };
+  combine(1);
+  combine(2);
+  if (live && r == 0) {
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      xyz[(size_t)t * N + i] = P.X.v[t];
+      xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
+      xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
+    }
+    flags[i] = (s_ok && kok) ? 1 : 0;
+  }
+}
+
 __device__ __forceinline__ void load_fe(fe& f, const uint32_t* __restrict__ base, uint64_t N, uint64_t i) {
 #pragma unroll
   for (int t = 0; t < 10; ++t) f.v[t] = base[(size_t)t * N + i];
@@ -573,6 +726,7 @@ struct pbft_ctx {
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
   int wa = 0;  // comb window of the installed key tables (WA_BIG, WA_MID or WA_SMALL)
+  uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
@@ -627,7 +781,9 @@ static_assert(steps<WB, WA_SMALL>::N >= steps<WB, WA_MID>::N && steps<WB, WA_MID
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static int ensure_work(pbft_ctx* c, uint64_t N) {
   const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
-  const size_t need = eidx_offset(N) + 4 * (size_t)MAX_STEPS * Npad + 256;
+  // (latency mode: SPLIT lanes per signature, 8-byte entry addresses, ceil(steps / SPLIT) per lane)
+  const size_t split = 8 * (size_t)((MAX_STEPS + SPLIT - 1) / SPLIT) * (Npad * SPLIT + BLOCK);
+  const size_t need = eidx_offset(N) + (4 * (size_t)MAX_STEPS * Npad > split ? 4 * (size_t)MAX_STEPS * Npad : split) + 256;
   if (need <= c->work_cap) return PBFT_OK;
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (c->d_work) HIP_TRY(hipFree(c->d_work));
@@ -657,7 +813,22 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
 #define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
   hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS,             \
                      (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
-  if (msg_len == PBFT_ENVELOPE_LEN) {
+#define PBFT_LAUNCH_SPLIT(LEN_, WA_)                                                                          \
+  hipLaunchKernelGGL((comb_split_kernel<LEN_, WA_>), dim3((unsigned)sblocks), b, (BLOCK / 64) * COMB_LDS_PER_WAVE, \
+                     st, dR, dS, (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Lpad,          \
+                     c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, (const uint8_t**)eidx)
+  if (N < c->split_below) {
+    const uint64_t sblocks = (N * SPLIT + BLOCK - 1) / BLOCK, Lpad = sblocks * BLOCK;
+    if (msg_len == PBFT_ENVELOPE_LEN) {
+      if (c->wa == WA_BIG) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_BIG);
+      else if (c->wa == WA_MID) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_MID);
+      else PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_SMALL);
+    } else {
+      if (c->wa == WA_BIG) PBFT_LAUNCH_SPLIT(-1, WA_BIG);
+      else if (c->wa == WA_MID) PBFT_LAUNCH_SPLIT(-1, WA_MID);
+      else PBFT_LAUNCH_SPLIT(-1, WA_SMALL);
+    }
+  } else if (msg_len == PBFT_ENVELOPE_LEN) {
     if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
     else if (c->wa == WA_MID) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_MID);
     else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
@@ -667,6 +838,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     else PBFT_LAUNCH_COMB(-1, WA_SMALL);
   }
 #undef PBFT_LAUNCH_COMB
+#undef PBFT_LAUNCH_SPLIT
   HIP_TRY(hipGetLastError());
   // signatures per finish lane: as many as keep >= one wave per SIMD (1,024 waves) busy
   const int fm = N >= (uint64_t)64 * 1024 * FIN_M ? FIN_M : N >= (uint64_t)64 * 1024 * 4 ? 4 : 1;
@@ -783,6 +955,7 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   pbft_ctx* c = new pbft_ctx();
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));

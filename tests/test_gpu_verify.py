@@ -313,3 +313,24 @@ def test_wire_records_and_stream_end_to_end(gv, golden):
     assert (v.msg == env).all()
     got = bitmap_to_bool(gv.verify(SigBatch(v.R, v.S, v.key_idx, v.msg, 85)), len(rows))
     assert (got == np.array([i % 17 != 3 for i in range(len(rows))])).all()
+
+
+def test_latency_mode_split_kernel_matches_single_lane(golden):
+    """comb_split_kernel (4 lanes per signature, batches < 2^16) and comb_kernel give identical bitmaps on every
+    golden batch (every adversarial class, every message length)."""
+    from pbft_amd import GpuBatchVerifier
+    results = {}
+    for mode, thr in (("split", "1000000000"), ("single", "0")):
+        os.environ["PBFT_SPLIT_BELOW"] = thr
+        try:
+            v = GpuBatchVerifier(0)
+        finally:
+            del os.environ["PBFT_SPLIT_BELOW"]
+        try:
+            for ml, b in golden_batches(golden):
+                v.set_keys(b["keys"])
+                got, _ = verify(v, b["R"], b["S"], b["key_idx"], b["msg"], ml)
+                assert (got == b["expected"].astype(bool)).all(), (mode, ml)
+                results[(mode, ml)] = got
+        finally:
+            v.close()
