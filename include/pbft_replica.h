@@ -31,6 +31,7 @@
 #ifndef PBFT_REPLICA_H
 #define PBFT_REPLICA_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #include "pbft_verify.h"
@@ -89,6 +90,14 @@ int pbft_replica_on_pre_prepare(pbft_replica *r, uint64_t view, uint64_t seq, co
 /* Ingress of a signed Prepare/Commit from replica `signer` (sig = R || S). */
 int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]);
+
+/* Ingress straight from the wire (include/pbft_wire.h): decode a byte stream of
+ * UviBytes frames (src/protocol_config.rs:50-76 upgrade_inbound) and push every
+ * signed Prepare / Commit into its round window; other frames are counted in
+ * *dropped.  *consumed = bytes of whole frames (keep the rest for the next read).
+ * Returns 0, or PBFT_EINVAL on a framing error. */
+int pbft_replica_push_frames(pbft_replica *r, const uint8_t *stream, size_t len, uint64_t *consumed,
+                             uint64_t *pushed, uint64_t *dropped);
 
 /* Verify every closed round window in one batch (force = also open windows),
  * insert the accepted votes and report newly reached quorums. */

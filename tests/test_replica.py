@@ -110,3 +110,44 @@ def test_pipelined_windows_one_batch():
     st = c.stats(0)
     assert st["batches"] == 1 and st["verified"] == 64
     c.close()
+
+
+def test_round_from_wire_frames():
+    """Votes arrive as UviBytes/JSON frames (pbft_replica_push_frames): split reads, reference-format unsigned
+    votes, a PrePrepare and a corrupt frame are dropped; the round still prepares and commits (f = 1)."""
+    import ctypes
+    from pbft_amd import wire
+    c = Cluster(4)
+    L = c.L
+    vp = ctypes.c_void_p
+    L.pbft_replica_push_frames.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t, vp, vp, vp]
+    for i in range(4):
+        assert L.pbft_replica_on_pre_prepare(c.reps[i], 1, 1, OP, len(OP), D, None) == 1
+    frames = []
+    for kind in (KIND_PREPARE, KIND_COMMIT):
+        for s in range(4):
+            frames.append(wire.encode_frame(wire.WireMsg(kind=kind, view=1, seq=1, digest=D, replica=s,
+                                                         sig=c.sign(s, kind, 1, 1, D))))
+        frames.append(wire.encode_frame(wire.WireMsg(kind=kind, view=1, seq=1, digest=D)))  # unsigned
+    frames.append(wire.encode_frame(wire.WireMsg(kind=wire.PREPREPARE, view=1, seq=1, digest=D, operation=OP,
+                                                 client="127.0.0.1:9000")))
+    frames.append(wire.uvi_encode(3) + b"{x}")
+    stream = b"".join(frames)
+    for r in range(4):
+        cut = 37 + 11 * r  # a read boundary inside the first frame, then the rest
+        tot_p = tot_d = 0
+        buf = stream[:cut]
+        rest = stream[cut:]
+        for chunk in (None, rest):
+            if chunk is not None:
+                buf += chunk
+            used, pushed, dropped = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+            assert L.pbft_replica_push_frames(c.reps[r], buf, len(buf), ctypes.byref(used), ctypes.byref(pushed),
+                                              ctypes.byref(dropped)) == 0
+            buf = buf[used.value:]
+            tot_p += pushed.value
+            tot_d += dropped.value
+        assert buf == b"" and tot_p == 8 and tot_d == 4
+        evs = c.flush(r)
+        assert (1, 1, EV_PREPARED) in evs and (1, 1, EV_COMMITTED) in evs
+    c.close()
