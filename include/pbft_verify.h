@@ -76,6 +76,14 @@ int pbft_verify_batch(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const u
                       const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                       uint64_t *bitmap_out);
 
+/* The same batch sharded over n_ctx distinct contexts (several GPUs of this
+ * process and/or cloned contexts of one GPU): contiguous 64-aligned shards,
+ * launched concurrently, bitmap words written in place.  Blocking.  (One
+ * process per GPU with an RCCL all-gather is the other layout: bench.py.) */
+int pbft_verify_batch_multi(pbft_ctx *const *ctxs, uint32_t n_ctx, const uint8_t *R, const uint8_t *S,
+                            const uint16_t *key_idx, const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride,
+                            uint64_t N, uint64_t *bitmap_out);
+
 /* Non-blocking form: enqueue copies + kernel; the host buffers must stay valid
  * until pbft_verify_wait returns.  One batch in flight per context. */
 int pbft_verify_batch_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,

@@ -1106,6 +1106,37 @@ int pbft_verify_wait(pbft_ctx* c) {
   return finish_async(c);
 }
 
+// One host batch over several contexts (GPUs of this process, or cloned contexts
+// of one GPU): contiguous 64-aligned shards, one async launch per context, each
+// writing its own bitmap words in place (no exchange needed when
+// the bitmaps return to one host process).
+int pbft_verify_batch_multi(pbft_ctx* const* ctxs, uint32_t n_ctx, const uint8_t* R, const uint8_t* S,
+                            const uint16_t* K, const uint8_t* M, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                            uint64_t* out) {
+  if (!ctxs || n_ctx == 0) return set_err(PBFT_EINVAL, "no contexts");
+  for (uint32_t i = 0; i < n_ctx; ++i)
+    for (uint32_t j = 0; j < i; ++j)
+      if (!ctxs[i] || ctxs[i] == ctxs[j]) return set_err(PBFT_EINVAL, "contexts must be distinct and non-null");
+  if (!check_batch_args(R, S, K, M, msg_len, msg_stride, N, out)) return set_err(PBFT_EINVAL, "bad batch arguments");
+  if (N == 0) return PBFT_OK;
+  const uint64_t words = (N + 63) / 64, per = (words + n_ctx - 1) / n_ctx;
+  int rc = PBFT_OK;
+  uint32_t launched = 0;
+  for (; launched < n_ctx; ++launched) {
+    const uint64_t lo = launched * per * 64;
+    if (lo >= N) break;
+    const uint64_t hi = lo + per * 64 < N ? lo + per * 64 : N;
+    rc = pbft_verify_batch_async(ctxs[launched], R + 32 * lo, S + 32 * lo, K + lo, M ? M + (size_t)msg_stride * lo : M,
+                                 msg_len, msg_stride, hi - lo, out + lo / 64);
+    if (rc) break;
+  }
+  for (uint32_t i = 0; i < launched; ++i) {
+    const int w = pbft_verify_wait(ctxs[i]);
+    if (!rc) rc = w;
+  }
+  return rc;
+}
+
 int pbft_verify_batch_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK,
                              const uint8_t* dM, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB,
                              void* stream) {

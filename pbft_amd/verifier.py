@@ -62,6 +62,17 @@ def bitmap_to_bool(bitmap: np.ndarray, n: int) -> np.ndarray:
     return bits[:n].astype(bool)
 
 
+def verify_multi(verifiers, b: "SigBatch") -> np.ndarray:
+    """pbft_verify_batch_multi: shard one batch over several contexts (GPUs and/or clones); bitmap words."""
+    lib = load()
+    n = len(b)
+    out = np.zeros((n + 63) // 64, dtype=np.uint64)
+    arr = (ctypes.c_void_p * len(verifiers))(*[v._ctx.value for v in verifiers])
+    check(lib.pbft_verify_batch_multi(arr, len(verifiers), _ptr(b.R), _ptr(b.S), _ptr(b.key_idx), _ptr(b.msg),
+                                      b.msg_len, b.msg.shape[1], n, _ptr(out)))
+    return out
+
+
 class GpuBatchVerifier:
     """One HIP context (one GPU).  Not thread-safe: one per host thread."""
 

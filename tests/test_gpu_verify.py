@@ -334,3 +334,21 @@ def test_latency_mode_split_kernel_matches_single_lane(golden):
                 results[(mode, ml)] = got
         finally:
             v.close()
+
+
+def test_verify_batch_multi_shards(gv, golden):
+    """pbft_verify_batch_multi over 3 contexts (cloned on this GPU; distinct GPUs in a multi-GPU process):
+    64-aligned shards, empty trailing shards for tiny N, bitmap identical to one context."""
+    from pbft_amd import SigBatch, bitmap_to_bool, verify_multi
+    b = dict(golden_batches(golden))[85]
+    gv.set_keys(b["keys"])
+    clones = [gv.clone(), gv.clone()]
+    try:
+        exp = b["expected"].astype(bool)
+        for n in (1, 64, 65, 130, len(exp)):
+            batch = SigBatch(b["R"][:n], b["S"][:n], b["key_idx"][:n], b["msg"][:n], 85)
+            got = bitmap_to_bool(verify_multi([gv] + clones, batch), n)
+            assert (got == exp[:n]).all(), n
+    finally:
+        for c in clones:
+            c.close()
