@@ -97,7 +97,7 @@ def cpu_baseline(keys, R, S, key_idx, msg, budget_s: float = 12.0):
                       f"{dt:.1f} s, {cores} threads of oracle/ed25519_oracle.c"}
 
 
-def pmc_traffic(wb: int, wa: int, n: int) -> dict:
+def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_pmc_cur.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
     p = os.path.join(ROOT, "profiles", "r01_pmc_comb", "derived.json")
@@ -105,7 +105,7 @@ def pmc_traffic(wb: int, wa: int, n: int) -> dict:
         d = json.load(open(p))
     except (OSError, ValueError):
         return {}
-    if d.get("sigs_per_launch") != n or f"WB={wb}" not in d.get("launch", "") or f"<85,{wa}>" not in d.get("launch", ""):
+    if d.get("sigs_per_launch") != n or f"PB={pb} PA={pa}" not in d.get("launch", ""):
         return {}
     return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"], "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
             "source": "profiles/r01_pmc_comb/derived.json (PMC passes, not this run)"}
@@ -187,10 +187,7 @@ def main():
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
     from pbft_amd.dist import allgather_bitmap
     from pbft_amd import _lib
-    from pbft_amd.roofline import (INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_per_verify,
-                                   windows_from_build_info)
-    wb, wa = windows_from_build_info(_lib.load().pbft_build_info().decode())
-    PRODUCTS_PER_VERIFY = products_per_verify(wb, wa)
+    from pbft_amd.roofline import INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_per_verify
 
     n_rep, n_seq = args.replicas, args.seqs
     seeds = key_seeds(n_rep)
@@ -201,8 +198,8 @@ def main():
     R, S, pub = v.sign(seeds, key_idx, msg, ENVELOPE)
     key_ok = v.set_keys(pub)
     assert key_ok.all()
-    wb, wa = v.windows()  # the key window set_keys chose for this key set
-    PRODUCTS_PER_VERIFY = products_per_verify(wb, wa)
+    pb, pa = v.positions()  # the key plan set_keys chose for this key set
+    PRODUCTS_PER_VERIFY = products_per_verify(pb, pa)
 
     dev = torch.device("cuda", local)
     d_R = torch.from_numpy(R).to(dev)
@@ -287,7 +284,7 @@ def main():
             stream = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21)),
                       "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
         cpu = None if args.no_cpu else cpu_baseline(pub, R, S, key_idx, msg)
-        pmc = pmc_traffic(wb, wa, n)
+        pmc = pmc_traffic(pb, pa, n)
         line = {
             "metric": "Ed25519 verifies/sec per node (1M-signature PBFT rounds)",
             "value": value,
@@ -309,7 +306,7 @@ def main():
                          "traffic": pmc.get("traffic_bytes_per_launch"),
                          "traffic_source": pmc.get("source"),
                          "valu_busy_pct": pmc.get("valu_busy_pct"),
-                         "gather_bytes_algorithmic": (gather_bytes_per_verify(wb, wa) + INPUT_BYTES) * n, "kernel": f"comb_kernel<85,{wa}> (WB={wb}) + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
+                         "gather_bytes_algorithmic": (gather_bytes_per_verify(pb, pa) + INPUT_BYTES) * n, "kernel": f"comb_kernel<85, plan PA={pa}> (PB={pb}) + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
                          "products_per_verify": PRODUCTS_PER_VERIFY},
             "p50_ms_4k_round": float(np.median(lat)) if lat else None,
             "p99_ms_4k_round": float(np.percentile(lat, 99)) if lat else None,

@@ -2,8 +2,8 @@
 // kernels + the C ABI declared in include/pbft_verify.h.
 //
 // Data layout in HBM (one context = one GPU):
-//   tabB   comb table of the base point, WB-bit signed windows
-//          (comb<WB>::P positions x comb<WB>::E entries x 128 B)
+//   tabB   comb table of the base point, plan PLB (10 positions of 25/26-bit
+//          signed windows, 128-B entries)
 //   tabA   one comb table of -A per replica key, same geometry with WA
 //   keys   raw 32-byte key encodings (hashed as given) + key_ok bytes
 //   batch  SoA: R[N][32], S[N][32], key_idx[N] u16, msg[N][stride]
@@ -29,24 +29,26 @@ using namespace pbft;
 #define PBFT_ENVELOPE_LEN 85
 #define BLOCK 256
 
-// Comb windows.  The base-point table uses 26-bit signed windows: 10 positions x
-// (2^25 + 1) entries x 128 B = 43 GB, one copy per device shared by all
-// contexts -- HBM capacity traded for arithmetic on a VALU-bound path (10
-// instead of 16 mixed additions for [s]B).  Each replica key gets an 18-bit
-// table (15 positions, 252 MB/key) while the key set fits
-// PBFT_KEY_TABLE_BUDGET_MB (default 96 GiB of the 288 GB HBM), else 16-bit
-// (67 MB/key), else 8-bit (0.5 MB/key).  25 steps per signature at n <= 390.
-// DESIGN.md §3-4; measured in profiles/r01_ab_log.md.
-#ifndef PBFT_WB
-#define PBFT_WB 26
+// Comb plans (verify_core.h `plan`): balanced windows over the 254 bits of a
+// signed-digit scalar < 2^253, i.e. the fewest positions (= comb steps) for the
+// HBM they take.  Base point: 10 positions (4 x 26 + 6 x 25 bits), 235M entries
+// x 128 B = 30 GB, one copy per device shared by all contexts.  Replica keys:
+// 14 positions (2 x 19 + 12 x 18 bits, 268 MB per key) while the key set fits
+// PBFT_KEY_TABLE_BUDGET_MB (default 96 GiB of the 288 GB HBM: <= 360 keys),
+// else 16 positions (14 x 16 + 2 x 15, 63 MB), else 32 (30 x 8 + 2 x 7,
+// 0.5 MB).  24 steps per signature at n <= 360.  DESIGN.md §3-4; measured in
+// profiles/r01_ab_log.md.
+#ifndef PBFT_PLAN_B
+#define PBFT_PLAN_B 10, 25, 4
 #endif
-static constexpr int WB = PBFT_WB;
-#ifndef PBFT_WA
-#define PBFT_WA 18
+#ifndef PBFT_PLAN_A
+#define PBFT_PLAN_A 14, 18, 2
 #endif
-static constexpr int WA_BIG = PBFT_WA;  // 15 positions x (2^17 + 1) x 128 B = 252 MB per key
-static constexpr int WA_MID = 16;       // 16 positions x (2^15 + 1) x 128 B =  67 MB per key
-static constexpr int WA_SMALL = 8;      // 32 positions x 129 x 128 B        = 0.5 MB per key
+using PLB = plan<PBFT_PLAN_B>;
+using PLA_BIG = plan<PBFT_PLAN_A>;
+using PLA_MID = plan<16, 15, 14>;
+using PLA_SMALL = plan<32, 7, 30>;
+static_assert(PLA_BIG::P < PLA_MID::P && PLA_MID::P < PLA_SMALL::P, "key plans are told apart by P");
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_last_error;
@@ -69,12 +71,12 @@ static int set_err(int code, const char* what) {
 
 // Comb tables for a set of points given by encoding (negate: tables of -P).
 // Pass 1, one thread per (key, position): decompress, key_ok, and the
-// position's base point 2^(W*pos) * (+-P) by W*pos doublings.
-template <int W>
+// position's base point 2^bitoff(pos) * (+-P) by bitoff(pos) doublings.
+template <class PL>
 __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __restrict__ enc, uint32_t n_keys,
                                                           int negate, ge* __restrict__ bases,
                                                           uint8_t* __restrict__ dec_ok, uint8_t* __restrict__ key_ok) {
-  constexpr int P = comb<W>::P;
+  constexpr int P = PL::P;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= (uint64_t)P * n_keys) return;
   const uint32_t key = (uint32_t)(tid / P);
@@ -90,7 +92,7 @@ __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __rest
   }
   if (!dec) ge_identity(A);
   if (negate) { ge t; ge_neg(t, A); A = t; }
-  for (int i = 0; i < W * pos; ++i) ge_dbl(A, A);
+  for (int i = 0; i < PL::bitoff(pos); ++i) ge_dbl(A, A);
   bases[tid] = A;
 }
 
@@ -100,27 +102,35 @@ __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __rest
 // 1 inversion + 3 muls each), so an entry costs ~15 field multiplications
 // instead of one inversion (~265).  Entry 0 of every position is the identity.
 #define TAB_RUN 16
-template <int W>
+template <class PL>
+__host__ __device__ constexpr uint32_t plan_runs(int pos) { return (PL::entries(pos) - 1 + TAB_RUN - 1) / TAB_RUN; }
+template <class PL>
+__host__ __device__ constexpr uint32_t plan_runs_total() {
+  uint32_t t = 0;
+  for (int p = 0; p < PL::P; ++p) t += plan_runs<PL>(p);
+  return t;
+}
+template <class PL>
 __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict__ bases,
                                                            const uint8_t* __restrict__ dec_ok, uint32_t n_keys,
                                                            uint32_t* __restrict__ tables) {
-  constexpr int P = comb<W>::P, E = comb<W>::E;
-  constexpr uint32_t RUNS = ((1u << (W - 1)) + TAB_RUN - 1) / TAB_RUN;  // entries 1 .. 2^(W-1)
+  constexpr int P = PL::P;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint64_t per_key = (uint64_t)P * RUNS;
+  const uint64_t per_key = plan_runs_total<PL>();  // runs of entries 1 .. 2^(width-1) over all positions
   if (tid >= per_key * n_keys) return;
   const uint32_t key = (uint32_t)(tid / per_key);
-  const uint32_t rem = (uint32_t)(tid % per_key);
-  const int pos = rem / RUNS;
-  const uint32_t run = rem % RUNS;
-  uint32_t* out = tables + (size_t)key * comb<W>::TABLE_WORDS + (size_t)pos * E * 32;
+  uint32_t run = (uint32_t)(tid % per_key);
+  int pos = 0;
+  while (run >= plan_runs<PL>(pos)) run -= plan_runs<PL>(pos++);
+  const uint32_t E = PL::entries(pos);
+  uint32_t* out = tables + (size_t)key * PL::TABLE_WORDS + (size_t)PL::offset(pos) * 32;
   if (run == 0) {
     niels id;
     niels_identity(id);
     store_niels(out, id);
   }
   const uint32_t j0 = 1 + run * TAB_RUN;
-  const uint32_t cnt = min((uint32_t)TAB_RUN, (1u << (W - 1)) + 1 - j0);
+  const uint32_t cnt = min((uint32_t)TAB_RUN, E - j0);
   if (!dec_ok[key]) {
     niels id;
     niels_identity(id);
@@ -165,19 +175,19 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
   }
 }
 
-template <int W>
+template <class PL>
 static int build_tables(const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables, uint8_t* d_key_ok,
                         hipStream_t st) {
   ge* d_bases = nullptr;
   uint8_t* d_dec = nullptr;
-  HIP_TRY(hipMalloc(&d_bases, sizeof(ge) * (size_t)comb<W>::P * n));
+  HIP_TRY(hipMalloc(&d_bases, sizeof(ge) * (size_t)PL::P * n));
   HIP_TRY(hipMalloc(&d_dec, n));
-  const uint64_t t1 = (uint64_t)comb<W>::P * n;
-  hipLaunchKernelGGL(comb_base_kernel<W>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
+  const uint64_t t1 = (uint64_t)PL::P * n;
+  hipLaunchKernelGGL(comb_base_kernel<PL>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
                      negate, d_bases, d_dec, d_key_ok);
   HIP_TRY(hipGetLastError());
-  const uint64_t t2 = (uint64_t)comb<W>::P * (((1u << (W - 1)) + TAB_RUN - 1) / TAB_RUN) * n;
-  hipLaunchKernelGGL(comb_entry_kernel<W>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
+  const uint64_t t2 = (uint64_t)plan_runs_total<PL>() * n;
+  hipLaunchKernelGGL(comb_entry_kernel<PL>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
                      d_dec, n, d_tables);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(st));
@@ -233,9 +243,9 @@ __device__ __forceinline__ u32x4 lds_read16(uint32_t addr) {
 #define FIN_WAVES_PER_EU 1
 #endif
 
-template <int WB_, int WA_>
+template <class PLB_, class PLA_>
 struct steps {
-  static constexpr int PB = comb<WB_>::P, PA = comb<WA_>::P;
+  static constexpr int PB = PLB_::P, PA = PLA_::P;
   static constexpr int PMIN = PB < PA ? PB : PA;
   static constexpr int N = PB + PA;
   static_assert(N <= 64, "sign mask holds one bit per step");
@@ -277,7 +287,7 @@ __device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t id
 #endif
 static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
 
-template <int LEN, int WA>
+template <int LEN, class PLA>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
@@ -285,8 +295,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
     uint32_t* __restrict__ eidx) {
-  using ST = steps<WB, WA>;
-  constexpr int EB = comb<WB>::E, EA = comb<WA>::E;
+  using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
   // wave-uniform LDS base of this wave's entry buffer (SGPR: the DMA's M0)
@@ -320,24 +329,26 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #endif
     sc_reduce512(k, h);
     // per-step entry index (128-B units from the step's table base) and sign
-    const uint32_t keybase = ki * (uint32_t)(comb<WA>::P * EA);
-    digit_stream<WB> ds;
+    const uint32_t keybase = ki * PLA::ENTRIES;
+    digits ds, dk;
     ds.init(s);
-    digit_stream<WA> dk;
     dk.init(k);
-#pragma unroll
-    for (int j = 0; j < ST::N; ++j) {
-      const bool isA = ST::is_a(j);
-      const int d = isA ? dk.next() : ds.next();
+    static_for<ST::N>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr bool isA = ST::is_a(j);
+      constexpr int pos = ST::pos(j);
+      int d;
+      if constexpr (isA) d = dk.template take_pos<PLA, pos>();
+      else d = ds.template take_pos<PLB, pos>();
       const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
       sgn |= (typename ST::mask_t)(d < 0 ? 1u : 0u) << j;
 #if PBFT_ABL_FETCH0  // ablation: every lane gathers entry 1 of its position (L2-resident)
-      const uint32_t e = (uint32_t)ST::pos(j) * (isA ? EA : EB) + 1u;
+      const uint32_t e = (isA ? PLA::offset(pos) : PLB::offset(pos)) + 1u;
 #else
-      const uint32_t e = isA ? keybase + (uint32_t)ST::pos(j) * EA + ad : (uint32_t)ST::pos(j) * EB + ad;
+      const uint32_t e = isA ? keybase + PLA::offset(pos) + ad : PLB::offset(pos) + ad;
 #endif
       eidx[(size_t)j * Npad + i] = e;
-    }
+    });
   }
   const uint8_t* tB = (const uint8_t*)tabB;
   const uint8_t* tA = (const uint8_t*)tabA;
@@ -442,7 +453,7 @@ FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
   for (int t = 0; t < 10; ++t) out.v[t] = (uint32_t)__shfl_xor((int)in.v[t], mask);
 }
 
-template <int LEN, int WA>
+template <int LEN, class PLA>
 __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
@@ -450,8 +461,7 @@ __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
     const uint8_t** __restrict__ eaddr) {
-  using ST = steps<WB, WA>;
-  constexpr int EB = comb<WB>::E, EA = comb<WA>::E;
+  using ST = steps<PLB, PLA>;
   constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -481,26 +491,28 @@ __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
     uint32_t h[16], k[8];
     sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * ii, (int)msg_len);
     sc_reduce512(k, h);
-    const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * comb<WA>::TABLE_WORDS * 4;
-    digit_stream<WB> ds;
+    const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * PLA::TABLE_WORDS * 4;
+    digits ds, dk;
     ds.init(s);
-    digit_stream<WA> dk;
     dk.init(k);
-#pragma unroll
-    for (int j = 0; j < SPLIT * T; ++j) {
-      if (j < ST::N) {
-        const bool isA = ST::is_a(j);
-        const int d = isA ? dk.next() : ds.next();
+    static_for<SPLIT * T>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr (j < ST::N) {
+        constexpr bool isA = ST::is_a(j);
+        constexpr int pos = ST::pos(j);
+        int d;
+        if constexpr (isA) d = dk.template take_pos<PLA, pos>();
+        else d = ds.template take_pos<PLB, pos>();
         if (j % SPLIT == r) {
           const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
           sgn |= (d < 0 ? 1u : 0u) << (j / SPLIT);
           eaddr[(size_t)(j / SPLIT) * Lpad + g] =
-              isA ? tA + ((size_t)ST::pos(j) * EA + ad) * 128 : (const uint8_t*)tabB + ((size_t)ST::pos(j) * EB + ad) * 128;
+              isA ? tA + ((size_t)PLA::offset(pos) + ad) * 128 : (const uint8_t*)tabB + ((size_t)PLB::offset(pos) + ad) * 128;
         }
       } else if (j % SPLIT == r) {
         eaddr[(size_t)(j / SPLIT) * Lpad + g] = (const uint8_t*)tabB;  // entry 0 of position 0: the identity
       }
-    }
+    });
   }
   const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);
   auto read_entry = [&](niels& q) {
@@ -664,7 +676,7 @@ __global__ void __launch_bounds__(BLOCK) sign_kernel(const uint32_t* __restrict_
   uint32_t seed[8], r[8], s[8], a[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) seed[j] = seeds[8 * si + j];
-  sign_lane<WB, LEN>(r, s, a, seed, msg + (size_t)msg_stride * i, (int)msg_len, tabB);
+  sign_lane<PLB, LEN>(r, s, a, seed, msg + (size_t)msg_stride * i, (int)msg_len, tabB);
 #pragma unroll
   for (int j = 0; j < 8; ++j) { R[8 * i + j] = r[j]; S[8 * i + j] = s[j]; }
   (void)n_seeds;
@@ -706,7 +718,7 @@ struct keyset {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n = 0;
-  int wa = 0;
+  int pa = 0;  // positions of the key plan (identifies PLA_BIG / PLA_MID / PLA_SMALL)
 };
 static void keyset_release(keyset* k) {
   if (k && --k->refs == 0) {
@@ -725,13 +737,13 @@ struct pbft_ctx {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
-  int wa = 0;  // comb window of the installed key tables (WA_BIG, WA_MID or WA_SMALL)
+  int pa = 0;  // comb positions of the installed key tables' plan (PLA_BIG, PLA_MID or PLA_SMALL)
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
     d_tabA = k ? k->d_tabA : nullptr; d_keys = k ? k->d_keys : nullptr; d_key_ok = k ? k->d_key_ok : nullptr;
-    n_keys = k ? k->n : 0; wa = k ? k->wa : 0;
+    n_keys = k ? k->n : 0; pa = k ? k->pa : 0;
   }
   // staging for the host-buffer API
   uint8_t* d_stage = nullptr;
@@ -776,8 +788,9 @@ static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
 //   xyz   [30][N] u32   R' limbs, comb -> finish            120 B/sig
 //   flags [N] u8                                              1 B/sig
 //   eidx  [steps][Npad] u32  per-step table entry indices    4 x steps B/sig
-static constexpr int MAX_STEPS = steps<WB, WA_SMALL>::N;  // the smallest key window has the most steps
-static_assert(steps<WB, WA_SMALL>::N >= steps<WB, WA_MID>::N && steps<WB, WA_MID>::N >= steps<WB, WA_BIG>::N, "");
+static constexpr int MAX_STEPS = steps<PLB, PLA_SMALL>::N;  // the smallest key plan has the most steps
+static_assert(steps<PLB, PLA_SMALL>::N >= steps<PLB, PLA_MID>::N && steps<PLB, PLA_MID>::N >= steps<PLB, PLA_BIG>::N,
+              "");
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static int ensure_work(pbft_ctx* c, uint64_t N) {
   const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
@@ -820,22 +833,22 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   if (N < c->split_below) {
     const uint64_t sblocks = (N * SPLIT + BLOCK - 1) / BLOCK, Lpad = sblocks * BLOCK;
     if (msg_len == PBFT_ENVELOPE_LEN) {
-      if (c->wa == WA_BIG) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_BIG);
-      else if (c->wa == WA_MID) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_MID);
-      else PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, WA_SMALL);
+      if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_BIG);
+      else if (c->pa == PLA_MID::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_MID);
+      else PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_SMALL);
     } else {
-      if (c->wa == WA_BIG) PBFT_LAUNCH_SPLIT(-1, WA_BIG);
-      else if (c->wa == WA_MID) PBFT_LAUNCH_SPLIT(-1, WA_MID);
-      else PBFT_LAUNCH_SPLIT(-1, WA_SMALL);
+      if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(-1, PLA_BIG);
+      else if (c->pa == PLA_MID::P) PBFT_LAUNCH_SPLIT(-1, PLA_MID);
+      else PBFT_LAUNCH_SPLIT(-1, PLA_SMALL);
     }
   } else if (msg_len == PBFT_ENVELOPE_LEN) {
-    if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_BIG);
-    else if (c->wa == WA_MID) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_MID);
-    else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, WA_SMALL);
+    if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_BIG);
+    else if (c->pa == PLA_MID::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_MID);
+    else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_SMALL);
   } else {
-    if (c->wa == WA_BIG) PBFT_LAUNCH_COMB(-1, WA_BIG);
-    else if (c->wa == WA_MID) PBFT_LAUNCH_COMB(-1, WA_MID);
-    else PBFT_LAUNCH_COMB(-1, WA_SMALL);
+    if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(-1, PLA_BIG);
+    else if (c->pa == PLA_MID::P) PBFT_LAUNCH_COMB(-1, PLA_MID);
+    else PBFT_LAUNCH_COMB(-1, PLA_SMALL);
   }
 #undef PBFT_LAUNCH_COMB
 #undef PBFT_LAUNCH_SPLIT
@@ -886,7 +899,7 @@ static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
 }
 
 // The base-point comb table is a constant of the curve: one copy per device,
-// shared by every context on it (reference-counted; at WB = 24 it is 11.8 GB).
+// shared by every context on it (reference-counted; 30 GB with the default plan).
 static std::mutex g_tabB_mu;
 static uint32_t* g_tabB[64] = {};
 static int g_tabB_refs[64] = {};
@@ -901,12 +914,12 @@ static int acquire_base_table(int device, hipStream_t st, uint32_t** out) {
     uint32_t* d_benc = nullptr;
     uint32_t* tab = nullptr;
     HIP_TRY(hipMalloc(&d_benc, 32));
-    if (hipMalloc(&tab, comb<WB>::TABLE_WORDS * 4) != hipSuccess) {
+    if (hipMalloc(&tab, PLB::TABLE_WORDS * 4) != hipSuccess) {
       (void)hipFree(d_benc);
       return set_err(PBFT_ENOMEM, "base-point table alloc");
     }
     HIP_TRY(hipMemcpyAsync(d_benc, benc, 32, hipMemcpyHostToDevice, st));
-    int rc = build_tables<WB>(d_benc, 1u, 0, tab, nullptr, st);
+    int rc = build_tables<PLB>(d_benc, 1u, 0, tab, nullptr, st);
     (void)hipFree(d_benc);
     if (rc) { (void)hipFree(tab); return rc; }
     g_tabB[device] = tab;
@@ -930,11 +943,11 @@ extern "C" {
 const char* pbft_last_error(void) { return g_last_error.c_str(); }
 
 const char* pbft_build_info(void) {
-  static char buf[160];
+  static char buf[256];
   snprintf(buf, sizeof buf,
-           "pbft_verify gfx950 WB=%d WA=%d|%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB|%zuB", WB,
-           WA_BIG, WA_MID, WA_SMALL, BLOCK, comb<WB>::TABLE_WORDS * 4, comb<WA_BIG>::TABLE_WORDS * 4,
-           comb<WA_MID>::TABLE_WORDS * 4, comb<WA_SMALL>::TABLE_WORDS * 4);
+           "pbft_verify gfx950 PB=%d PA=%d|%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB|%zuB", PLB::P,
+           PLA_BIG::P, PLA_MID::P, PLA_SMALL::P, BLOCK, PLB::TABLE_WORDS * 4, PLA_BIG::TABLE_WORDS * 4,
+           PLA_MID::TABLE_WORDS * 4, PLA_SMALL::TABLE_WORDS * 4);
   return buf;
 }
 
@@ -1006,18 +1019,18 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
     return (uint64_t)n * entries_per_key < (1ull << 32) && bytes <= budget_mb * (size_t)1048576 &&
            bytes + ((size_t)4 << 30) < free_b;
   };
-  int wa = WA_SMALL;
-  size_t tab_words = comb<WA_SMALL>::TABLE_WORDS;
-  if (fits(comb<WA_BIG>::TABLE_WORDS, (uint64_t)comb<WA_BIG>::P * comb<WA_BIG>::E)) {
-    wa = WA_BIG;
-    tab_words = comb<WA_BIG>::TABLE_WORDS;
-  } else if (fits(comb<WA_MID>::TABLE_WORDS, (uint64_t)comb<WA_MID>::P * comb<WA_MID>::E)) {
-    wa = WA_MID;
-    tab_words = comb<WA_MID>::TABLE_WORDS;
+  int pa = PLA_SMALL::P;
+  size_t tab_words = PLA_SMALL::TABLE_WORDS;
+  if (fits(PLA_BIG::TABLE_WORDS, PLA_BIG::ENTRIES)) {
+    pa = PLA_BIG::P;
+    tab_words = PLA_BIG::TABLE_WORDS;
+  } else if (fits(PLA_MID::TABLE_WORDS, PLA_MID::ENTRIES)) {
+    pa = PLA_MID::P;
+    tab_words = PLA_MID::TABLE_WORDS;
   }
   const size_t tab_bytes = tab_words * 4 * (size_t)n;
   keyset* k = new keyset();
-  k->wa = wa;
+  k->pa = pa;
   k->n = n;
   if (hipMalloc(&k->d_tabA, tab_bytes) != hipSuccess || hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess ||
       hipMalloc(&k->d_key_ok, n) != hipSuccess) {
@@ -1028,9 +1041,9 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (hipMemcpyAsync(k->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key upload");
   if (!rc)
-    rc = wa == WA_BIG   ? build_tables<WA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
-         : wa == WA_MID ? build_tables<WA_MID>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
-                        : build_tables<WA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
+    rc = pa == PLA_BIG::P   ? build_tables<PLA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+         : pa == PLA_MID::P ? build_tables<PLA_MID>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+                            : build_tables<PLA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
   if (!rc && key_ok && hipMemcpyAsync(key_ok, k->d_key_ok, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key_ok download");
   if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
@@ -1293,10 +1306,10 @@ int pbft_verify_reserve(pbft_ctx* c, uint64_t max_n) {
   return ensure_work(c, max_n);
 }
 
-int pbft_verify_ctx_info(pbft_ctx* c, uint32_t* wb, uint32_t* wa, uint32_t* n_keys) {
+int pbft_verify_ctx_info(pbft_ctx* c, uint32_t* pb, uint32_t* pa, uint32_t* n_keys) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
-  if (wb) *wb = (uint32_t)WB;
-  if (wa) *wa = (uint32_t)c->wa;
+  if (pb) *pb = (uint32_t)PLB::P;
+  if (pa) *pa = (uint32_t)c->pa;
   if (n_keys) *n_keys = c->n_keys;
   return PBFT_OK;
 }

@@ -22,15 +22,36 @@
 #include "sc25519.h"
 #include "sha512.h"
 
+#include <type_traits>
+
 namespace pbft {
 
-// Table geometry for window W: positions P = ceil(254/W), entries 2^(W-1)+1.
-template <int W>
-struct comb {
-  static constexpr int P = (254 + W - 1) / W;
-  static constexpr int E = (1 << (W - 1)) + 1;
+// Comb table geometry ("plan") over the 254 bits a signed-digit recoding of a
+// scalar < 2^253 needs: P positions, the first NB with windows of W+1 bits, the
+// rest W bits (P*W + NB >= 254; balanced plans use exactly 254).  Position pos
+// starts at bit bitoff(pos) and holds entries j * 2^bitoff(pos) * P0 for
+// j = 0 .. 2^(width-1) (entry 0 = identity) at entry offset(pos) of the table.
+template <int P_, int W_, int NB_ = 0>
+struct plan {
+  static_assert(P_ * W_ + NB_ >= 254 && NB_ <= P_, "windows must cover 254 bits");
+  static constexpr int P = P_;
+  __host__ __device__ static constexpr int width(int pos) { return pos < NB_ ? W_ + 1 : W_; }
+  __host__ __device__ static constexpr uint32_t entries(int pos) { return (1u << (width(pos) - 1)) + 1u; }
+  __host__ __device__ static constexpr uint32_t offset(int pos) {
+    return pos <= NB_ ? (uint32_t)pos * ((1u << W_) + 1u)
+                      : (uint32_t)NB_ * ((1u << W_) + 1u) + (uint32_t)(pos - NB_) * ((1u << (W_ - 1)) + 1u);
+  }
+  __host__ __device__ static constexpr int bitoff(int pos) {
+    return pos <= NB_ ? pos * (W_ + 1) : NB_ * (W_ + 1) + (pos - NB_) * W_;
+  }
+  static constexpr uint32_t ENTRIES = offset(P_);
   static constexpr int ENTRY_WORDS = 32;  // 30 limbs + 2 pad = 128 B
-  static constexpr size_t TABLE_WORDS = (size_t)P * E * ENTRY_WORDS;
+  static constexpr size_t TABLE_WORDS = (size_t)ENTRIES * ENTRY_WORDS;
+};
+// uniform windows of W bits: positions P = ceil(254/W), entries 2^(W-1)+1 each
+template <int W>
+struct comb : plan<(254 + W - 1) / W, W, 0> {
+  static constexpr uint32_t E = (1u << (W - 1)) + 1u;
 };
 
 FE_FN void store_niels(uint32_t* dst, const niels& n) {
@@ -137,10 +158,13 @@ FE_FN void ge_from_niels_signed(ge& P, const niels& q, bool neg) {
   P.Z.v[0] = 2;
 }
 
-// Signed radix-2^W digit stream over a 256-bit scalar held in 8 words.
-// next() returns the digit of the lowest remaining window and shifts.
-template <int W>
-struct digit_stream {
+// Signed-digit stream over a scalar < 2^253 held in 8 words, one window at a
+// time from the bottom: take<W>() returns the next W-bit window's digit in
+// [-2^(W-1), 2^(W-1)) and carries; take_last<W>() returns the top window's
+// digit without recoding, in [0, 2^(W-1)] (the scalar's bit 253 is 0, so the
+// top window plus the incoming carry never exceeds that: every table has the
+// entry 2^(W-1)).  Digit i of a plan is the take at width(i) (take_last at P-1).
+struct digits {
   uint32_t w[8];
   uint32_t carry;
   FE_FN void init(const uint32_t s[8]) {
@@ -148,7 +172,8 @@ struct digit_stream {
     for (int i = 0; i < 8; ++i) w[i] = s[i];
     carry = 0;
   }
-  FE_FN int next() {
+  template <int W>
+  FE_FN int take() {
     const uint32_t mask = (1u << W) - 1u;
     int d = (int)((w[0] & mask) + carry);
 #pragma unroll
@@ -156,6 +181,16 @@ struct digit_stream {
     w[7] >>= W;
     carry = (d >= (1 << (W - 1))) ? 1u : 0u;
     return d - (int)(carry << W);
+  }
+  template <int W>
+  FE_FN int take_last() {
+    return (int)((w[0] & ((1u << W) - 1u)) + carry);
+  }
+  // the digit of position pos of plan PL (positions taken in order)
+  template <class PL, int pos>
+  FE_FN int take_pos() {
+    if constexpr (pos == PL::P - 1) return take_last<PL::width(pos)>();
+    else return take<PL::width(pos)>();
   }
 };
 
@@ -193,9 +228,18 @@ FE_FN void canon_y(uint32_t y[8], const uint32_t enc[8]) {
   }
 }
 
-// The complete per-lane check.  tabB: B comb table; tabA: the -A comb table of
-// this lane's key; a_enc: raw key encoding (hashed as given).
-template <int WB, int WA, int LEN>
+// Compile-time loop: f(std::integral_constant<int, i>) for i = 0 .. N-1.
+template <int N, int I = 0, class F>
+FE_FN void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>());
+    static_for<N, I + 1>(f);
+  }
+}
+
+// The complete per-lane check.  PLB / PLA: plans of the B table and of this
+// lane's -A table; a_enc: raw key encoding (hashed as given).
+template <class PLB, class PLA, int LEN>
 FE_FN bool verify_lane(const uint32_t r_enc[8], const uint32_t s[8], const uint32_t a_enc[8], bool key_ok,
                        const uint8_t* msg, int len, const uint32_t* tabB, const uint32_t* tabA) {
   const bool s_ok = sc_lt_L(s);
@@ -204,30 +248,28 @@ FE_FN bool verify_lane(const uint32_t r_enc[8], const uint32_t s[8], const uint3
   sc_reduce512(k, h);
 
   ge P;
-  digit_stream<WB> ds;
+  digits ds, dk;
   ds.init(s);
-  digit_stream<WA> dk;
   dk.init(k);
-  constexpr int PB = comb<WB>::P, EB = comb<WB>::E;
-  constexpr int PA = comb<WA>::P, EA = comb<WA>::E;
-  constexpr int PMAX = PB > PA ? PB : PA;
-  for (int i = 0; i < PMAX; ++i) {
-    if (i < PB) {
-      const int d = ds.next();
+  constexpr int PB = PLB::P, PA = PLA::P;
+  static_for<(PB > PA ? PB : PA)>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    if constexpr (i < PB) {
+      const int d = ds.template take_pos<PLB, i>();
       const int ad = d < 0 ? -d : d;
       niels q;
-      load_niels(q, tabB + ((size_t)i * EB + ad) * 32);
+      load_niels(q, tabB + ((size_t)PLB::offset(i) + ad) * 32);
       if (i == 0) ge_from_niels_signed(P, q, d < 0);  // first step: no addition
       else ge_madd_signed(P, P, q, d < 0);
     }
-    if (i < PA) {
-      const int d = dk.next();
+    if constexpr (i < PA) {
+      const int d = dk.template take_pos<PLA, i>();
       const int ad = d < 0 ? -d : d;
       niels q;
-      load_niels(q, tabA + ((size_t)i * EA + ad) * 32);
+      load_niels(q, tabA + ((size_t)PLA::offset(i) + ad) * 32);
       ge_madd_signed(P, P, q, d < 0);
     }
-  }
+  });
 
   fe zi, x, y;
   fe_invert(zi, P.Z);
@@ -243,19 +285,20 @@ FE_FN bool verify_lane(const uint32_t r_enc[8], const uint32_t s[8], const uint3
   return s_ok && key_ok && eq && !y_is_small_order(yw);
 }
 
-// [k]B for k < 2^253 with the base-point comb table (RFC 8032 signing side).
-template <int W>
+// [k]B for k < 2^253 with the base-point comb table of plan PL (RFC 8032 signing side).
+template <class PL>
 FE_FN void comb_mul_base(ge& P, const uint32_t k[8], const uint32_t* tabB) {
-  digit_stream<W> ds;
+  digits ds;
   ds.init(k);
-  for (int i = 0; i < comb<W>::P; ++i) {
-    const int d = ds.next();
+  static_for<PL::P>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int d = ds.template take_pos<PL, i>();
     const int ad = d < 0 ? -d : d;
     niels q;
-    load_niels(q, tabB + ((size_t)i * comb<W>::E + ad) * 32);
+    load_niels(q, tabB + ((size_t)PL::offset(i) + ad) * 32);
     if (i == 0) ge_from_niels_signed(P, q, d < 0);
     else ge_madd_signed(P, P, q, d < 0);
-  }
+  });
 }
 
 FE_FN void ge_compress_words(uint32_t enc[8], const ge& P) {
@@ -271,7 +314,7 @@ FE_FN void ge_compress_words(uint32_t enc[8], const ge& P) {
 
 // RFC 8032 Ed25519 signature of M under secret seed (8 LE words).
 // Outputs R and S encodings (8 LE words each) and the public key A.
-template <int W, int LEN>
+template <class PL, int LEN>
 FE_FN void sign_lane(uint32_t r_out[8], uint32_t s_out[8], uint32_t a_out[8], const uint32_t seed[8],
                      const uint8_t* msg, int len, const uint32_t* tabB) {
   uint32_t h[16];
@@ -287,12 +330,12 @@ FE_FN void sign_lane(uint32_t r_out[8], uint32_t s_out[8], uint32_t a_out[8], co
   for (int i = 0; i < 16; ++i) wide[i] = i < 8 ? a[i] : 0u;
   sc_reduce512(ared, wide);                         // [a]B = [a mod L]B
   ge P;
-  comb_mul_base<W>(P, ared, tabB);
+  comb_mul_base<PL>(P, ared, tabB);
   ge_compress_words(a_out, P);
   uint32_t rh[16], r[8];
   sha512_pre<32, LEN>(rh, prefix, msg, len);        // r = SHA-512(prefix || M) mod L
   sc_reduce512(r, rh);
-  comb_mul_base<W>(P, r, tabB);
+  comb_mul_base<PL>(P, r, tabB);
   ge_compress_words(r_out, P);
   uint32_t kh[16], k[8];
   sha512_ram<LEN>(kh, r_out, a_out, msg, len);      // k = SHA-512(R || A || M) mod L
@@ -300,16 +343,16 @@ FE_FN void sign_lane(uint32_t r_out[8], uint32_t s_out[8], uint32_t a_out[8], co
   sc_muladd(s_out, k, a, r);                        // S = (r + k*a) mod L
 }
 
-// Table entry (pos, j) of the comb for base point P0: j * 2^(W*pos) * P0.
-template <int W>
+// Table entry (pos, j) of plan PL for base point P0: j * 2^bitoff(pos) * P0.
+template <class PL>
 FE_FN void comb_entry(niels& out, const ge& P0, int pos, int j) {
   if (j == 0) { niels_identity(out); return; }
   ge Q = P0;
-  for (int i = 0; i < W * pos; ++i) ge_dbl(Q, Q);
+  for (int i = 0; i < PL::bitoff(pos); ++i) ge_dbl(Q, Q);
   ge acc;
   ge_identity(acc);
   bool started = false;
-  for (int b = W - 1; b >= 0; --b) {
+  for (int b = 31; b >= 0; --b) {
     if (started) ge_dbl(acc, acc);
     if ((j >> b) & 1) {
       if (started) { ge t; ge_add(t, acc, Q); acc = t; }

@@ -5,12 +5,13 @@ gather, by random 128-B table gathers), not by streaming HBM and not by MFMA:
 per signature it reads 161 B of batch input and gathers (PB + PA) table lines
 of 128 B, but issues ~2e4 32x32->64 multiply-accumulates.
 
-products_per_verify(WB, WA) counts the v_mad_u64_u32 products the implemented
-algorithm needs per signature (signed comb windows WB for [s]B and WA for
-[k](-A); Montgomery batch inversion over FIN_M signatures per lane):
+products_per_verify(PB, PA) counts the v_mad_u64_u32 products the implemented
+algorithm needs per signature (comb plans with PB positions for [s]B and PA for
+[k](-A), i.e. PB + PA steps; Montgomery batch inversion over FIN_M signatures
+per lane):
   comb       (PB + PA - 1) mixed additions x 7 field muls x 100 products
              + 1 mul for the first step, built directly from its table entry
-             (PB = ceil(254 / WB), PA = ceil(254 / WA); 10 + 15 at 26/18)
+             (10 + 14 positions with the default balanced plans)
   inversion  (254 squarings x 55 + 11 muls x 100) / FIN_M
   batch      3 muls per signature (prefix, 1/Z_m, running inverse) +
              2 affine muls (x, y), x 100
@@ -30,27 +31,23 @@ ENTRY_BYTES = 128
 INPUT_BYTES = 32 + 32 + 2 + 85  # R, S, key index, envelope
 
 
-def positions(w: int) -> int:
-    return (254 + w - 1) // w
+def products_per_verify(pb: int, pa: int) -> int:
+    return ((pb + pa - 1) * 7 + 1) * 100 + (254 * 55 + 11 * 100) // FIN_M + 5 * 100 + (81 + 44)
 
 
-def products_per_verify(wb: int, wa: int) -> int:
-    return ((positions(wb) + positions(wa) - 1) * 7 + 1) * 100 + (254 * 55 + 11 * 100) // FIN_M + 5 * 100 + (81 + 44)
+def gather_bytes_per_verify(pb: int, pa: int) -> int:
+    return (pb + pa) * ENTRY_BYTES
 
 
-def gather_bytes_per_verify(wb: int, wa: int) -> int:
-    return (positions(wb) + positions(wa)) * ENTRY_BYTES
-
-
-def windows_from_build_info(info: str):
-    """(WB, WA_big) from pbft_build_info(), e.g. 'pbft_verify gfx950 WB=26 WA=18|16|8 ...'."""
-    m = re.search(r"WB=(\d+) WA=(\d+)", info)
+def positions_from_build_info(info: str):
+    """(PB, PA_big) from pbft_build_info(), e.g. 'pbft_verify gfx950 PB=10 PA=14|16|32 ...'."""
+    m = re.search(r"PB=(\d+) PA=(\d+)", info)
     if not m:
         raise ValueError(f"unexpected build info: {info!r}")
     return int(m.group(1)), int(m.group(2))
 
 
-# defaults of the shipped build (WB = 26, WA = 18 for n <= 390 keys)
-WB = 26
-WA = 18
-PRODUCTS_PER_VERIFY = products_per_verify(WB, WA)
+# defaults of the shipped build (base point 10 positions, keys 14 for n <= 360)
+PB = 10
+PA = 14
+PRODUCTS_PER_VERIFY = products_per_verify(PB, PA)

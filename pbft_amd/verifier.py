@@ -148,11 +148,11 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_records(self._ctx, _ptr(rec), n, _ptr(out)))
         return out
 
-    def windows(self) -> tuple[int, int]:
-        """(WB, WA): comb windows of the base-point table and of the installed key set."""
-        wb, wa, nk = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-        check(self._lib.pbft_verify_ctx_info(self._ctx, ctypes.byref(wb), ctypes.byref(wa), ctypes.byref(nk)))
-        return wb.value, wa.value
+    def positions(self) -> tuple[int, int]:
+        """(PB, PA): comb positions (= steps) of the base-point plan and of the installed key set's plan."""
+        pb, pa, nk = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        check(self._lib.pbft_verify_ctx_info(self._ctx, ctypes.byref(pb), ctypes.byref(pa), ctypes.byref(nk)))
+        return pb.value, pa.value
 
     def last_kernel_ms(self) -> float:
         return float(self._lib.pbft_last_kernel_ms(self._ctx))

@@ -16,12 +16,38 @@ static void bytes_from_words(uint8_t* b, const uint32_t w[8]) {
   for (int i = 0; i < 8; ++i) for (int j = 0; j < 4; ++j) b[4 * i + j] = (uint8_t)(w[i] >> (8 * j));
 }
 
+// Non-uniform plan exercised on the host: 14 positions of 7 bits + 26 of 6 bits
+// (14*7 + 26*6 = 254, the balanced shape of the GPU's plans, incl. take_last).
+using PLAN_H = plan<40, 6, 14>;
+
+// Table of plan PL: position bases by repeated doubling, entries by repeated
+// addition (independent of comb_entry, which the w = 4 tables still use).
+template <class PL>
+static void build_table_incremental(const ge& P0, uint32_t* out) {
+  ge base = P0;
+  for (int pos = 0; pos < PL::P; ++pos) {
+    if (pos > 0)
+      for (int i = 0; i < PL::width(pos - 1); ++i) ge_dbl(base, base);
+    niels n;
+    niels_identity(n);
+    store_niels(out + (size_t)PL::offset(pos) * 32, n);
+    ge acc = base;
+    for (uint32_t j = 1; j < PL::entries(pos); ++j) {
+      ge_to_niels(n, acc);
+      store_niels(out + ((size_t)PL::offset(pos) + j) * 32, n);
+      ge t;
+      ge_add(t, acc, base);
+      acc = t;
+    }
+  }
+}
+
 template <int W>
 static void build_table(const ge& P0, uint32_t* out) {
   for (int pos = 0; pos < comb<W>::P; ++pos)
-    for (int j = 0; j < comb<W>::E; ++j) {
+    for (int j = 0; j < (int)comb<W>::E; ++j) {
       niels n;
-      comb_entry<W>(n, P0, pos, j);
+      comb_entry<comb<W>>(n, P0, pos, j);
       store_niels(out + ((size_t)pos * comb<W>::E + j) * 32, n);
     }
 }
@@ -78,7 +104,8 @@ int hh_decompress(const uint8_t* enc, uint8_t* out_compressed) {
 
 static int table_words(int w) {
   switch (w) { case 4: return (int)comb<4>::TABLE_WORDS; case 5: return (int)comb<5>::TABLE_WORDS;
-               case 6: return (int)comb<6>::TABLE_WORDS; case 8: return (int)comb<8>::TABLE_WORDS; }
+               case 6: return (int)comb<6>::TABLE_WORDS; case 8: return (int)comb<8>::TABLE_WORDS;
+               case 67: return (int)PLAN_H::TABLE_WORDS; }
   return -1;
 }
 int hh_table_words(int w) { return table_words(w); }
@@ -95,6 +122,7 @@ int hh_build_table(int w, const uint8_t* enc, int negate, uint32_t* out) {
     case 5: build_table<5>(P, out); break;
     case 6: build_table<6>(P, out); break;
     case 8: build_table<8>(P, out); break;
+    case 67: build_table_incremental<PLAN_H>(P, out); break;
     default: return -1;
   }
   return 1;
@@ -115,8 +143,9 @@ int hh_verify_batch(int w, const uint32_t* tabB, const uint32_t* tabA_all, const
     words_from_bytes(a, keys + 32 * (size_t)ki);
     const uint32_t* tA = tabA_all + (size_t)ki * tw;
     bool ok;
-    if (w == 4) ok = verify_lane<4, 4, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
-    else if (w == 8) ok = verify_lane<8, 8, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
+    if (w == 4) ok = verify_lane<comb<4>, comb<4>, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
+    else if (w == 8) ok = verify_lane<comb<8>, comb<8>, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
+    else if (w == 67) ok = verify_lane<PLAN_H, PLAN_H, -1>(r, s, a, kok, msg + (size_t)msg_stride * i, (int)msg_len, tabB, tA);
     else return -1;
     accept[i] = ok;
   }
@@ -131,12 +160,12 @@ extern "C" int hh_comb2(int w, const uint32_t* tabB, const uint32_t* tabA, const
   uint32_t s[8], k[8];
   words_from_bytes(s, s32); words_from_bytes(k, k32);
   ge P; ge_identity(P);
-  digit_stream<4> ds; ds.init(s);
-  digit_stream<4> dk; dk.init(k);
+  digits ds; ds.init(s);
+  digits dk; dk.init(k);
   for (int i = 0; i < comb<4>::P; ++i) {
-    int d = ds.next(); int ad = d < 0 ? -d : d; niels q;
+    int d = i + 1 < comb<4>::P ? ds.take<4>() : ds.take_last<4>(); int ad = d < 0 ? -d : d; niels q;
     load_niels(q, tabB + ((size_t)i * comb<4>::E + ad) * 32); ge_madd_signed(P, P, q, d < 0);
-    d = dk.next(); ad = d < 0 ? -d : d;
+    d = i + 1 < comb<4>::P ? dk.take<4>() : dk.take_last<4>(); ad = d < 0 ? -d : d;
     load_niels(q, tabA + ((size_t)i * comb<4>::E + ad) * 32); ge_madd_signed(P, P, q, d < 0);
   }
   fe zi, x, y; fe_invert(zi, P.Z); fe_mul(x, P.X, zi); fe_mul(y, P.Y, zi);

@@ -108,8 +108,8 @@ def test_comb_tables_and_mul(hh):
         assert out.raw == E.compress(E.pt_add(E.pt_mul(s, E.BASE), E.pt_mul(k, E.pt_neg(A)))), (s, k)
 
 
-def test_verify_lane_golden(hh, golden):
-    W = 4
+@pytest.mark.parametrize("W", [4, 67])  # 67: the non-uniform plan<40, 6, 14> (balanced 7/6-bit windows)
+def test_verify_lane_golden(hh, golden, W):
     tw = hh.hh_table_words(W)
     tabB = np.zeros(tw, dtype=np.uint32)
     assert hh.hh_build_table(W, E.compress(E.BASE), 0, tabB.ctypes.data) == 1

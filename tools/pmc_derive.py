@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """profiles/<run>/derived.json from rocprofv3 --pmc pass CSVs of the verify launch pair (read by bench.py).
 
-usage: python tools/pmc_derive.py PMC_DIR WB WA [n_sigs]
+usage: python tools/pmc_derive.py PMC_DIR PB PA [n_sigs]   (comb positions of the base-point / key plans)
 """
 import collections
 import csv
@@ -10,7 +10,7 @@ import json
 import os
 import sys
 
-d, wb, wa = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+d, pb, pa = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 n = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
 
 
@@ -23,7 +23,7 @@ def agg(name):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
-out = {"launch": f"comb_kernel<85,{wa}> (WB={wb}) + finish_kernel, one 2^20-signature round", "sigs_per_launch": n}
+out = {"launch": f"comb_kernel<85> PB={pb} PA={pa} + finish_kernel, one 2^20-signature round", "sigs_per_launch": n}
 tot = 0.0
 for k in ("comb_kernel", "finish_kernel"):
     m = agg(k)
