@@ -95,7 +95,11 @@ int pbft_verify_wait(pbft_ctx *ctx);
 
 /* Device-resident form: all pointers are device pointers on the context's
  * device; stream is a hipStream_t (NULL = the context's stream).  Enqueues the
- * kernel only.  d_msg must stay readable for N*msg_stride + 16 bytes. */
+ * kernels only.  d_R / d_S 16-byte aligned; d_msg must stay readable for
+ * N*msg_stride + 16 bytes.  A context's workspace is reused by every launch:
+ * launches of one context must be ordered (one stream, or events between
+ * streams) -- use pbft_verify_ctx_clone for independent concurrent streams.
+ * Capturable into a hipGraph after pbft_verify_reserve. */
 int pbft_verify_batch_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d_S, const uint16_t *d_key_idx,
                              const uint8_t *d_msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                              uint64_t *d_bitmap, void *stream);

@@ -140,6 +140,10 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_batch_device(self._ctx, d_R, d_S, d_key_idx, d_msg, msg_len, msg_stride, n,
                                                  d_bitmap, stream or None))
 
+    def reserve(self, max_n: int) -> None:
+        """Pre-size the workspace (required before capturing verify_device into a graph)."""
+        check(self._lib.pbft_verify_reserve(self._ctx, max_n))
+
     def verify_records(self, records: np.ndarray) -> np.ndarray:
         """Blocking verify of (N, 160) binary wire records (include/pbft_wire.h); returns bitmap words."""
         rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, 160)

@@ -352,3 +352,35 @@ def test_verify_batch_multi_shards(gv, golden):
     finally:
         for c in clones:
             c.close()
+
+
+def test_device_launch_captured_in_hip_graph(gv, golden):
+    """pbft_verify_reserve + pbft_verify_batch_device captured into a HIP graph (torch.cuda.CUDAGraph on ROCm)
+    and replayed: the replays give the oracle's bitmap (inputs swapped in place between replays)."""
+    import torch
+    from pbft_amd import bitmap_to_bool
+    b = dict(golden_batches(golden))[85]
+    gv.set_keys(b["keys"])
+    exp = b["expected"].astype(bool)
+    n = len(exp)
+    dev = torch.device("cuda", 0)
+    dR, dS = torch.from_numpy(b["R"].copy()).to(dev), torch.from_numpy(b["S"].copy()).to(dev)
+    dK = torch.from_numpy(b["key_idx"].astype(np.uint16).view(np.int16)).to(dev)
+    mp = np.zeros(n * 85 + 64, np.uint8)
+    mp[: n * 85] = b["msg"].reshape(-1)
+    dM = torch.from_numpy(mp).to(dev)
+    dB = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    gv.reserve(n)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gv.verify_device(dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(), 85, 85, n, dB.data_ptr(),
+                         torch.cuda.current_stream().cuda_stream)
+    for rep in range(3):
+        dB.zero_()
+        if rep == 2:  # new inputs in the same buffers: every signature's S flipped -> all rejected
+            dS.copy_(torch.from_numpy(b["S"] ^ 1).to(dev))
+        g.replay()
+        torch.cuda.synchronize()
+        got = bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n)
+        assert (got == (exp if rep < 2 else np.zeros(n, bool))).all(), rep
