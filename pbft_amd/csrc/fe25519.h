@@ -87,18 +87,45 @@ FE_FN void fe_reduce_wide(fe& h, uint64_t h0, uint64_t h1, uint64_t h2, uint64_t
   h.v[8] = (uint32_t)h8; h.v[9] = (uint32_t)h9;
 }
 
-#ifndef PBFT_FE_MUL_COLUMN_ORDER
+// Latency-oriented reduction of the 10 64-bit columns: every carry of a round is
+// computed at once (two rounds), so the dependent chain is ~4 operations deep
+// instead of the 12 sequential carries of fe_reduce_wide (~40 % more
+// instructions).  For code that runs one wave per SIMD on a serial chain -- the
+// inversion of the finish kernel, R decompression in the latency kernel -- where
+// VALU latency, not issue, is the bound.  Output limbs <= 2^26 + 2^17.6
+// (limb 0) / 2^25 + 2^16.6 (limb 1) / 2^26 + 2^13.4: within every bound fe_sub
+// and fe_mul need (tools/limb_bounds.py, host harness tests).
+FE_FN void fe_reduce_par(fe& h, uint64_t c[10]) {
+  uint64_t q[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    q[k] = c[k] >> ((k & 1) ? 25 : 26);
+    c[k] &= (k & 1) ? M25 : M26;
+  }
+  c[0] += q[9] * 19u;
+#pragma unroll
+  for (int k = 1; k < 10; ++k) c[k] += q[k - 1];
+  uint32_t r[10], l[10];
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+    r[k] = (uint32_t)(c[k] >> ((k & 1) ? 25 : 26));
+    l[k] = (uint32_t)c[k] & ((k & 1) ? M25 : M26);
+  }
+  h.v[0] = l[0] + 19u * r[9];
+#pragma unroll
+  for (int k = 1; k < 10; ++k) h.v[k] = l[k] + r[k - 1];
+}
+
 // Operand-scanning order: the 10 column accumulators are updated round-robin,
 // so consecutive v_mad_u64_u32 never depend on each other (10-way ILP per lane;
 // the dependent-mad latency is ~17 cycles on gfx950, tools/microbench/mad_latency.hip).
-FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
+FE_FN void fe_mul_cols(uint64_t acc[10], const fe& f, const fe& g) {
   uint32_t g19[10], fx[10];
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     g19[i] = 19u * g.v[i];
     fx[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
   }
-  uint64_t acc[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) acc[k] = MUL64(f.v[0], g.v[k]);
 #pragma unroll
@@ -119,44 +146,14 @@ FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
 #endif
     }
   }
+}
+FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
+  uint64_t acc[10];
+  fe_mul_cols(acc, f, g);
   fe_reduce_wide(h, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], acc[8], acc[9]);
 }
-#else
-FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
-  const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
-  const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
-  const uint32_t g0 = g.v[0], g1 = g.v[1], g2 = g.v[2], g3 = g.v[3], g4 = g.v[4];
-  const uint32_t g5 = g.v[5], g6 = g.v[6], g7 = g.v[7], g8 = g.v[8], g9 = g.v[9];
-  const uint32_t g1_19 = 19u * g1, g2_19 = 19u * g2, g3_19 = 19u * g3, g4_19 = 19u * g4, g5_19 = 19u * g5;
-  const uint32_t g6_19 = 19u * g6, g7_19 = 19u * g7, g8_19 = 19u * g8, g9_19 = 19u * g9;
-  const uint32_t f1_2 = 2u * f1, f3_2 = 2u * f3, f5_2 = 2u * f5, f7_2 = 2u * f7, f9_2 = 2u * f9;
 
-  uint64_t h0 = MUL64(f0, g0) + MUL64(f1_2, g9_19) + MUL64(f2, g8_19) + MUL64(f3_2, g7_19) + MUL64(f4, g6_19) +
-                MUL64(f5_2, g5_19) + MUL64(f6, g4_19) + MUL64(f7_2, g3_19) + MUL64(f8, g2_19) + MUL64(f9_2, g1_19);
-  uint64_t h1 = MUL64(f0, g1) + MUL64(f1, g0) + MUL64(f2, g9_19) + MUL64(f3, g8_19) + MUL64(f4, g7_19) +
-                MUL64(f5, g6_19) + MUL64(f6, g5_19) + MUL64(f7, g4_19) + MUL64(f8, g3_19) + MUL64(f9, g2_19);
-  uint64_t h2 = MUL64(f0, g2) + MUL64(f1_2, g1) + MUL64(f2, g0) + MUL64(f3_2, g9_19) + MUL64(f4, g8_19) +
-                MUL64(f5_2, g7_19) + MUL64(f6, g6_19) + MUL64(f7_2, g5_19) + MUL64(f8, g4_19) + MUL64(f9_2, g3_19);
-  uint64_t h3 = MUL64(f0, g3) + MUL64(f1, g2) + MUL64(f2, g1) + MUL64(f3, g0) + MUL64(f4, g9_19) +
-                MUL64(f5, g8_19) + MUL64(f6, g7_19) + MUL64(f7, g6_19) + MUL64(f8, g5_19) + MUL64(f9, g4_19);
-  uint64_t h4 = MUL64(f0, g4) + MUL64(f1_2, g3) + MUL64(f2, g2) + MUL64(f3_2, g1) + MUL64(f4, g0) +
-                MUL64(f5_2, g9_19) + MUL64(f6, g8_19) + MUL64(f7_2, g7_19) + MUL64(f8, g6_19) + MUL64(f9_2, g5_19);
-  uint64_t h5 = MUL64(f0, g5) + MUL64(f1, g4) + MUL64(f2, g3) + MUL64(f3, g2) + MUL64(f4, g1) +
-                MUL64(f5, g0) + MUL64(f6, g9_19) + MUL64(f7, g8_19) + MUL64(f8, g7_19) + MUL64(f9, g6_19);
-  uint64_t h6 = MUL64(f0, g6) + MUL64(f1_2, g5) + MUL64(f2, g4) + MUL64(f3_2, g3) + MUL64(f4, g2) +
-                MUL64(f5_2, g1) + MUL64(f6, g0) + MUL64(f7_2, g9_19) + MUL64(f8, g8_19) + MUL64(f9_2, g7_19);
-  uint64_t h7 = MUL64(f0, g7) + MUL64(f1, g6) + MUL64(f2, g5) + MUL64(f3, g4) + MUL64(f4, g3) +
-                MUL64(f5, g2) + MUL64(f6, g1) + MUL64(f7, g0) + MUL64(f8, g9_19) + MUL64(f9, g8_19);
-  uint64_t h8 = MUL64(f0, g8) + MUL64(f1_2, g7) + MUL64(f2, g6) + MUL64(f3_2, g5) + MUL64(f4, g4) +
-                MUL64(f5_2, g3) + MUL64(f6, g2) + MUL64(f7_2, g1) + MUL64(f8, g0) + MUL64(f9_2, g9_19);
-  uint64_t h9 = MUL64(f0, g9) + MUL64(f1, g8) + MUL64(f2, g7) + MUL64(f3, g6) + MUL64(f4, g5) +
-                MUL64(f5, g4) + MUL64(f6, g3) + MUL64(f7, g2) + MUL64(f8, g1) + MUL64(f9, g0);
-  fe_reduce_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
-}
-
-#endif
-
-FE_FN void fe_sq(fe& h, const fe& f) {
+FE_FN void fe_sq_cols(uint64_t c[10], const fe& f) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];
   const uint32_t f0_2 = 2u * f0, f1_2 = 2u * f1, f2_2 = 2u * f2, f3_2 = 2u * f3, f4_2 = 2u * f4;
@@ -178,44 +175,64 @@ FE_FN void fe_sq(fe& h, const fe& f) {
   uint64_t h8 = MUL64(f0_2, f8) + MUL64(f1_2, f7_2) + MUL64(f2_2, f6) + MUL64(f3_2, f5_2) +
                 MUL64(f4, f4) + MUL64(f9, f9_38);
   uint64_t h9 = MUL64(f0_2, f9) + MUL64(f1_2, f8) + MUL64(f2_2, f7) + MUL64(f3_2, f6) + MUL64(f4_2, f5);
-  fe_reduce_wide(h, h0, h1, h2, h3, h4, h5, h6, h7, h8, h9);
+  c[0] = h0; c[1] = h1; c[2] = h2; c[3] = h3; c[4] = h4; c[5] = h5; c[6] = h6; c[7] = h7; c[8] = h8; c[9] = h9;
+}
+FE_FN void fe_sq(fe& h, const fe& f) {
+  uint64_t c[10];
+  fe_sq_cols(c, f);
+  fe_reduce_wide(h, c[0], c[1], c[2], c[3], c[4], c[5], c[6], c[7], c[8], c[9]);
+}
+// PAR = latency-oriented reduction (fe_reduce_par)
+template <bool PAR>
+FE_FN void fe_sqT(fe& h, const fe& f) {
+  if constexpr (PAR) { uint64_t c[10]; fe_sq_cols(c, f); fe_reduce_par(h, c); }
+  else fe_sq(h, f);
+}
+template <bool PAR>
+FE_FN void fe_mulT(fe& h, const fe& f, const fe& g) {
+  if constexpr (PAR) { uint64_t c[10]; fe_mul_cols(c, f, g); fe_reduce_par(h, c); }
+  else fe_mul(h, f, g);
 }
 
+template <bool PAR = false>
 FE_FN void fe_sqn(fe& h, const fe& f, int n) {
-  fe_sq(h, f);
-  for (int i = 1; i < n; ++i) fe_sq(h, h);
+  fe_sqT<PAR>(h, f);
+  for (int i = 1; i < n; ++i) fe_sqT<PAR>(h, h);
 }
 
 // z^(2^250 - 1) and z^11 (shared by invert and pow22523)
+template <bool PAR = false>
 FE_FN void fe_pow250(fe& out, fe& z11, const fe& z) {
   fe t0, t1, z9, z2_5_0, z2_10_0, z2_20_0, z2_50_0;
-  fe_sq(t1, z);                 // z^2
-  fe_sq(t0, t1); fe_sq(t0, t0); // z^8
-  fe_mul(z9, t0, z);            // z^9
-  fe_mul(z11, z9, t1);          // z^11
-  fe_sq(t0, z11);               // z^22
-  fe_mul(z2_5_0, t0, z9);       // z^31 = z^(2^5-1)
-  fe_sqn(t0, z2_5_0, 5); fe_mul(z2_10_0, t0, z2_5_0);
-  fe_sqn(t0, z2_10_0, 10); fe_mul(z2_20_0, t0, z2_10_0);
-  fe_sqn(t0, z2_20_0, 20); fe_mul(t1, t0, z2_20_0);
-  fe_sqn(t0, t1, 10); fe_mul(z2_50_0, t0, z2_10_0);
-  fe_sqn(t0, z2_50_0, 50); fe_mul(t1, t0, z2_50_0);      // 2^100 - 1
-  fe_sqn(t0, t1, 100); fe_mul(t1, t0, t1);               // 2^200 - 1
-  fe_sqn(t0, t1, 50); fe_mul(out, t0, z2_50_0);          // 2^250 - 1
+  fe_sqT<PAR>(t1, z);                       // z^2
+  fe_sqT<PAR>(t0, t1); fe_sqT<PAR>(t0, t0); // z^8
+  fe_mulT<PAR>(z9, t0, z);                  // z^9
+  fe_mulT<PAR>(z11, z9, t1);                // z^11
+  fe_sqT<PAR>(t0, z11);                     // z^22
+  fe_mulT<PAR>(z2_5_0, t0, z9);             // z^31 = z^(2^5-1)
+  fe_sqn<PAR>(t0, z2_5_0, 5); fe_mulT<PAR>(z2_10_0, t0, z2_5_0);
+  fe_sqn<PAR>(t0, z2_10_0, 10); fe_mulT<PAR>(z2_20_0, t0, z2_10_0);
+  fe_sqn<PAR>(t0, z2_20_0, 20); fe_mulT<PAR>(t1, t0, z2_20_0);
+  fe_sqn<PAR>(t0, t1, 10); fe_mulT<PAR>(z2_50_0, t0, z2_10_0);
+  fe_sqn<PAR>(t0, z2_50_0, 50); fe_mulT<PAR>(t1, t0, z2_50_0);   // 2^100 - 1
+  fe_sqn<PAR>(t0, t1, 100); fe_mulT<PAR>(t1, t0, t1);            // 2^200 - 1
+  fe_sqn<PAR>(t0, t1, 50); fe_mulT<PAR>(out, t0, z2_50_0);       // 2^250 - 1
 }
 
+template <bool PAR = false>
 FE_FN void fe_invert(fe& out, const fe& z) {
   fe t, z11;
-  fe_pow250(t, z11, z);
-  fe_sqn(t, t, 5);
-  fe_mul(out, t, z11);  // z^(2^255 - 21) = z^(p-2)
+  fe_pow250<PAR>(t, z11, z);
+  fe_sqn<PAR>(t, t, 5);
+  fe_mulT<PAR>(out, t, z11);  // z^(2^255 - 21) = z^(p-2)
 }
 
+template <bool PAR = false>
 FE_FN void fe_pow22523(fe& out, const fe& z) {
   fe t, z11;
-  fe_pow250(t, z11, z);
-  fe_sqn(t, t, 2);
-  fe_mul(out, t, z);    // z^(2^252 - 3) = z^((p-5)/8)
+  fe_pow250<PAR>(t, z11, z);
+  fe_sqn<PAR>(t, t, 2);
+  fe_mulT<PAR>(out, t, z);    // z^(2^252 - 3) = z^((p-5)/8)
 }
 
 // Fully reduce to the canonical representative < p, as 8 little-endian u32 words.

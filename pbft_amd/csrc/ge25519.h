@@ -82,6 +82,7 @@ FE_FN bool ge_is_small_order(const ge& p) {
 
 // curve25519-dalek 3.2.1 CompressedEdwardsY::decompress (y not range-checked;
 // x = 0 with sign bit 1 accepted).  w = 8 LE words of the encoding.
+template <bool PAR = false>
 FE_FN bool ge_decompress(ge& p, const uint32_t w[8]) {
   fe y, one, yy, u, v, v3, v7, r, chk, d, i, nu, nui, t;
   fe_from_words(y, w);
@@ -93,7 +94,7 @@ FE_FN bool ge_decompress(ge& p, const uint32_t w[8]) {
   fe_sq(v3, v); fe_mul(v3, v3, v);
   fe_sq(v7, v3); fe_mul(v7, v7, v);
   fe_mul(t, u, v7);
-  fe_pow22523(r, t);
+  fe_pow22523<PAR>(r, t);
   fe_mul(r, r, u); fe_mul(r, r, v3);
   fe_sq(chk, r); fe_mul(chk, chk, v);
   fe_neg(nu, u); fe_carry(nu);

@@ -417,20 +417,34 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   }
 }
 
-// ---- latency mode: SPLIT lanes per signature ---------------------------------
+// ---- latency mode: small batches --------------------------------------------
 // For small batches (BASELINE config #5: 4096-signature rounds) one lane per
-// signature leaves most SIMDs idle and the round takes one lane's serial time.
-// comb_split_kernel gives every signature SPLIT = 4 lanes: each lane computes
-// the challenge hash itself (redundantly: it is on the critical path anyway),
-// then the steps j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a
-// step in the last round add the identity entry), and the 4 partial points are
-// summed with two shuffle + extended-addition rounds.  ~2x lower latency per
-// round, ~1.3x the VALU work per signature; used for batches < 2^16 signatures.
+// signature leaves most SIMDs idle, and the round's latency is one lane's
+// serial work: SHA-512, 24 comb steps, then the finish kernel's inversion.
+// comb_latency_kernel (blocks of 4 waves -- one per SIMD, so each may use the
+// whole register file -- and 48 signatures per block) instead
+//  * gives every signature SPLIT = 4 lanes in waves 0-2: each lane computes the
+//    challenge hash itself (it is on the critical path anyway), then the steps
+//    j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a step in the
+//    last round add the identity entry), and the 4 partial points are summed
+//    with two shuffle + extended-addition rounds;
+//  * meanwhile wave 3 decompresses the 48 R encodings (dalek's decompress,
+//    ge_decompress) -- the one exponentiation per signature, off the comb's
+//    critical path -- so no inversion is needed: after a block barrier R' is
+//    compared with R projectively (X' == x_R Z', Y' == y_R Z'), R's small order
+//    is read from its canonical y, and each comb wave writes 16 bitmap bits
+//    (the bitmap as u16 pieces: piece 3 * block + wave).
+// Equivalent to the throughput path's compare (R' == decompress(R) as points,
+// DESIGN.md "R check"); ~2.5x lower latency than one lane per signature.
 static constexpr int SPLIT = 4;
+static constexpr int LAT_COMB_WAVES = 3;
+static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // 48 signatures per block
+static constexpr int LAT_BLOCK = (LAT_COMB_WAVES + 1) * 64;  // + 1 decompression wave
 #ifndef PBFT_SPLIT_BELOW
 #define PBFT_SPLIT_BELOW 65536
 #endif
-static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_split_kernel
+static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_latency_kernel
+static constexpr uint32_t LAT_LDS = LAT_COMB_WAVES * COMB_LDS_PER_WAVE + 21 * 64 * 4;  // entry buffers + x_R, y_R, ok
 
 // Line-coalesced gather with per-lane 64-bit entry addresses (the split kernel's
 // lanes of one wave gather from both tables in the same step).
@@ -454,12 +468,12 @@ FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
 }
 
 template <int LEN, class PLA>
-__global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
+__global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
-    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
     const uint8_t** __restrict__ eaddr) {
   using ST = steps<PLB, PLA>;
   constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
@@ -467,7 +481,30 @@ __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
-  const uint64_t g = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;  // global lane, < Lpad
+  uint32_t* rdec = (uint32_t*)(lds + LAT_COMB_WAVES * COMB_LDS_PER_WAVE);  // [21][64]: x_R, y_R limbs, ok
+  if (wave == LAT_COMB_WAVES) {
+    // ---- decompression wave: R of signature blockIdx * LAT_SIGS + lane (lanes >= LAT_SIGS idle)
+    const uint64_t i = (uint64_t)blockIdx.x * LAT_SIGS + lane;
+    const uint64_t ii = i < N ? i : 0;
+    uint32_t rr[8], ry[8];
+    load32(rr, R + (size_t)rs_stride * ii);
+    ge Rp;
+#if PBFT_ABL_LAT_NODEC  // ablation: no decompression (timing only)
+    bool ok = true;
+    fe_zero(Rp.X); fe_zero(Rp.Y);
+#else
+    bool ok = ge_decompress<true>(Rp, rr);  // dalek 3.2.1 CompressedEdwardsY::decompress (latency-oriented)
+#endif
+    canon_y(ry, rr);
+    ok = ok && !y_is_small_order(ry);  // small-order R (verify_strict)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { rdec[t * 64 + lane] = Rp.X.v[t]; rdec[(10 + t) * 64 + lane] = Rp.Y.v[t]; }
+    rdec[20 * 64 + lane] = ok ? 1u : 0u;
+    __syncthreads();
+    return;
+  }
+  // ---- comb waves: 16 signatures per wave, SPLIT lanes each
+  const uint64_t g = (uint64_t)blockIdx.x * (LAT_COMB_WAVES * 64) + threadIdx.x;  // global comb lane, < Lpad
   const uint64_t i = g / SPLIT;
   const int r = (int)(g % SPLIT);
   const bool live = i < N;
@@ -546,7 +583,9 @@ __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
       dma_entry_lines64(nadr, lane, ebuf);
       if (t + 2 < T) nadr = eaddr[(size_t)(t + 2) * Lpad + g];
     }
+#if !PBFT_ABL_LAT_NOSTEPS  // ablation: gathers only (timing only)
     ge_madd_signed(P, P, q, (sgn >> t) & 1u);
+#endif
 #pragma unroll
     for (int u = 0; u < 10; ++u) asm("" : "+v"(P.X.v[u]), "+v"(P.Y.v[u]), "+v"(P.Z.v[u]), "+v"(P.T.v[u]));
   }
@@ -560,15 +599,24 @@ __global__ void __launch_bounds__(BLOCK, 2) comb_split_kernel(
   };
   combine(1);
   combine(2);
-  if (live && r == 0) {
+  __syncthreads();  // x_R, y_R of the block's signatures are in LDS
+  bool acc = false;
+  if (r == 0 && live) {
+    const int l = (int)(threadIdx.x >> 2);  // signature within the block
+    fe xr, yr, t1, t2;
 #pragma unroll
-    for (int t = 0; t < 10; ++t) {
-      xyz[(size_t)t * N + i] = P.X.v[t];
-      xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
-      xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
-    }
-    flags[i] = (s_ok && kok) ? 1 : 0;
+    for (int t = 0; t < 10; ++t) { xr.v[t] = rdec[t * 64 + l]; yr.v[t] = rdec[(10 + t) * 64 + l]; }
+    fe_mul(t1, xr, P.Z);
+    fe_mul(t2, yr, P.Z);
+    acc = rdec[20 * 64 + l] && s_ok && kok && fe_eq(P.X, t1) && fe_eq(P.Y, t2);
   }
+  // lanes 4j (j = 0..15) hold this wave's 16 results: one 16-bit piece of the block's bitmap word
+  const uint64_t vote = __ballot(acc);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bits |= (uint32_t)((vote >> (4 * j)) & 1u) << j;
+  const uint64_t piece = (uint64_t)blockIdx.x * LAT_COMB_WAVES + wave;  // signatures 16 piece .. 16 piece + 15
+  if (lane == 0 && piece < 4 * ((N + 63) / 64)) ((uint16_t*)bitmap)[piece] = (uint16_t)bits;  // bits past N: 0
 }
 
 __device__ __forceinline__ void load_fe(fe& f, const uint32_t* __restrict__ base, uint64_t N, uint64_t i) {
@@ -626,7 +674,7 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
     else fe_mul(pre[m], pre[m - 1], z);
   });
   fe inv;
-  fe_invert(inv, pre[FM - 1]);
+  fe_invert<true>(inv, pre[FM - 1]);  // the serial chain of a 1-wave-per-SIMD kernel: latency-oriented carries
   fin_unroll<FM>::down([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
@@ -826,12 +874,15 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
 #define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
   hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS,             \
                      (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
-#define PBFT_LAUNCH_SPLIT(LEN_, WA_)                                                                          \
-  hipLaunchKernelGGL((comb_split_kernel<LEN_, WA_>), dim3((unsigned)sblocks), b, (BLOCK / 64) * COMB_LDS_PER_WAVE, \
-                     st, dR, dS, (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Lpad,          \
-                     c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, (const uint8_t**)eidx)
-  if (N < c->split_below) {
-    const uint64_t sblocks = (N * SPLIT + BLOCK - 1) / BLOCK, Lpad = sblocks * BLOCK;
+#define PBFT_LAUNCH_SPLIT(LEN_, WA_)                                                                           \
+  hipLaunchKernelGGL((comb_latency_kernel<LEN_, WA_>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, st, dR, dS, \
+                     (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Lpad, c->d_tabB,           \
+                     c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, dB, (const uint8_t**)eidx)
+  const bool latency_mode = N < c->split_below;
+  if (latency_mode) {
+    // enough blocks for every u16 piece of the ceil(N/64) bitmap words (>= ceil(N / LAT_SIGS))
+    const uint64_t pieces = 4 * ((N + 63) / 64);
+    const uint64_t sblocks = (pieces + LAT_COMB_WAVES - 1) / LAT_COMB_WAVES, Lpad = sblocks * LAT_COMB_WAVES * 64;
     if (msg_len == PBFT_ENVELOPE_LEN) {
       if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_BIG);
       else if (c->pa == PLA_MID::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_MID);
@@ -853,17 +904,19 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
 #undef PBFT_LAUNCH_COMB
 #undef PBFT_LAUNCH_SPLIT
   HIP_TRY(hipGetLastError());
-  // signatures per finish lane: as many as keep >= one wave per SIMD (1,024 waves) busy
-  const int fm = N >= (uint64_t)64 * 1024 * FIN_M ? FIN_M : N >= (uint64_t)64 * 1024 * 4 ? 4 : 1;
+  if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
+    // signatures per finish lane: as many as keep >= one wave per SIMD (1,024 waves) busy
+    const int fm = N >= (uint64_t)64 * 1024 * FIN_M ? FIN_M : N >= (uint64_t)64 * 1024 * 4 ? 4 : 1;
 #define PBFT_LAUNCH_FIN(M_)                                                                                 \
   hipLaunchKernelGGL(finish_kernel<M_>, dim3((unsigned)((((N + 64 * M_ - 1) / (64 * M_)) * 64 + BLOCK - 1) / \
                                                         BLOCK)),                                           \
                      dim3(BLOCK), 0, st, dR, rs_stride, xyz, flags, N, dB)
-  if (fm == FIN_M) PBFT_LAUNCH_FIN(FIN_M);
-  else if (fm == 4) PBFT_LAUNCH_FIN(4);
-  else PBFT_LAUNCH_FIN(1);
+    if (fm == FIN_M) PBFT_LAUNCH_FIN(FIN_M);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4);
+    else PBFT_LAUNCH_FIN(1);
 #undef PBFT_LAUNCH_FIN
-  HIP_TRY(hipGetLastError());
+    HIP_TRY(hipGetLastError());
+  }
 #if !PBFT_NO_LAUNCH_EVENTS
   HIP_TRY(hipEventRecord(c->ev1, st));
 #endif

@@ -67,6 +67,14 @@ void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
     case 4: { fe t; fe_add(t, fa, fb); fe_mul(fo, t, t); break; }     // (a+b)^2 via mul of unreduced
     case 5: { fe t; fe_sub(t, fa, fb); fe_mul(fo, t, fb); break; }    // (a-b)*b
     case 6: { fe t; fe_add(t, fa, fb); fe_sq(fo, t); break; }         // (a+b)^2 via sq of unreduced
+    // latency-oriented (parallel-carry) variants
+    case 7: fe_mulT<true>(fo, fa, fb); break;
+    case 8: fe_sqT<true>(fo, fa); break;
+    case 9: fe_invert<true>(fo, fa); break;
+    case 10: fe_pow22523<true>(fo, fa); break;
+    case 11: { fe t; fe_add(t, fa, fb); fe_mulT<true>(fo, t, t); break; }
+    case 12: { fe t; fe_sub(t, fa, fb); fe_mulT<true>(fo, t, fb); break; }
+    case 13: { fe t, u; fe_sqT<true>(t, fa); fe_sub(u, fb, t); fe_mulT<true>(fo, u, t); break; }  // par output as subtrahend
     default: fo = fa;
   }
   fe_to_words(wo, fo);
@@ -91,8 +99,15 @@ void hh_reduce512(const uint8_t* x64, uint8_t* out32) {
 int hh_decompress(const uint8_t* enc, uint8_t* out_compressed) {
   uint32_t w[8];
   words_from_bytes(w, enc);
-  ge p;
-  if (!ge_decompress(p, w)) return 0;
+  ge p, q;
+  const bool ok = ge_decompress(p, w);
+  if (ok != ge_decompress<true>(q, w)) return -1;  // the latency-oriented form must agree
+  if (!ok) return 0;
+  uint32_t a[8], b[8];
+  for (int c = 0; c < 2; ++c) {
+    fe_to_words(a, c ? p.X : p.Y); fe_to_words(b, c ? q.X : q.Y);
+    for (int i = 0; i < 8; ++i) if (a[i] != b[i]) return -1;
+  }
   fe zi, x, y;
   fe_invert(zi, p.Z); fe_mul(x, p.X, zi); fe_mul(y, p.Y, zi);
   uint32_t xw[8], yw[8];

@@ -50,9 +50,17 @@ def test_field_ops(hh):
         assert _fe(hh, 4, a, b) == (a + b) ** 2 % P
         assert _fe(hh, 5, a, b) == (a - b) * b % P
         assert _fe(hh, 6, a, b) == (a + b) ** 2 % P
+        # latency-oriented (parallel-carry) reductions: same values
+        assert _fe(hh, 7, a, b) == a * b % P
+        assert _fe(hh, 8, a, b) == a * a % P
+        assert _fe(hh, 11, a, b) == (a + b) ** 2 % P
+        assert _fe(hh, 12, a, b) == (a - b) * b % P
+        assert _fe(hh, 13, a, b) == (b - a * a) * (a * a) % P
     for a in vals[:60]:
         assert _fe(hh, 2, a, 0) == pow(a, P - 2, P)
         assert _fe(hh, 3, a, 0) == pow(a, (P - 5) // 8, P)
+        assert _fe(hh, 9, a, 0) == pow(a, P - 2, P)
+        assert _fe(hh, 10, a, 0) == pow(a, (P - 5) // 8, P)
 
 
 @pytest.mark.parametrize("ln", [0, 1, 47, 48, 63, 64, 85, 111, 112, 175, 176, 239, 240, 300, 1023])
