@@ -316,7 +316,7 @@ def test_wire_records_and_stream_end_to_end(gv, golden):
 
 
 def test_latency_mode_split_kernel_matches_single_lane(golden):
-    """comb_split_kernel (4 lanes per signature, batches < 2^16) and comb_kernel give identical bitmaps on every
+    """comb_latency_kernel (4 lanes per signature, batches < 2^16) and comb_kernel give identical bitmaps on every
     golden batch (every adversarial class, every message length)."""
     from pbft_amd import GpuBatchVerifier
     results = {}
