@@ -1,21 +1,25 @@
 /*
  * pbft_replica.h — C ABI of the host-side PBFT verification state machine that
  * feeds the GPU verifier: signed envelopes, a round
- * batcher keyed by (view, seq), and the prepare / commit quorum predicates.
- * Compiled into pbft_amd/libpbft_verify.so.
+ * batcher keyed by (view, seq), the prepare / commit quorum predicates, a
+ * watermark-bounded and garbage-collected log, and the libp2p PeerId -> key
+ * binding.  Compiled into pbft_amd/libpbft_verify.so.
  *
  * Reference interfaces mirrored (ameya-deshmukh/pbft):
  *   pbft_replica_on_pre_prepare  Pbft::process_pre_prepare / validate_pre_prepare
  *                                src/behavior.rs:100-157 (digest check
  *                                src/message.rs:139-145, view check :134-141,
- *                                conflicting digest :144-151)
- *   pbft_replica_push            PbftHandler message_to_handler_event
- *                                src/handler.rs:533-548 -> inject_node_event
- *                                src/behavior.rs:340-412, but the per-message
- *                                validate_prepare/validate_commit (:159-195) become
- *                                "enqueue into the round window"
- *   pbft_replica_flush           the batched validation: every closed window's
- *                                Prepare+Commit signatures in ONE GPU batch, then
+ *                                conflicting digest :144-151) plus the signature
+ *                                check the reference leaves as a TODO (:127)
+ *   pbft_replica_push            inject_node_event src/behavior.rs:340-412, but the
+ *                                per-message validate_prepare / validate_commit
+ *                                (:159-195) become "enqueue into the round window";
+ *                                the signer is the AUTHENTICATED peer (the reference
+ *                                keys votes by the connection's peer_id, :346, :380)
+ *   pbft_replica_push_frames     PbftHandler -> message_to_handler_event
+ *                                src/handler.rs:533-548 for one connection
+ *   pbft_replica_flush           the batched validation: every ready sub-window's
+ *                                signatures in ONE GPU batch, then
  *                                State::insert_prepare/insert_commit
  *                                (src/state.rs:49-67) for accepted ones only
  *   pbft_replica_prepared        Pbft::prepared src/behavior.rs:177-182 with the
@@ -23,10 +27,30 @@
  *   pbft_replica_committed_local Pbft::committed_local :214-223 with 2f+1 commits
  *                                keyed by (view, seq) (reference keys commits by
  *                                view only, src/state.rs:22-23)
+ *   pbft_replica_set_log_window  the h / H watermarks the reference leaves as
+ *   pbft_replica_stable_checkpoint  TODOs (src/behavior.rs:154, :192; its logs are
+ *                                unbounded HashMaps, src/state.rs:9-11)
+ *   pbft_key_from_peer_id        libp2p-core 0.31 PeerId of an Ed25519 identity
+ *   pbft_replica_peer_index      (src/main.rs:39-40): 00 24 08 01 12 20 || A[32]
+ *
+ * Round batcher rules (one window per (view, seq), three sub-windows):
+ *   - a signed PrePrepare is verified at the next flush (it gates the window);
+ *   - the Prepare sub-window is READY once the distinct backups with an accepted
+ *     or pending Prepare reach 2f (or all n-1 backups have sent one); the Commit
+ *     sub-window once distinct replicas reach 2f+1 (or all n).  Each closes on
+ *     its own count, so a phase-ordered run (Commits sent only after PREPARED)
+ *     with f silent replicas progresses without a deadline flush;
+ *   - flush(force = 1) (the caller's deadline) verifies everything pending;
+ *   - every candidate vote of a (kind, signer) is kept until one verifies (at
+ *     most PBFT_MAX_CANDIDATES): a forged vote cannot pre-empt the real one;
+ *     among accepted votes of one signer the last one wins (src/state.rs:56, :66);
+ *   - seqs outside (h, h + log_window] are dropped; a window is erased once it
+ *     is committed locally and every lower seq is too (h advances), or by
+ *     pbft_replica_stable_checkpoint.
  *
  * Errors: negative PBFT_E* codes (pbft_verify.h); invalid signatures, wrong
- * digests and stale views are dropped and counted, never raised (the reference
- * panics via .unwrap(), src/behavior.rs:97, :345, :371).
+ * digests, stale views and out-of-window seqs are dropped and counted, never
+ * raised (the reference panics via .unwrap(), src/behavior.rs:97, :345, :371).
  */
 #ifndef PBFT_REPLICA_H
 #define PBFT_REPLICA_H
@@ -47,6 +71,11 @@ extern "C" {
 
 #define PBFT_EVENT_PREPARED 1
 #define PBFT_EVENT_COMMITTED_LOCAL 2
+#define PBFT_EVENT_PRE_PREPARED 3 /* the PrePrepare's signature verified: send Prepare */
+
+#define PBFT_MAX_CANDIDATES 4       /* pending votes kept per (window, kind, signer) */
+#define PBFT_DEFAULT_LOG_WINDOW 4096 /* H - h */
+#define PBFT_PEER_ID_BYTES 38       /* 00 24 08 01 12 20 || A[32] */
 
 typedef struct pbft_replica pbft_replica;
 
@@ -57,6 +86,12 @@ typedef struct {
 
 typedef struct {
   uint64_t pushed, verified, accepted, rejected_sig, rejected_digest, rejected_view, duplicates, batches;
+  uint64_t rejected_watermark; /* seq outside (h, h + log_window]                      */
+  uint64_t rejected_signer;    /* frame's "replica" is not the authenticated peer / not the primary */
+  uint64_t dropped_flood;      /* candidates beyond PBFT_MAX_CANDIDATES                */
+  uint64_t windows_gc;         /* windows erased (committed prefix or checkpoint)       */
+  uint64_t low_watermark;      /* h                                                     */
+  uint64_t live_windows;       /* windows currently held                                */
 } pbft_replica_stats;
 
 /* Optional verifier override (tests without a GPU): same SoA contract as
@@ -70,43 +105,70 @@ typedef int (*pbft_digest_fn)(void *user, const uint8_t *op, uint32_t op_len, ui
 
 /* n replicas (f = (n-1)/3), this replica's id, the replica key set keys[n][32]
  * (also installed on ctx with pbft_verify_set_keys).  ctx may be NULL only if a
- * verifier override is installed before the first flush. */
+ * verifier override is installed before the first flush.  The primary of view v
+ * is replica v mod n (Castro-Liskov p = v mod |R|). */
 int pbft_replica_create(pbft_ctx *ctx, uint32_t n, uint32_t self_id, const uint8_t *keys, pbft_replica **out);
 int pbft_replica_destroy(pbft_replica *r);
 int pbft_replica_set_verifier(pbft_replica *r, pbft_batch_verify_fn fn, void *user);
 int pbft_replica_set_digest_fn(pbft_replica *r, pbft_digest_fn fn, void *user);
+/* H - h (default PBFT_DEFAULT_LOG_WINDOW; >= 1). */
+int pbft_replica_set_log_window(pbft_replica *r, uint64_t log_window);
 
 /* Encode the 85-byte signed envelope "PBFT" || kind || view LE || seq LE || digest. */
 void pbft_envelope(uint8_t out[PBFT_ENVELOPE_BYTES], uint8_t kind, uint64_t view, uint64_t seq,
                    const uint8_t digest[64]);
 
-/* Accept a PrePrepare for (view, seq) carrying the client operation bytes.
- * Recomputes the Blake2b-512 digest on the GPU; returns 1 accepted, 0 dropped
- * (digest mismatch / wrong view / conflicting digest for (view, seq)).
- * digest_out (optional) receives the digest. */
+/* A PrePrepare for (view, seq) carrying the client operation bytes and the
+ * primary's signature (R || S over the kind-0 envelope of the claimed digest).
+ * Recomputes the Blake2b-512 digest (GPU, or the digest override); returns 1 if
+ * queued for signature verification (PBFT_EVENT_PRE_PREPARED at the flush that
+ * accepts it), 0 if dropped (digest mismatch / wrong view / out of window /
+ * conflicting digest already accepted for (view, seq)).  digest_out (optional)
+ * receives the recomputed digest. */
 int pbft_replica_on_pre_prepare(pbft_replica *r, uint64_t view, uint64_t seq, const uint8_t *op, uint32_t op_len,
-                                const uint8_t claimed_digest[64], uint8_t digest_out[64]);
+                                const uint8_t claimed_digest[64], const uint8_t primary_sig[64],
+                                uint8_t digest_out[64]);
 
-/* Ingress of a signed Prepare/Commit from replica `signer` (sig = R || S). */
+/* A signed Prepare/Commit from replica `signer` (sig = R || S).  `signer` must be
+ * the AUTHENTICATED sender (the connection's peer, pbft_replica_peer_index),
+ * never a field of the message.  Returns 1 queued, 0 dropped. */
 int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]);
 
-/* Ingress straight from the wire (include/pbft_wire.h): decode a byte stream of
- * UviBytes frames (src/protocol_config.rs:50-76 upgrade_inbound) and push every
- * signed Prepare / Commit into its round window; other frames are counted in
- * *dropped.  *consumed = bytes of whole frames (keep the rest for the next read).
- * Returns 0, or PBFT_EINVAL on a framing error. */
-int pbft_replica_push_frames(pbft_replica *r, const uint8_t *stream, size_t len, uint64_t *consumed,
-                             uint64_t *pushed, uint64_t *dropped);
+/* Ingress straight from one connection's byte stream (include/pbft_wire.h):
+ * decode UviBytes frames (src/protocol_config.rs:50-76 upgrade_inbound); signed
+ * Prepare / Commit frames whose "replica" equals peer_idx (the authenticated
+ * connection) are pushed, signed PrePrepare frames go to on_pre_prepare (their
+ * signature must be the view's primary's), everything else is counted in
+ * *dropped.  *consumed = bytes of whole frames (keep the rest for the next
+ * read).  Returns 0, or PBFT_EINVAL on a framing error. */
+int pbft_replica_push_frames(pbft_replica *r, uint32_t peer_idx, const uint8_t *stream, size_t len,
+                             uint64_t *consumed, uint64_t *pushed, uint64_t *dropped);
 
-/* Verify every closed round window in one batch (force = also open windows),
- * insert the accepted votes and report newly reached quorums. */
+/* Verify every READY sub-window (force = every pending signature) in one batch,
+ * insert the accepted votes, report newly reached events, and GC the committed
+ * prefix.  *n_events = events written (<= max_events; later ones are dropped). */
 int pbft_replica_flush(pbft_replica *r, int force, pbft_round_event *events, uint32_t max_events,
                        uint32_t *n_events);
+
+/* Stable checkpoint at seq (PBFT §4.3): h = max(h, seq); windows <= h erased. */
+int pbft_replica_stable_checkpoint(pbft_replica *r, uint64_t seq);
 
 int pbft_replica_prepared(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_committed_local(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_get_stats(pbft_replica *r, pbft_replica_stats *out);
+
+/* libp2p PeerId <-> Ed25519 key.  A PeerId of an Ed25519 identity is the
+ * identity multihash of the protobuf-encoded public key: 00 24 08 01 12 20 || A.
+ * pbft_key_from_peer_id: 0 and A[32], or PBFT_EINVAL (wrong length / prefix).
+ * pbft_peer_id_from_key: writes the 38 bytes.
+ * pbft_key_from_peer_id_b58: the same from the base58btc text form ("12D3KooW...").
+ * pbft_replica_peer_index: the replica index whose key the PeerId carries, or
+ * PBFT_EINVAL if it is malformed or not a replica of this set. */
+int pbft_key_from_peer_id(const uint8_t *peer_id, size_t len, uint8_t A[32]);
+void pbft_peer_id_from_key(const uint8_t A[32], uint8_t peer_id[PBFT_PEER_ID_BYTES]);
+int pbft_key_from_peer_id_b58(const char *text, size_t len, uint8_t A[32]);
+int pbft_replica_peer_index(pbft_replica *r, const uint8_t *peer_id, size_t len);
 
 #ifdef __cplusplus
 }

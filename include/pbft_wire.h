@@ -50,11 +50,11 @@ extern "C" {
 #define PBFT_RECORD_BYTES 160
 
 /* Frame decode status (pbft_wire_decode_votes) */
-#define PBFT_WIRE_OK 0        /* signed Prepare/Commit -> one SoA row       */
+#define PBFT_WIRE_OK 0        /* signed PrePrepare/Prepare/Commit -> one SoA row */
 #define PBFT_WIRE_EJSON 1     /* not a JSON Message of the reference schema */
 #define PBFT_WIRE_EDIGEST 2   /* digest is not 128 hex chars               */
 #define PBFT_WIRE_EUNSIGNED 3 /* no replica/signature fields               */
-#define PBFT_WIRE_EKIND 4     /* PrePrepare / ClientRequest (not a vote)    */
+#define PBFT_WIRE_EKIND 4     /* ClientRequest (not signed by a replica)     */
 #define PBFT_WIRE_ESIGNER 5   /* replica index >= n_replicas               */
 
 typedef struct {
@@ -96,7 +96,12 @@ int pbft_wire_decode_json(const char *json, size_t len, pbft_wire_msg *out, char
  * Stops at the first incomplete frame, after max_rows signed votes, or after
  * max_frames frames.  For every decoded frame f: status[f] = PBFT_WIRE_*;
  * each OK frame appends row r: R[r], S[r], key_idx[r] = replica, msg[r] = the
- * 85-byte envelope (stride 85), kind[r], view[r], seq[r].  Outputs: *n_frames,
+ * 85-byte envelope (stride 85), kind[r] (0 PrePrepare, 1 Prepare, 2 Commit),
+ * view[r], seq[r].  A PrePrepare row checks the primary's signature over the
+ * CLAIMED digest only: the caller still recomputes the digest of its operation
+ * (validate_digest, src/message.rs:139-145), as pbft_replica_push_frames does,
+ * and checks that key_idx is the view's primary; key_idx of a vote must be the
+ * authenticated connection's peer (src/behavior.rs:346, :380).  Outputs: *n_frames,
  * *n_rows, *consumed (bytes of whole frames).  Returns 0, or PBFT_EINVAL on a
  * framing error (bad varint / frame > PBFT_UVI_MAX_FRAME) at *consumed. */
 int pbft_wire_decode_votes(const uint8_t *stream, size_t len, uint32_t n_replicas, uint64_t max_frames,

@@ -489,7 +489,7 @@ int pbft_wire_decode_votes(const uint8_t* stream, size_t len, uint32_t n_replica
     pbft_wire_msg m;
     uint8_t st = PBFT_WIRE_OK;
     if (pbft_wire_decode_json(js, (size_t)fl, &m, arena, sizeof arena) != 0) st = PBFT_WIRE_EJSON;
-    else if (m.kind != PBFT_MSG_PREPARE && m.kind != PBFT_MSG_COMMIT) st = PBFT_WIRE_EKIND;
+    else if (m.kind == PBFT_MSG_CLIENT_REQUEST) st = PBFT_WIRE_EKIND;  // signed PrePrepares pass: kind-0 rows
     else if (!m.digest_ok) st = PBFT_WIRE_EDIGEST;
     else if (!m.has_sig) st = PBFT_WIRE_EUNSIGNED;
     else if (m.replica >= n_replicas) st = PBFT_WIRE_ESIGNER;
@@ -508,38 +508,6 @@ int pbft_wire_decode_votes(const uint8_t* stream, size_t len, uint32_t n_replica
     off += hn + (size_t)fl;
     *consumed = off;
   }
-  return 0;
-}
-
-int pbft_replica_push_frames(pbft_replica* r, const uint8_t* stream, size_t len, uint64_t* consumed,
-                             uint64_t* pushed, uint64_t* dropped) {
-  if (!r || !consumed || (!stream && len)) return PBFT_EINVAL;
-  constexpr uint64_t CH = 256;  // frames per decode call
-  uint8_t st[CH], Rb[CH * 32], Sb[CH * 32], Mb[CH * PBFT_ENVELOPE_BYTES], kd[CH];
-  uint16_t K[CH];
-  uint64_t vw[CH], sq[CH];
-  uint64_t np = 0, nd = 0;
-  size_t off = 0;
-  while (off < len) {
-    uint64_t nf, nr, used;
-    const int rc = pbft_wire_decode_votes(stream + off, len - off, 0xFFFFu, CH, CH, st, Rb, Sb, K, Mb, kd, vw, sq,
-                                          &nf, &nr, &used);
-    if (rc) { *consumed = off; return rc; }
-    if (nf == 0) break;  // incomplete frame
-    for (uint64_t j = 0; j < nr; ++j) {
-      uint8_t sig[64];
-      memcpy(sig, Rb + 32 * j, 32);
-      memcpy(sig + 32, Sb + 32 * j, 32);
-      // the envelope's digest bytes are the vote's digest (pbft_envelope layout: 21-byte header)
-      if (pbft_replica_push(r, kd[j], vw[j], sq[j], Mb + PBFT_ENVELOPE_BYTES * j + 21, K[j], sig) == 1) ++np;
-      else ++nd;
-    }
-    nd += nf - nr;
-    off += used;
-  }
-  *consumed = off;
-  if (pushed) *pushed = np;
-  if (dropped) *dropped = nd;
   return 0;
 }
 

@@ -320,6 +320,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
       a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
     }
     s_ok = sc_lt_L(s);
+    sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
     uint32_t h[16], k[8];
 #if PBFT_ABL_NOSHA  // ablation: no challenge hash (k from R and A directly)
 #pragma unroll
@@ -525,6 +526,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
       a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
     }
     s_ok = sc_lt_L(s);
+    sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
     uint32_t h[16], k[8];
     sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * ii, (int)msg_len);
     sc_reduce512(k, h);

@@ -194,6 +194,18 @@ struct digits {
   }
 };
 
+// The comb recodes s into table indices, and `digits` assumes s < 2^253 (the
+// top digit indexes the last position's table directly).  An attacker-supplied
+// s >= L is rejected by check_scalar anyway, but its digits would index past
+// the end of the base-point table (bit 253..255 set: up to 2^(W+2) entries too
+// far).  So a rejected s is replaced by 0 before recoding: the lane's result
+// is already decided (bit 0) and every gather stays inside the table.
+FE_FN void sc_clamp_rejected(uint32_t s[8], bool s_ok) {
+  const uint32_t m = 0u - (uint32_t)s_ok;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] &= m;
+}
+
 // y in {0, 1, p-1, y8, p-y8}: the y-coordinates of the 8 small-order points.
 FE_FN bool y_is_small_order(const uint32_t y[8]) {
   const uint32_t Y8A[8] = {0x8f95e826u, 0xb027b2c2u, 0x89f4c345u, 0xf098eff2u,
@@ -249,7 +261,11 @@ FE_FN bool verify_lane(const uint32_t r_enc[8], const uint32_t s[8], const uint3
 
   ge P;
   digits ds, dk;
-  ds.init(s);
+  uint32_t sc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) sc[i] = s[i];
+  sc_clamp_rejected(sc, s_ok);  // rejected s: recode 0 (no gather past the table)
+  ds.init(sc);
   dk.init(k);
   constexpr int PB = PLB::P, PA = PLA::P;
   static_for<(PB > PA ? PB : PA)>([&](auto ic) {

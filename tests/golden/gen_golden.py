@@ -52,6 +52,7 @@ CLASSES = {
     16: "A not on curve",
     17: "s = 0 / s = L-1 random R",
     18: "valid, s high nibble set (s >= 2^252)",
+    19: "s >= 2^253 (bits 253-255: 2^256-1, s + 2^253, s | 2^254)",
 }
 
 
@@ -234,6 +235,12 @@ def build_batch(rnd: random.Random, msg_len: int, n_valid: int, n_each_adv: int)
         sig, ki, m = valid_sig()
         sv = rnd.choice((0, E.L - 1))
         add(sig[:32] + sv.to_bytes(32, "little"), ki, m, 17)
+        # s with bits 253..255 set: rejected by check_scalar; recoded naively its top comb digit would index
+        # past the end of the base-point table
+        sig, ki, m = valid_sig()
+        s0 = int.from_bytes(sig[32:], "little")
+        sv = rnd.choice((2**256 - 1, s0 + 2**253, s0 | 2**254, s0 | 2**255 | 2**254 | 2**253))
+        add(sig[:32] + sv.to_bytes(32, "little"), ki, m, 19)
 
     # shuffle lanes so classes interleave within waves
     order = list(range(len(R)))

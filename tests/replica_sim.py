@@ -12,8 +12,8 @@ import numpy as np
 
 from conftest import ROOT
 
-KIND_PREPARE, KIND_COMMIT = 1, 2
-EV_PREPARED, EV_COMMITTED = 1, 2
+KIND_PREPREPARE, KIND_PREPARE, KIND_COMMIT = 0, 1, 2
+EV_PREPARED, EV_COMMITTED, EV_PRE_PREPARED = 1, 2, 3
 
 
 class Event(ctypes.Structure):
@@ -22,7 +22,9 @@ class Event(ctypes.Structure):
 
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("pushed", "verified", "accepted", "rejected_sig", "rejected_digest",
-                                                "rejected_view", "duplicates", "batches")]
+                                                "rejected_view", "duplicates", "batches", "rejected_watermark",
+                                                "rejected_signer", "dropped_flood", "windows_gc", "low_watermark",
+                                                "live_windows")]
 
 
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -39,7 +41,15 @@ def lib():
     L.pbft_replica_set_verifier.argtypes = [vp, VERIFY_FN, vp]
     L.pbft_replica_set_digest_fn.argtypes = [vp, DIGEST_FN, vp]
     L.pbft_replica_on_pre_prepare.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
-                                              ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p]
+                                              ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+    L.pbft_replica_push_frames.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, vp, vp, vp]
+    L.pbft_replica_set_log_window.argtypes = [vp, ctypes.c_uint64]
+    L.pbft_replica_stable_checkpoint.argtypes = [vp, ctypes.c_uint64]
+    L.pbft_replica_peer_index.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]
+    L.pbft_key_from_peer_id.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+    L.pbft_key_from_peer_id_b58.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+    L.pbft_peer_id_from_key.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L.pbft_peer_id_from_key.restype = None
     L.pbft_replica_push.argtypes = [vp, ctypes.c_uint8, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
                                     ctypes.c_uint32, ctypes.c_char_p]
     L.pbft_replica_flush.argtypes = [vp, ctypes.c_int, ctypes.POINTER(Event), ctypes.c_uint32,
@@ -114,11 +124,21 @@ class Cluster:
         self.o.oracle_sign(sig, self.seeds[i], env.raw, 85)
         return sig.raw
 
-    def flush(self, i, force=0):
-        ev = (Event * 64)()
+    def flush(self, i, force=0, max_events=4096):
+        ev = (Event * max_events)()
         ne = ctypes.c_uint32()
-        assert self.L.pbft_replica_flush(self.reps[i], force, ev, 64, ctypes.byref(ne)) == 0
+        assert self.L.pbft_replica_flush(self.reps[i], force, ev, max_events, ctypes.byref(ne)) == 0
         return [(e.view, e.seq, e.kind) for e in ev[: ne.value]]
+
+    def primary(self, view=1):
+        return view % self.n
+
+    def pre_prepare(self, i, view, seq, op, digest=None, sig=None):
+        """Deliver the primary's signed PrePrepare for (view, seq) to replica i."""
+        d = hashlib.blake2b(op, digest_size=64).digest() if digest is None else digest
+        if sig is None:
+            sig = self.sign(self.primary(view), KIND_PREPREPARE, view, seq, d)
+        return self.L.pbft_replica_on_pre_prepare(self.reps[i], view, seq, op, len(op), d, sig, None)
 
     def stats(self, i):
         s = Stats()
@@ -128,3 +148,62 @@ class Cluster:
     def close(self):
         for r in self.reps:
             self.L.pbft_replica_destroy(r)
+
+
+class PhaseSim:
+    """Phase-ordered PBFT rounds over an in-process network (SURVEY.md §3 S2-S4 in Castro-Liskov order):
+    the primary multicasts a signed PrePrepare; a replica sends its Prepare only after the PRE_PREPARED event and
+    its Commit only after PREPARED.  `silent` replicas never send anything; `forgers` send, before every honest
+    vote, a garbage-signature vote under each honest replica's id (`pbft_replica_push` with a spoofed signer:
+    what a transport that trusted the frame's field would deliver).  Flushes are never forced."""
+
+    def __init__(self, cluster, silent=(), forgers=(), op=b"testOperation"):
+        self.c, self.silent, self.forgers, self.op = cluster, set(silent), set(forgers), op
+        self.D = hashlib.blake2b(op, digest_size=64).digest()
+        self.inbox = {i: [] for i in range(cluster.n)}
+        self.events = {i: [] for i in range(cluster.n)}
+
+    def honest(self):
+        return [i for i in range(self.c.n) if i not in self.silent and i not in self.forgers]
+
+    def _multicast(self, src, kind, view, seq):
+        sig = self.c.sign(src, kind, view, seq, self.D)
+        for dst in range(self.c.n):
+            if self.forgers:
+                bad = bytes([sig[0] ^ 0x55]) + sig[1:]
+                self.inbox[dst].append((kind, view, seq, self.D, src, bad))
+            self.inbox[dst].append((kind, view, seq, self.D, src, sig))
+
+    def start(self, view, seqs):
+        p = self.c.primary(view)
+        assert p not in self.silent
+        for q in seqs:
+            for i in range(self.c.n):
+                assert self.c.pre_prepare(i, view, q, self.op) == 1
+
+    def run(self, max_rounds=20):
+        """Deliver, flush (never forced), react to events; until quiescent.  Returns rounds used."""
+        L = self.c.L
+        for rnd in range(max_rounds):
+            progressed = False
+            for i in range(self.c.n):
+                box, self.inbox[i] = self.inbox[i], []
+                for kind, view, seq, d, src, sig in box:
+                    L.pbft_replica_push(self.c.reps[i], kind, view, seq, d, src, sig)
+                    progressed = True
+            for i in range(self.c.n):
+                if i in self.silent:
+                    continue
+                for v, q, k in self.c.flush(i):
+                    progressed = True
+                    self.events[i].append((v, q, k))
+                    if k == EV_PRE_PREPARED:
+                        self._multicast(i, KIND_PREPARE, v, q)
+                    elif k == EV_PREPARED:
+                        self._multicast(i, KIND_COMMIT, v, q)
+            if not progressed:
+                return rnd
+        return max_rounds
+
+    def committed(self, i, view, seqs):
+        return all((view, q, EV_COMMITTED) in self.events[i] for q in seqs)

@@ -81,19 +81,19 @@ def adversarial(rng, pub, R, S, key_idx, msg, frac=0.01):
     """Mutate a seeded `frac` of lanes across the §8(d) adversarial classes."""
     R, S, key_idx, msg = R.copy(), S.copy(), key_idx.copy(), msg.copy()
     n = len(R)
-    idx = rng.choice(n, size=max(11, int(n * frac)), replace=False)
+    idx = rng.choice(n, size=max(12, int(n * frac)), replace=False)
     so = [bytes.fromhex(h) for h in KAT["small_order_encodings"]]
     nc = [bytes.fromhex(h) for h in KAT["noncanonical_decodable_encodings"]]
     # an encoding that does not decode (y^2 - 1)/(d y^2 + 1) non-square: y = 2 is one
     noc = (2).to_bytes(32, "little")
     for j, i in enumerate(idx):
-        c = j % 11
+        c = j % 12
         if c == 0:
             msg[i, rng.integers(85)] ^= 1 << rng.integers(8)
         elif c == 1:
             R[i, rng.integers(32)] ^= 1 << rng.integers(8)
         elif c == 2:
-            S[i, rng.integers(31)] ^= 1 << rng.integers(8)
+            S[i, rng.integers(32)] ^= 1 << rng.integers(8)  # byte 31 too: bits 253..255 (VERDICT r01 item 2)
         elif c == 3:
             s = int.from_bytes(S[i].tobytes(), "little") + L
             S[i] = np.frombuffer(s.to_bytes(32, "little"), dtype=np.uint8)
@@ -110,8 +110,14 @@ def adversarial(rng, pub, R, S, key_idx, msg, frac=0.01):
         elif c == 9:
             R[i] = 0
             S[i] = 0
-        else:
+        elif c == 10:
             key_idx[i] = len(pub) + 3  # out of the installed key set
+        else:  # s >= 2^253: rejected, and must not gather past the end of the base-point table
+            top = (0xff, 0x20, 0x40, 0xe0)[j % 4]
+            if top == 0xff:
+                S[i] = 0xff
+            else:
+                S[i, 31] |= top
     return R, S, key_idx, msg, idx
 
 

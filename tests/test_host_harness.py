@@ -134,3 +134,59 @@ def test_verify_lane_golden(hh, golden, W):
                                   b["R"].ctypes.data, b["S"].ctypes.data, b["key_idx"].ctypes.data, mbuf.ctypes.data,
                                   ml, stride, n, acc.ctypes.data) == 0
         assert (acc == b["expected"]).all(), (ml, np.nonzero(acc != b["expected"])[0][:10])
+
+
+_GUARD_SCRIPT = r"""
+import ctypes, sys
+import numpy as np
+sys.path.insert(0, {tests!r})
+from conftest import golden_batches
+lib = ctypes.CDLL({lib!r})
+vp = ctypes.c_void_p
+lib.hh_guard_verify.argtypes = [ctypes.c_char_p, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, vp,
+                                ctypes.c_int]
+g = np.load({npz!r})
+b = dict(golden_batches(g))[85]
+probe = {probe}
+sel = np.nonzero((b["key_idx"] == 0) & np.isin(b["cls"], [0, 3, 4, 5, 17, 19]))[0]
+if probe:
+    sel = sel[b["cls"][sel] == 19]
+R, S = np.ascontiguousarray(b["R"][sel]), np.ascontiguousarray(b["S"][sel])
+if probe:
+    S[:] = 0xff  # s = 2^256 - 1
+M = np.zeros(len(sel) * 85 + 16, np.uint8)
+M[: len(sel) * 85] = b["msg"][sel].ravel()
+acc = np.zeros(len(sel), np.uint8)
+rc = lib.hh_guard_verify(b["keys"][0].tobytes(), R.ctypes.data, S.ctypes.data, M.ctypes.data, 85, 85, len(sel),
+                         acc.ctypes.data, probe)
+assert rc == 0, rc
+if not probe:
+    assert (acc == b["expected"][sel]).all()
+    assert (b["cls"][sel] == 19).sum() >= 1
+print("ok", len(sel))
+"""
+
+
+def _guard_run(probe: int):
+    import subprocess
+    import sys
+    lib = os.path.join(ROOT, "tests", "native", "libhost_harness.so")
+    if not os.path.exists(lib):
+        pytest.skip("host harness not built")
+    code = _GUARD_SCRIPT.format(tests=os.path.join(ROOT, "tests"), lib=lib,
+                                npz=os.path.join(ROOT, "tests", "golden", "verify_vectors.npz"), probe=probe)
+    return subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+
+
+def test_guard_page_no_gather_past_tables():
+    """both comb tables end at a PROT_NONE page; the product's verify_lane on golden lanes incl.
+    class 19 (s with bits 253..255 set) reads nothing past either table and gives the oracle's bits."""
+    p = _guard_run(0)
+    assert p.returncode == 0 and p.stdout.startswith("ok"), (p.returncode, p.stdout, p.stderr[-2000:])
+
+
+def test_guard_page_catches_unclamped_recoding():
+    """Negative control: recoding s = 2^256 - 1 WITHOUT the s < L clamp (the r01 kernels) faults on the guard page,
+    so the test above would have caught the defect."""
+    p = _guard_run(1)
+    assert p.returncode == -11, (p.returncode, p.stdout, p.stderr[-2000:])

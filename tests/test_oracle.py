@@ -120,9 +120,9 @@ def test_golden_expected_is_python_oracle(golden):
 def test_golden_class_coverage(golden):
     b = dict(golden_batches(golden))[85]
     cls, exp = b["cls"], b["expected"]
-    assert set(cls.tolist()) >= set(range(18))
+    assert set(cls.tolist()) >= set(range(18)) | {19}
     assert exp[cls == 0].all() and exp[cls == 18].all() and exp[cls == 10].all()  # valid + mixed-order accept
-    for c in range(1, 18):
+    for c in list(range(1, 18)) + [19]:
         if c != 10:
             assert not exp[cls == c].any(), c
 
@@ -155,7 +155,7 @@ def _sodium():
 
 
 # classes where libsodium 1.0.18's verify_detached == dalek verify_strict
-SODIUM_AGREES = {0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16, 17, 18}
+SODIUM_AGREES = {0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 16, 17, 18, 19}
 
 
 def test_libsodium_agrees_on_its_classes(golden):
@@ -179,7 +179,7 @@ def test_libsodium_agrees_on_its_classes(golden):
 
 
 # classes without small-order/torsion points or non-canonical encodings: OpenSSL == dalek
-OPENSSL_AGREES = {0, 1, 2, 3, 4, 5, 6, 11, 16, 17, 18}
+OPENSSL_AGREES = {0, 1, 2, 3, 4, 5, 6, 11, 16, 17, 18, 19}
 
 
 def test_openssl_agrees_on_its_classes(golden):

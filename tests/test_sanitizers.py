@@ -1,0 +1,47 @@
+"""Host code under AddressSanitizer + UndefinedBehaviorSanitizer (VERDICT r01 missing item 8).
+
+tests/native/sanitize_main.cpp links the product's host sources (replica.cpp, wire.cpp) and the host build of the
+kernels' __host__ __device__ arithmetic (verify_core.h, digest_kernels.h) with -fsanitize=address,undefined and
+no recovery: any heap/stack overflow (e.g. a comb gather past an exactly-sized table on s >= 2^253), use after
+free or undefined behaviour aborts the run.  Host only: nothing here touches a GPU.
+"""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+NATIVE = os.path.join(ROOT, "tests", "native")
+BIN = os.path.join(NATIVE, "sanitize_main")
+SRCS = [os.path.join(NATIVE, "sanitize_main.cpp"),
+        os.path.join(ROOT, "pbft_amd", "csrc", "host", "replica.cpp"),
+        os.path.join(ROOT, "pbft_amd", "csrc", "host", "wire.cpp")]
+DEPS = SRCS + [os.path.join(ROOT, "pbft_amd", "csrc", f) for f in os.listdir(os.path.join(ROOT, "pbft_amd", "csrc"))
+               if f.endswith(".h")] + [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SAN = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+       "-Xarch_host", "-fno-sanitize-recover=all"]
+
+
+def _build():
+    if os.path.exists(BIN) and all(os.path.getmtime(d) <= os.path.getmtime(BIN) for d in DEPS):
+        return
+    if not os.path.exists(HIPCC):
+        pytest.skip("hipcc not present")
+    cmd = [HIPCC, "--offload-host-only", "-O0", "-g", "-std=c++17", "-fno-omit-frame-pointer"] + SAN + \
+          ["-o", BIN] + SRCS
+    subprocess.run(cmd, check=True, timeout=600)
+
+
+def test_host_code_clean_under_asan_ubsan():
+    _build()
+    env = dict(os.environ)
+    sym = "/opt/rocm/lib/llvm/bin/llvm-symbolizer"
+    if os.path.exists(sym):
+        env["ASAN_SYMBOLIZER_PATH"] = sym
+    env["ASAN_OPTIONS"] = "detect_leaks=1:abort_on_error=0:halt_on_error=1"
+    p = subprocess.run([BIN], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
+    assert "sanitized host run ok" in p.stdout
+    assert "arithmetic: 120 accepted, 120 rejected" in p.stdout

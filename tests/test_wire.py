@@ -138,7 +138,10 @@ def test_decode_votes_stream_to_soa():
         if r < 0.1:
             m.sig, m.replica, st = None, None, 3                     # unsigned (reference-format) vote
         elif r < 0.15:
-            m.kind, m.operation, m.client, st = PREPREPARE, b"x", "1.1.1.1:1", 4
+            m.kind, m.operation, m.client, st = PREPREPARE, b"x", "1.1.1.1:1", 0  # signed PrePrepare: kind-0 row
+        elif r < 0.17:
+            m = WireMsg(kind=CLIENT_REQUEST, operation=b"op", timestamp=3, client="1.1.1.1:1")
+            st = 4                                                    # not a replica-signed message
         elif r < 0.2:
             st = 5 if m.replica >= 4 else 0                           # n_replicas = 4 below
         frame = wire.encode_frame(m)
