@@ -1,26 +1,34 @@
 #!/usr/bin/env python3
-"""Benchmark: Ed25519 verifies/s per node on PBFT round batches (BASELINE.json metric).
+"""Benchmark: Ed25519 verifies/s per node on 1M-signature PBFT rounds (BASELINE.json metric).
 
-Workload (BASELINE.json configs[3], weak-scaled): n = 256 replicas; every
-replica signs a Prepare and a Commit envelope for each of 2048 sequence
-numbers -> 2^20 signatures per GPU per step ("one config-#4 round per GPU").
-A step = one pass of the hot path over that batch with inputs resident in HBM:
-the verify kernel (SHA-512 challenge, scalar reduction, comb double-scalar
-multiplication, compression, compare, ballot) followed, for N > 1, by the RCCL
-all-gather of the per-GPU accept bitmaps over xGMI (the round's exchange step).
+Workload (BASELINE.json configs[3]): ONE round of n = 256 replicas x 2048
+sequence numbers x {Prepare, Commit} = 2^20 signed 85-byte envelopes, sharded
+by signature index over the N GPUs of the node (pbft_amd.dist.shard_bounds:
+contiguous, 64-aligned).  A step = every rank verifies its shard with inputs
+resident in HBM (verify kernels: SHA-512 challenge, scalar reduction, comb
+double-scalar multiplication, compression, compare, ballot), then the per-rank
+bitmaps are combined with one RCCL all-gather over xGMI into the round's
+bitmap.  value = 2^20 x steps / max-over-ranks wall time (strong scaling: the
+round is fixed, more GPUs share it).  0.1 % of the round's signatures are
+corrupted (seeded positions): the assembled bitmap is checked against them.
+A weak-scaling figure (every rank verifies a whole 2^20 round) is reported
+beside it as `weak_scaling`.
 
 Synthetic data: sk_i = SHA-512("pbft-key" || seed || i)[0:32],
 85-byte envelope "PBFT" || kind || view u64 || seq u64 || Blake2b-512("op-"||seq),
 signatures produced by the product's own GPU signer (pbft_sign_batch).
 
-Also reported: the dominant kernel's roofline (VALU integer products, see
-DESIGN.md §Roofline), p50 latency of a 4096-signature round (config #5's batch
-size), and the CPU baseline = the oracle's C restatement timed on this host
-(rank 0 only, bounded sample).
+Rank 0 at N = 1 also reports: the dominant kernels' roofline, the 131k-signature
+shard an 8-GPU node gives each GPU, the host-buffer (PCIe-inclusive) 2^20 round,
+config #2 (n = 4, 1,024 pipelined requests = 8,192 signatures), p50 of a
+4096-signature round and config #5 streaming, and two CPU baselines on this
+host's cores: the oracle's C restatement ("port") and OpenSSL EVP_DigestVerify
+(the SURVEY.md §8c substitute for ed25519-dalek).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -33,10 +41,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 N_REPLICAS = 256
-SEQS_PER_GPU = 2048
+SEQS = 2048
 ENVELOPE = 85
-# algorithmic 32x32->64 products per verify for the comb algorithm
 SEED = 0x5EED0000 + 4
+ADV_FRAC = 0.001
 
 
 def key_seeds(n: int, seed: int = SEED) -> np.ndarray:
@@ -60,6 +68,15 @@ def envelopes(seq0: int, n_seq: int, n_rep: int):
     return msg, key_idx
 
 
+def corrupt(S: np.ndarray, frac: float, seed: int):
+    """Flip one bit of s in a seeded `frac` of the signatures; returns the corrupted copy and the positions."""
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(len(S), size=max(1, int(len(S) * frac)), replace=False))
+    S = S.copy()
+    S[idx, rng.integers(0, 31, len(idx))] ^= np.uint8(4)
+    return S, idx
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -67,48 +84,77 @@ def dist_env():
     return ws, rank, local
 
 
-def cpu_baseline(keys, R, S, key_idx, msg, budget_s: float = 12.0):
-    """Oracle C restatement (oracle/ed25519_oracle.c) on this host's cores."""
-    import ctypes
-    lib_path = os.path.join(ROOT, "oracle", "liboracle.so")
-    if not os.path.exists(lib_path):
-        return None
-    lib = ctypes.CDLL(lib_path)
-    vp = ctypes.c_void_p
-    lib.oracle_verify_batch.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
-                                        ctypes.c_uint64, vp, ctypes.c_int]
+def host_cores() -> int:
     cores = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
-    cores = max(1, min(int(os.environ.get("OMP_NUM_THREADS", cores)), cores))
-    # calibrate on a small sample, then run ~budget_s seconds of work
-    n0 = min(len(R), 512 * cores)
+    return max(1, min(int(os.environ.get("OMP_NUM_THREADS", cores)), cores))
+
+
+def _cpu_lib(name: str, fn: str):
+    path = os.path.join(ROOT, "oracle", name)
+    if not os.path.exists(path):
+        return None
+    lib = ctypes.CDLL(path)
+    vp = ctypes.c_void_p
+    getattr(lib, fn).argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
+                                 ctypes.c_uint64, vp, ctypes.c_int]
+    return lib
+
+
+def cpu_rate(fn, keys, R, S, key_idx, msg, budget_s: float, cores: int, expect=None):
+    """Calibrate on a small sample, then time ~budget_s seconds of the same batch on `cores` threads."""
     out = np.zeros(len(R), dtype=np.uint8)
+    args = lambda n: (keys.ctypes.data, len(keys), R.ctypes.data, S.ctypes.data, key_idx.ctypes.data,  # noqa: E731
+                      msg.ctypes.data, ENVELOPE, ENVELOPE, n, out.ctypes.data, cores)
+    n0 = min(len(R), 256 * cores)
     t = time.perf_counter()
-    lib.oracle_verify_batch(keys.ctypes.data, len(keys), R.ctypes.data, S.ctypes.data, key_idx.ctypes.data,
-                            msg.ctypes.data, ENVELOPE, ENVELOPE, n0, out.ctypes.data, cores)
+    fn(*args(n0))
     rate0 = n0 / (time.perf_counter() - t)
     n = int(min(len(R), max(n0, rate0 * budget_s)))
     t = time.perf_counter()
-    lib.oracle_verify_batch(keys.ctypes.data, len(keys), R.ctypes.data, S.ctypes.data, key_idx.ctypes.data,
-                            msg.ctypes.data, ENVELOPE, ENVELOPE, n, out.ctypes.data, cores)
+    fn(*args(n))
     dt = time.perf_counter() - t
-    assert out[:n].all(), "CPU oracle rejected a valid synthetic signature"
-    return {"value": n / dt, "unit": "verifies/s", "cores": cores, "kind": "port",
-            "sample": f"first {n} signatures of the rank-0 round (n=256 replicas, 85-B envelopes), "
-                      f"{dt:.1f} s, {cores} threads of oracle/ed25519_oracle.c"}
+    if expect is not None:
+        assert (out[:n].astype(bool) == expect[:n]).all(), "CPU baseline disagrees with the expected bits"
+    return n / dt, n, dt
+
+
+def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
+    cores = host_cores()
+    res = {}
+    o = _cpu_lib("liboracle.so", "oracle_verify_batch")
+    if o is not None:
+        v, n, dt = cpu_rate(o.oracle_verify_batch, keys, R, S, key_idx, msg, budget_s, cores, expect)
+        res["port"] = {"value": v, "unit": "verifies/s", "cores": cores, "kind": "port",
+                       "sample": f"first {n} signatures of the config-#4 round (n=256, 85-B envelopes, 0.1% "
+                                 f"corrupted), {dt:.1f} s, {cores} threads of oracle/ed25519_oracle.c "
+                                 f"(dalek verify_strict restatement)"}
+    s = _cpu_lib("libossl_baseline.so", "ossl_verify_batch")
+    if s is not None:
+        s.ossl_version.restype = ctypes.c_char_p
+        v, n, dt = cpu_rate(s.ossl_verify_batch, keys, R, S, key_idx, msg, budget_s, cores, expect)
+        res["openssl"] = {"value": v, "unit": "verifies/s", "cores": cores, "kind": "openssl-substitute",
+                          "sample": f"first {n} signatures of the config-#4 round, {dt:.1f} s, {cores} threads of "
+                                    f"{s.ossl_version().decode()} EVP_DigestVerify (oracle/openssl_baseline.c; "
+                                    f"SURVEY §8c substitute for ed25519-dalek verify_batch)"}
+    return res
 
 
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_pmc_cur.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
-    p = os.path.join(ROOT, "profiles", "r01_pmc_comb", "derived.json")
-    try:
-        d = json.load(open(p))
-    except (OSError, ValueError):
-        return {}
-    if d.get("sigs_per_launch") != n or f"PB={pb} PA={pa}" not in d.get("launch", ""):
-        return {}
-    return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"], "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
-            "source": "profiles/r01_pmc_comb/derived.json (PMC passes, not this run)"}
+    for rnd in ("r02", "r01"):
+        p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_comb", "derived.json")
+        try:
+            d = json.load(open(p))
+        except (OSError, ValueError):
+            continue
+        if d.get("sigs_per_launch") != n or f"PB={pb} PA={pa}" not in d.get("launch", ""):
+            continue
+        return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
+                "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
+                "valu_insts_per_sig": d["comb_kernel"].get("valu_insts_per_sig"),
+                "source": f"profiles/{rnd}_pmc_comb/derived.json (PMC passes, not this run)"}
+    return {}
 
 
 def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int = 4096, n_ctx: int = 4,
@@ -146,7 +192,7 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
         if now >= t_sched:
             ci = k % n_ctx
             if pending[ci] is not None:  # backlog: this stream is still busy
-                b = ctxs[ci].wait(pending[ci][0])
+                ctxs[ci].wait(pending[ci][0])
                 lat.append((time.perf_counter() - pending[ci][1]) * 1e3)
                 done += 1
             pending[ci] = (ctxs[ci].submit(batches[k % len(batches)]), t_sched if period else time.perf_counter())
@@ -159,7 +205,99 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
             "offered_sigs_per_s": offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else None,
             "achieved_sigs_per_s": done * batch / wall, "batches": int(done),
             "p50_ms": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)),
-            "path": "host buffers: H2D + comb + finish + D2H per batch"}
+            "path": "host buffers: H2D + verify kernels + D2H per batch"}
+
+
+def time_device(v, stream, d, n, iters, torch):
+    """Average ms of `iters` back-to-back device-resident launches over the first n signatures (HIP events on the
+    launch stream), and the wall ms per launch."""
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    e0.record(stream)
+    for _ in range(iters):
+        v.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                        ENVELOPE, n, d["B"].data_ptr(), stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters, (time.perf_counter() - t) * 1e3 / iters
+
+
+def to_device(torch, dev, R, S, key_idx, msg):
+    n = len(R)
+    msg_pad = np.zeros(n * ENVELOPE + 64, dtype=np.uint8)  # + slack for unaligned tail reads
+    msg_pad[: n * ENVELOPE] = msg.reshape(-1)
+    return {"R": torch.from_numpy(np.ascontiguousarray(R)).to(dev),
+            "S": torch.from_numpy(np.ascontiguousarray(S)).to(dev),
+            "K": torch.from_numpy(np.ascontiguousarray(key_idx).view(np.int16)).to(dev),
+            "M": torch.from_numpy(msg_pad).to(dev),
+            "B": torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)}
+
+
+def e2e_host_round(v, R, S, key_idx, msg, expect, torch, iters: int = 5):
+    """PCIe-inclusive 2^20 round: pinned host buffers -> pbft_verify_batch (chunked H2D on a copy stream overlapping
+    the verify kernels, bitmap D2H).  Returns verifies/s and ms per round (median of iters)."""
+    from pbft_amd import SigBatch, bitmap_to_bool
+    n = len(R)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()  # noqa: E731
+    b = SigBatch(pin(R), pin(S), pin(key_idx), pin(msg), ENVELOPE)
+    bm = v.verify(b)  # warm (staging allocation)
+    assert (bitmap_to_bool(bm, n) == expect).all(), "host-buffer path bitmap differs"
+    ts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        v.verify(b)
+        ts.append(time.perf_counter() - t)
+    ms = float(np.median(ts)) * 1e3
+    return {"value": n / (ms * 1e-3), "unit": "verifies/s", "ms_per_round": ms, "sigs": n,
+            "path": "pinned host buffers: H2D (2^18-signature chunks on a copy stream, overlapped) + verify kernels "
+                    "+ bitmap D2H, pbft_verify_batch", "bytes_h2d_per_sig": 32 + 32 + 2 + ENVELOPE}
+
+
+def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
+    """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 signatures per window batch, one GPU
+    (device-resident p50 and host-buffer p50) vs the CPU baselines on the same batch."""
+    from pbft_amd import SigBatch, bitmap_to_bool
+    c = v.clone()
+    try:
+        seeds = key_seeds(4, 0x5EED0000 + 2)
+        msg, key_idx = envelopes(1, 1024, 4)
+        R, S, pub = c.sign(seeds, key_idx, msg, ENVELOPE)
+        assert c.set_keys(pub).all()
+        d = to_device(torch, dev, R, S, key_idx, msg)
+        lat = []
+        for it in range(iters + 5):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            c.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                            ENVELOPE, len(R), d["B"].data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            if it >= 5:
+                lat.append((time.perf_counter() - t) * 1e3)
+        assert bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), len(R)).all()
+        host = []
+        b = SigBatch(R, S, key_idx, msg, ENVELOPE)
+        for it in range(min(iters, 100) + 3):
+            t = time.perf_counter()
+            bm = c.verify(b)
+            if it >= 3:
+                host.append((time.perf_counter() - t) * 1e3)
+        assert bitmap_to_bool(bm, len(R)).all()
+        out = {"sigs": len(R), "replicas": 4, "requests": 1024,
+               "device_p50_ms": float(np.median(lat)), "device_verifies_per_s": len(R) / (np.median(lat) * 1e-3),
+               "host_buffer_p50_ms": float(np.median(host))}
+        if cpu:
+            cores = host_cores()
+            for name, lib, fn in (("cpu_port", "liboracle.so", "oracle_verify_batch"),
+                                  ("cpu_openssl", "libossl_baseline.so", "ossl_verify_batch")):
+                L = _cpu_lib(lib, fn)
+                if L is not None:
+                    rate, n, dt = cpu_rate(getattr(L, fn), pub, R, S, key_idx, msg, 2.0, cores,
+                                           np.ones(len(R), bool))
+                    out[name] = {"verifies_per_s": rate, "window_ms": len(R) / rate * 1e3, "cores": cores}
+        return out
+    finally:
+        c.close()
 
 
 def main():
@@ -167,9 +305,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--seqs", type=int, default=SEQS_PER_GPU, help="sequence numbers per GPU per round")
+    ap.add_argument("--seqs", type=int, default=SEQS, help="sequence numbers in the round (2 x replicas x seqs sigs)")
     ap.add_argument("--replicas", type=int, default=N_REPLICAS)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="only the headline line (no side legs)")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--settle-s", type=float, default=0.3, help="untimed GPU settle time before the warmup steps")
     args = ap.parse_args()
@@ -185,50 +324,52 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
-    from pbft_amd.dist import allgather_bitmap
-    from pbft_amd import _lib
+    from pbft_amd.dist import allgather_bitmap, round_bitmap, shard_bounds, shard_words
     from pbft_amd.roofline import INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_per_verify
 
     n_rep, n_seq = args.replicas, args.seqs
     seeds = key_seeds(n_rep)
-    msg, key_idx = envelopes(1 + rank * n_seq, n_seq, n_rep)
-    n = len(msg)
+    msg, key_idx = envelopes(1, n_seq, n_rep)
+    n_total = len(msg)
     v = GpuBatchVerifier(local)
-    # the product's GPU signer produces the round (and the replica public keys)
-    R, S, pub = v.sign(seeds, key_idx, msg, ENVELOPE)
+    # the product's GPU signer produces the round (and the replica public keys); every rank builds the same round
+    R, S_good, pub = v.sign(seeds, key_idx, msg, ENVELOPE)
+    S, bad = corrupt(S_good, ADV_FRAC, SEED)
+    expect = np.ones(n_total, bool)
+    expect[bad] = False
     key_ok = v.set_keys(pub)
     assert key_ok.all()
     pb, pa = v.positions()  # the key plan set_keys chose for this key set
-    PRODUCTS_PER_VERIFY = products_per_verify(pb, pa)
 
     dev = torch.device("cuda", local)
-    d_R = torch.from_numpy(R).to(dev)
-    d_S = torch.from_numpy(S).to(dev)
-    d_K = torch.from_numpy(key_idx.view(np.int16)).to(dev)
-    msg_pad = np.zeros(n * ENVELOPE + 64, dtype=np.uint8)  # +slack for unaligned tail reads
-    msg_pad[: n * ENVELOPE] = msg.reshape(-1)
-    d_M = torch.from_numpy(msg_pad).to(dev)
-    words = (n + 63) // 64
-    d_B = torch.zeros(words, dtype=torch.int64, device=dev)
-    d_all = torch.zeros(words * ws, dtype=torch.int64, device=dev)
-    # a dedicated (non-null) stream: kernel, events and the all-gather are ordered on it
+    lo, hi = shard_bounds(n_total, rank, ws)
+    n = hi - lo
+    d = to_device(torch, dev, R[lo:hi], S[lo:hi], key_idx[lo:hi], msg[lo:hi])
+    per_words = shard_words(n_total, ws)
+    d_local = torch.zeros(per_words, dtype=torch.int64, device=dev)   # this rank's bitmap words (padded)
+    d_all = torch.zeros(per_words * ws, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
-    stream = torch.cuda.Stream(dev)
+    stream = torch.cuda.Stream(dev)  # a dedicated stream: kernels, events and the all-gather are ordered on it
     torch.cuda.set_stream(stream)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
-        v.verify_device(d_R.data_ptr(), d_S.data_ptr(), d_K.data_ptr(), d_M.data_ptr(), ENVELOPE, ENVELOPE, n,
-                        d_B.data_ptr(), stream.cuda_stream)
+        if n:
+            v.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                            ENVELOPE, n, d_local.data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
         if ws > 1:
-            allgather_bitmap(d_B, ws, d_all)
+            allgather_bitmap(d_local, ws, d_all)
+
+    def check_round():
+        words = round_bitmap(d_local, n_total, ws, d_all)
+        got = bitmap_to_bool(words.cpu().numpy().view(np.uint64), n_total)
+        assert (got == expect).all(), f"round bitmap differs from the expected bits at {np.nonzero(got != expect)[0][:8]}"
 
     # Settle: the table builds just ran the GPU flat out; keep launching rounds for --settle-s seconds so that
-    # clocks and address-translation caches reach steady state before the W warmup + K timed steps (measured:
-    # 3 warmup steps alone leave the first timed rounds ~5 % slow).  Untimed, reported in the line.
+    # clocks and address-translation caches reach steady state before the W warmup + K timed steps.
     t_settle = time.perf_counter()
     while time.perf_counter() - t_settle < args.settle_s:
         step()
@@ -236,9 +377,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness sanity on the real round: every synthetic signature is valid
-    bm = d_B.cpu().numpy().view(np.uint64)
-    assert bitmap_to_bool(bm, n).all(), "GPU rejected a valid synthetic signature"
+    check_round()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if ws > 1:
@@ -257,33 +396,70 @@ def main():
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-        full = d_all.cpu().numpy().view(np.uint64)
-        assert bitmap_to_bool(full, words * 64 * ws).sum() >= 0
+    check_round()  # the bitmap of the last timed step, assembled from every rank's shard
 
-    # p50 latency of a 4096-signature round (config #5 batch size), device-resident
-    lat = []
-    if rank == 0 and args.latency_iters > 0:
+    # weak-scaling figure (labelled, not the headline): every rank verifies the WHOLE round
+    weak = None
+    if not args.no_extras:
+        dw = to_device(torch, dev, R, S, key_idx, msg) if ws > 1 else d
+        wb = torch.zeros((n_total + 63) // 64, dtype=torch.int64, device=dev)
+        dw["B"] = wb
+        time_device(v, stream, dw, n_total, 2, torch)
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            v.verify_device(dw["R"].data_ptr(), dw["S"].data_ptr(), dw["K"].data_ptr(), dw["M"].data_ptr(),
+                            ENVELOPE, ENVELOPE, n_total, wb.data_ptr(), stream.cuda_stream)
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        wdt = time.perf_counter() - t
+        if ws > 1:
+            tt = torch.tensor([wdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            wdt = float(tt.item())
+        weak = {"value": n_total * ws * args.steps / wdt, "unit": "verifies/s", "scaling": "weak",
+                "sigs_per_gpu": n_total, "ms_per_step": wdt / args.steps * 1e3,
+                "note": "every rank verifies a whole 2^20 round (no exchange)"}
+        if dw is not d:
+            del dw
+        got = bitmap_to_bool(wb.cpu().numpy().view(np.uint64), n_total)
+        assert (got == expect).all()
+
+    extras = {}
+    if rank == 0 and not args.no_extras and ws == 1:
+        # the per-GPU shard of an 8-GPU node (131,072 signatures): kernel time with the finish width it selects
+        n8 = shard_bounds(n_total, 0, 8)[1]
+        k8, w8 = time_device(v, stream, d, n8, 50, torch)
+        extras["shard_of_8"] = {"sigs": n8, "kernel_ms": k8, "wall_ms_per_launch": w8,
+                                "verifies_per_s_per_gpu": n8 / (k8 * 1e-3),
+                                "note": "device-resident launch over the shard one GPU of 8 verifies"}
+        # p50 latency of a 4096-signature round (config #5 batch size), device-resident
+        lat = []
         n4 = min(4096, n)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for it in range(args.latency_iters + 5):
             torch.cuda.synchronize()
             t = time.perf_counter()
-            v.verify_device(d_R.data_ptr(), d_S.data_ptr(), d_K.data_ptr(), d_M.data_ptr(), ENVELOPE, ENVELOPE,
-                            n4, d_B.data_ptr(), stream.cuda_stream)
+            v.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                            ENVELOPE, n4, d["B"].data_ptr(), stream.cuda_stream)
             torch.cuda.synchronize()
             if it >= 5:
                 lat.append((time.perf_counter() - t) * 1e3)
+        extras["p50_ms_4k_round"] = float(np.median(lat))
+        extras["p99_ms_4k_round"] = float(np.percentile(lat, 99))
+        # config #5: 2^24 sigs/s offered to an 8-GPU node = 2^21 per GPU; and back-to-back 4k batches
+        extras["stream_4k"] = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21)),
+                               "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
+        extras["e2e_2^20"] = e2e_host_round(v, R, S, key_idx, msg, expect, torch)
+        extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
 
     if rank == 0:
-        total = n * ws * args.steps
+        total = n_total * args.steps
         value = total / dt
-        products = PRODUCTS_PER_VERIFY * n / (kern_avg * 1e-3)
-        stream = None
-        if args.latency_iters > 0:
-            # config #5: 2^24 sigs/s offered to an 8-GPU node = 2^21 per GPU; and back-to-back 4k batches
-            stream = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21)),
-                      "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
-        cpu = None if args.no_cpu else cpu_baseline(pub, R, S, key_idx, msg)
+        products = products_per_verify(pb, pa) * n / (kern_avg * 1e-3)
+        cpu = {} if args.no_cpu or ws > 1 else cpu_baselines(pub, R, S, key_idx, msg, expect)
         pmc = pmc_traffic(pb, pa, n)
         line = {
             "metric": "Ed25519 verifies/sec per node (1M-signature PBFT rounds)",
@@ -294,25 +470,31 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "u32 (GF(2^255-19) radix 2^25.5 limbs, 32x32->64 products)",
-            "data": "synthetic: 256 replica keys, 85-B signed Prepare/Commit envelopes, GPU-signed (RFC 8032)",
-            "config": {"workload": "config#4 round per GPU: n=256 replicas x 2048 seqs x {Prepare,Commit}",
-                       "sigs_per_gpu": n, "sigs_per_step": n * ws, "msg_len": ENVELOPE, "settle_s": args.settle_s,
+            "data": "synthetic: 256 replica keys, 85-B signed Prepare/Commit envelopes, GPU-signed (RFC 8032), "
+                    "0.1% of signatures corrupted (bitmap checked)",
+            "config": {"workload": "config#4: one round of n=256 replicas x 2048 seqs x {Prepare,Commit} = 2^20 "
+                                   "signatures, sharded by index over the GPUs",
+                       "sigs_per_step": n_total, "sigs_per_gpu": n, "msg_len": ENVELOPE, "settle_s": args.settle_s,
                        "parallelism": f"shard-by-index x{ws}" + (" + RCCL all-gather of bitmaps" if ws > 1 else "")},
             "roofline": {"bound": "valu", "achieved": products / 1e12, "peak": VALU_MAD_PEAK_PER_S / 1e12,
                          "unit": "T products/s (v_mad_u64_u32)", "frac": products / VALU_MAD_PEAK_PER_S,
                          "traffic": pmc.get("traffic_bytes_per_launch"),
                          "traffic_source": pmc.get("source"),
                          "valu_busy_pct": pmc.get("valu_busy_pct"),
-                         "gather_bytes_algorithmic": (gather_bytes_per_verify(pb, pa) + INPUT_BYTES) * n, "kernel": f"comb_kernel<85, plan PA={pa}> (PB={pb}) + finish_kernel (one verify launch pair)", "kernel_avg_ms": kern_avg,
-                         "products_per_verify": PRODUCTS_PER_VERIFY},
-            "p50_ms_4k_round": float(np.median(lat)) if lat else None,
-            "p99_ms_4k_round": float(np.percentile(lat, 99)) if lat else None,
-            "stream_4k": stream,
-            "cpu_baseline": cpu,
+                         "valu_insts_per_sig": pmc.get("valu_insts_per_sig"),
+                         "gather_bytes_algorithmic": (gather_bytes_per_verify(pb, pa) + INPUT_BYTES) * n,
+                         "kernel": f"verify launch over this rank's shard: comb_kernel<85, plan PA={pa}> (PB={pb}) "
+                                   f"+ finish", "kernel_avg_ms": kern_avg,
+                         "products_per_verify": products_per_verify(pb, pa)},
+            "weak_scaling": weak,
+            "cpu_baseline": cpu.get("port"),
+            "cpu_baseline_openssl": cpu.get("openssl"),
+            "vs_cpu_openssl": value / cpu["openssl"]["value"] if "openssl" in cpu else None,
         }
+        line.update(extras)
         print(json.dumps(line), flush=True)
     v.close()
     if dist is not None:

@@ -804,6 +804,9 @@ struct pbft_ctx {
   uint8_t* d_work = nullptr;
   size_t work_cap = 0;
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
+  // host-buffer pipeline: H2D of chunk c+1 (copy stream) overlaps the kernels of chunk c
+  hipStream_t cstream = nullptr;
+  hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
   bool in_flight = false;
   uint64_t* async_out = nullptr;
   uint64_t* h_bitmap = nullptr;  // pinned
@@ -935,22 +938,62 @@ static bool check_batch_args(const void* R, const void* S, const void* K, const 
   return true;
 }
 
-// Copy a host batch into the staging buffer and launch.  Returns device bitmap.
+// Staging layout of n signatures: R | S | key_idx | msg (+ slack for unaligned message reads).
+struct stage_layout {
+  size_t offS, offK, offM, bytes;
+  stage_layout(uint64_t n, uint32_t msg_stride) {
+    offS = 32 * n;
+    offK = 64 * n;
+    offM = (offK + 2 * n + 255) & ~(size_t)255;
+    bytes = (offM + (size_t)msg_stride * n + 64 + 255) & ~(size_t)255;
+  }
+};
+
+// Host batches above this many signatures are copied and verified in chunks on two
+// staging halves: the H2D copy of chunk c+1 (context copy stream) overlaps the
+// kernels of chunk c (context stream).  A multiple of 64: chunks own whole
+// bitmap words.  2^18 keeps every chunk in the one-lane-per-signature mode.
+static constexpr uint64_t PIPE_CHUNK = 1ull << 18;
+
+// Copy a host batch into the staging buffer and launch.  Result: the device bitmap.
 static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint8_t* M,
                             uint32_t msg_len, uint32_t msg_stride, uint64_t N) {
   const uint64_t words = (N + 63) / 64;
-  const size_t offS = 32 * N, offK = 64 * N;
-  const size_t offM = (offK + 2 * N + 255) & ~(size_t)255;
-  const size_t mbytes = (size_t)msg_stride * N;
-  const size_t total = offM + mbytes + 64;  // + slack for unaligned message reads
-  int rc = ensure_stage(c, total, words);
+  if (N <= PIPE_CHUNK) {
+    const stage_layout L(N, msg_stride);
+    int rc = ensure_stage(c, L.bytes, words);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(c->d_stage, R, 32 * N, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_stage + L.offS, S, 32 * N, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_stage + L.offK, K, 2 * N, hipMemcpyHostToDevice, c->stream));
+    if ((size_t)msg_stride * N)
+      HIP_TRY(hipMemcpyAsync(c->d_stage + L.offM, M, (size_t)msg_stride * N, hipMemcpyHostToDevice, c->stream));
+    return launch_verify(c, c->d_stage, c->d_stage + L.offS, (const uint16_t*)(c->d_stage + L.offK),
+                         c->d_stage + L.offM, msg_len, msg_stride, N, c->d_bitmap, c->stream);
+  }
+  const stage_layout L(PIPE_CHUNK, msg_stride);
+  int rc = ensure_stage(c, 2 * L.bytes, words);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c->d_stage, R, 32 * N, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->d_stage + offS, S, 32 * N, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->d_stage + offK, K, 2 * N, hipMemcpyHostToDevice, c->stream));
-  if (mbytes) HIP_TRY(hipMemcpyAsync(c->d_stage + offM, M, mbytes, hipMemcpyHostToDevice, c->stream));
-  return launch_verify(c, c->d_stage, c->d_stage + offS, (const uint16_t*)(c->d_stage + offK), c->d_stage + offM,
-                       msg_len, msg_stride, N, c->d_bitmap, c->stream);
+  uint64_t chunk = 0;
+  for (uint64_t lo = 0; lo < N; lo += PIPE_CHUNK, ++chunk) {
+    const uint64_t n = N - lo < PIPE_CHUNK ? N - lo : PIPE_CHUNK;
+    const int b = (int)(chunk & 1);
+    uint8_t* base = c->d_stage + (size_t)b * L.bytes;
+    if (chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));  // kernels of chunk-2 done
+    HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream));
+    if ((size_t)msg_stride * n)
+      HIP_TRY(hipMemcpyAsync(base + L.offM, M + (size_t)msg_stride * lo, (size_t)msg_stride * n,
+                             hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
+    rc = launch_verify(c, base, base + L.offS, (const uint16_t*)(base + L.offK), base + L.offM, msg_len, msg_stride,
+                       n, c->d_bitmap + lo / 64, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
+  }
+  return PBFT_OK;
 }
 
 // The base-point comb table is a constant of the curve: one copy per device,
@@ -1027,9 +1070,16 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
+  HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  for (int b = 0; b < 2; ++b) {
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[b], hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_consumed[b], hipEventDisableTiming));
+  }
   int rc = acquire_base_table(device, c->stream, &c->d_tabB);
   if (rc) {
     (void)hipEventDestroy(c->ev0); (void)hipEventDestroy(c->ev1); (void)hipEventDestroy(c->ev_done);
+    for (int b = 0; b < 2; ++b) { (void)hipEventDestroy(c->ev_copied[b]); (void)hipEventDestroy(c->ev_consumed[b]); }
+    (void)hipStreamDestroy(c->cstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return rc;
@@ -1050,6 +1100,11 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
+  for (int b = 0; b < 2; ++b) {
+    if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
+    if (c->ev_consumed[b]) (void)hipEventDestroy(c->ev_consumed[b]);
+  }
+  if (c->cstream) { (void)hipStreamSynchronize(c->cstream); (void)hipStreamDestroy(c->cstream); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return PBFT_OK;

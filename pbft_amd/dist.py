@@ -55,3 +55,11 @@ def assemble(gathered_words, n_total: int, world: int):
         nw = (hi - lo + 63) // 64
         chunks.append(gathered_words[r * per: r * per + nw])
     return torch.cat(chunks)[:words]
+
+
+def round_bitmap(local, n_total: int, world: int, gathered=None):
+    """The round's bitmap words from every rank's shard words (bench.py's exchange step and its check):
+    one all-gather of the equal-length padded shards, then the padding words dropped."""
+    if world == 1:
+        return local[: (n_total + 63) // 64]
+    return assemble(allgather_bitmap(local, world, gathered), n_total, world)

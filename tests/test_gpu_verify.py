@@ -390,3 +390,55 @@ def test_device_launch_captured_in_hip_graph(gv, golden):
         torch.cuda.synchronize()
         got = bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n)
         assert (got == (exp if rep < 2 else np.zeros(n, bool))).all(), rep
+
+
+def test_config2_pipelined_window(gv, coracle):
+    """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 Prepare + Commit signatures in one
+    window batch (latency-mode kernel), 1 % adversarial, bit-exact with the C oracle; the same batch through the
+    one-lane-per-signature kernels (PBFT_SPLIT_BELOW = 0) gives the same bits."""
+    from pbft_amd import GpuBatchVerifier
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 4, 1024, tag=2)
+    assert len(R) == 8192
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(2)
+    R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
+    got, _ = verify(gv, R2, S2, K2, M2, 85)
+    exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
+    assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
+    assert not got[idx].any() and got.sum() == len(R) - len(idx)
+    os.environ["PBFT_SPLIT_BELOW"] = "0"
+    try:
+        v1 = GpuBatchVerifier(0)
+    finally:
+        del os.environ["PBFT_SPLIT_BELOW"]
+    try:
+        v1.set_keys(pub)
+        got1, _ = verify(v1, R2, S2, K2, M2, 85)
+        assert (got1 == exp).all()
+    finally:
+        v1.close()
+
+
+@pytest.mark.parametrize("budget_mb,pa", [("1500", 16), ("40", 32)])
+def test_smaller_key_plans(gv, coracle, golden, budget_mb, pa):
+    """The 16- and 32-position key plans (PLA_MID / PLA_SMALL), chosen by pbft_verify_set_keys when the key set does
+    not fit PBFT_KEY_TABLE_BUDGET_MB: golden corpus (latency kernel) and a config-#3 round (comb kernel) bit-exact."""
+    from pbft_amd import GpuBatchVerifier
+    v = GpuBatchVerifier(0)
+    os.environ["PBFT_KEY_TABLE_BUDGET_MB"] = budget_mb
+    try:
+        for ml, b in golden_batches(golden):
+            assert (v.set_keys(b["keys"]) == b["key_ok"].astype(bool)).all()
+            assert v.positions()[1] == pa
+            got, _ = verify(v, b["R"], b["S"], b["key_idx"], b["msg"], ml)
+            assert (got == b["expected"].astype(bool)).all(), (pa, ml)
+        seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=9)   # 2^16 signatures, 16 replicas
+        assert v.set_keys(pub).all() and v.positions()[1] == pa
+        rng = np.random.default_rng(9)
+        R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
+        got, _ = verify(v, R2, S2, K2, M2, 85)
+        exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
+        assert (got == exp).all(), (pa, np.nonzero(got != exp)[0][:10])
+    finally:
+        del os.environ["PBFT_KEY_TABLE_BUDGET_MB"]
+        v.close()

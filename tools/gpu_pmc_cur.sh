@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; D=gpurun_out/pmc_cur; rm -rf $D; mkdir -p $D; export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $D/counters_list.txt 2>&1 || true
-B="python3 bench.py --steps 5 --warmup 1 --no-cpu --latency-iters 0"
+B="python3 bench.py --steps 5 --warmup 1 --no-cpu --no-extras"
 i=0
 for grp in "SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
            "SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" \
