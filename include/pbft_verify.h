@@ -124,6 +124,18 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
                     const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint8_t *R,
                     uint8_t *S, uint8_t *pub);
 
+/* Tuning options of one context (defaults are chosen by batch size / free HBM):
+ *   PBFT_OPT_SPLIT_BELOW          batches below this many signatures use the 4-lanes-per-signature latency
+ *                                 kernel (default 65536; env PBFT_SPLIT_BELOW)
+ *   PBFT_OPT_FINISH_WIDTH         signatures per lane of the batch-inversion finish kernel: 1, 4 or 16
+ *                                 (0 = by batch size)
+ *   PBFT_OPT_KEY_TABLE_BUDGET_MB  HBM budget for the replica key tables at the next pbft_verify_set_keys
+ *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 96 GiB); selects the key comb plan */
+#define PBFT_OPT_SPLIT_BELOW 1
+#define PBFT_OPT_FINISH_WIDTH 2
+#define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
+int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
+
 /* Diagnostics */
 const char *pbft_last_error(void);
 const char *pbft_build_info(void); /* kernel windows, arch, version */

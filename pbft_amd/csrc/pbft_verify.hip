@@ -33,11 +33,12 @@ using namespace pbft;
 // signed-digit scalar < 2^253, i.e. the fewest positions (= comb steps) for the
 // HBM they take.  Base point: 10 positions (4 x 26 + 6 x 25 bits), 235M entries
 // x 128 B = 30 GB, one copy per device shared by all contexts.  Replica keys:
-// 14 positions (2 x 19 + 12 x 18 bits, 268 MB per key) while the key set fits
-// PBFT_KEY_TABLE_BUDGET_MB (default 96 GiB of the 288 GB HBM: <= 360 keys),
-// else 16 positions (14 x 16 + 2 x 15, 63 MB), else 32 (30 x 8 + 2 x 7,
-// 0.5 MB).  24 steps per signature at n <= 360.  DESIGN.md §3-4; measured in
-// profiles/r01_ab_log.md.
+// the widest plan whose tables fit the key-table budget (default 70 % of the
+// free HBM, ~180 GB on MI355X; PBFT_OPT_KEY_TABLE_BUDGET_MB): 13 positions
+// (7 x 20 + 6 x 19 bits, 671 MB per key: n <= 268), 14 (2 x 19 + 12 x 18,
+// 268 MB), 16 (14 x 16 + 2 x 15, 63 MB), else 32 (30 x 8 + 2 x 7, 0.5 MB).
+// 23 steps per signature at n = 256.  DESIGN.md §3-4; measured in
+// profiles/r01_ab_log.md, profiles/r02_ab_log.md.
 #ifndef PBFT_PLAN_B
 #define PBFT_PLAN_B 10, 25, 4
 #endif
@@ -45,10 +46,12 @@ using namespace pbft;
 #define PBFT_PLAN_A 14, 18, 2
 #endif
 using PLB = plan<PBFT_PLAN_B>;
+using PLA_HUGE = plan<13, 19, 7>;  // 7 x 20 + 6 x 19 bits: 671 MB per key (n = 256: 172 GB)
 using PLA_BIG = plan<PBFT_PLAN_A>;
 using PLA_MID = plan<16, 15, 14>;
 using PLA_SMALL = plan<32, 7, 30>;
-static_assert(PLA_BIG::P < PLA_MID::P && PLA_MID::P < PLA_SMALL::P, "key plans are told apart by P");
+static_assert(PLA_HUGE::P < PLA_BIG::P && PLA_BIG::P < PLA_MID::P && PLA_MID::P < PLA_SMALL::P,
+              "key plans are told apart by P");
 
 // ------------------------------------------------------------------ errors
 static thread_local std::string g_last_error;
@@ -153,7 +156,7 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
     if (t + 1 < cnt) { ge nx; ge_add(nx, acc, Q); acc = nx; }
   }
   fe inv;
-  fe_invert(inv, pre[cnt - 1]);
+  fe_invert_gcd(inv, pre[cnt - 1]);
   fe k2d;
   fe_const_2d(k2d);
   for (int t = (int)cnt - 1; t >= 0; --t) {
@@ -442,7 +445,7 @@ static constexpr int LAT_COMB_WAVES = 3;
 static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // 48 signatures per block
 static constexpr int LAT_BLOCK = (LAT_COMB_WAVES + 1) * 64;  // + 1 decompression wave
 #ifndef PBFT_SPLIT_BELOW
-#define PBFT_SPLIT_BELOW 65536
+#define PBFT_SPLIT_BELOW 12288  // measured crossover: 8,192 sigs 0.105 ms here vs 0.133 ms one-lane; 16,384: 0.195 vs 0.133
 #endif
 static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_latency_kernel
 static constexpr uint32_t LAT_LDS = LAT_COMB_WAVES * COMB_LDS_PER_WAVE + 21 * 64 * 4;  // entry buffers + x_R, y_R, ok
@@ -676,7 +679,11 @@ __global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const u
     else fe_mul(pre[m], pre[m - 1], z);
   });
   fe inv;
-  fe_invert<true>(inv, pre[FM - 1]);  // the serial chain of a 1-wave-per-SIMD kernel: latency-oriented carries
+#if PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
+  fe_invert<true>(inv, pre[FM - 1]);
+#else
+  fe_invert_gcd(inv, pre[FM - 1]);  // divsteps: ~19k instructions instead of ~44k on the serial chain
+#endif
   fin_unroll<FM>::down([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
@@ -768,7 +775,7 @@ struct keyset {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n = 0;
-  int pa = 0;  // positions of the key plan (identifies PLA_BIG / PLA_MID / PLA_SMALL)
+  int pa = 0;  // positions of the key plan (identifies PLA_HUGE / PLA_BIG / PLA_MID / PLA_SMALL)
 };
 static void keyset_release(keyset* k) {
   if (k && --k->refs == 0) {
@@ -787,8 +794,10 @@ struct pbft_ctx {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n_keys = 0;
-  int pa = 0;  // comb positions of the installed key tables' plan (PLA_BIG, PLA_MID or PLA_SMALL)
+  int pa = 0;  // comb positions of the installed key tables' plan (PLA_HUGE, PLA_BIG, PLA_MID or PLA_SMALL)
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
+  int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
+  uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
@@ -889,20 +898,24 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     const uint64_t pieces = 4 * ((N + 63) / 64);
     const uint64_t sblocks = (pieces + LAT_COMB_WAVES - 1) / LAT_COMB_WAVES, Lpad = sblocks * LAT_COMB_WAVES * 64;
     if (msg_len == PBFT_ENVELOPE_LEN) {
-      if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_BIG);
+      if (c->pa == PLA_HUGE::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_HUGE);
+      else if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_BIG);
       else if (c->pa == PLA_MID::P) PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_MID);
       else PBFT_LAUNCH_SPLIT(PBFT_ENVELOPE_LEN, PLA_SMALL);
     } else {
-      if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(-1, PLA_BIG);
+      if (c->pa == PLA_HUGE::P) PBFT_LAUNCH_SPLIT(-1, PLA_HUGE);
+      else if (c->pa == PLA_BIG::P) PBFT_LAUNCH_SPLIT(-1, PLA_BIG);
       else if (c->pa == PLA_MID::P) PBFT_LAUNCH_SPLIT(-1, PLA_MID);
       else PBFT_LAUNCH_SPLIT(-1, PLA_SMALL);
     }
   } else if (msg_len == PBFT_ENVELOPE_LEN) {
-    if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_BIG);
+    if (c->pa == PLA_HUGE::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_HUGE);
+    else if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_BIG);
     else if (c->pa == PLA_MID::P) PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_MID);
     else PBFT_LAUNCH_COMB(PBFT_ENVELOPE_LEN, PLA_SMALL);
   } else {
-    if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(-1, PLA_BIG);
+    if (c->pa == PLA_HUGE::P) PBFT_LAUNCH_COMB(-1, PLA_HUGE);
+    else if (c->pa == PLA_BIG::P) PBFT_LAUNCH_COMB(-1, PLA_BIG);
     else if (c->pa == PLA_MID::P) PBFT_LAUNCH_COMB(-1, PLA_MID);
     else PBFT_LAUNCH_COMB(-1, PLA_SMALL);
   }
@@ -910,13 +923,16 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
 #undef PBFT_LAUNCH_SPLIT
   HIP_TRY(hipGetLastError());
   if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
-    // signatures per finish lane: as many as keep >= one wave per SIMD (1,024 waves) busy
-    const int fm = N >= (uint64_t)64 * 1024 * FIN_M ? FIN_M : N >= (uint64_t)64 * 1024 * 4 ? 4 : 1;
+    // signatures per finish lane (one divsteps inversion per lane): measured on MI355X
+    // (tools/size_probe.py, profiles/r02_size_probe.md) -- 1 up to 2^16, 4 up to 2^18, then 16
+    int fm = N >= ((uint64_t)1 << 19) ? FIN_M : N > ((uint64_t)1 << 16) ? 4 : 1;
+    if (c->fin_m) fm = c->fin_m;
 #define PBFT_LAUNCH_FIN(M_)                                                                                 \
   hipLaunchKernelGGL(finish_kernel<M_>, dim3((unsigned)((((N + 64 * M_ - 1) / (64 * M_)) * 64 + BLOCK - 1) / \
                                                         BLOCK)),                                           \
                      dim3(BLOCK), 0, st, dR, rs_stride, xyz, flags, N, dB)
     if (fm == FIN_M) PBFT_LAUNCH_FIN(FIN_M);
+    else if (fm == 8) PBFT_LAUNCH_FIN(8);
     else if (fm == 4) PBFT_LAUNCH_FIN(4);
     else PBFT_LAUNCH_FIN(1);
 #undef PBFT_LAUNCH_FIN
@@ -1043,9 +1059,9 @@ const char* pbft_last_error(void) { return g_last_error.c_str(); }
 const char* pbft_build_info(void) {
   static char buf[256];
   snprintf(buf, sizeof buf,
-           "pbft_verify gfx950 PB=%d PA=%d|%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB|%zuB", PLB::P,
-           PLA_BIG::P, PLA_MID::P, PLA_SMALL::P, BLOCK, PLB::TABLE_WORDS * 4, PLA_BIG::TABLE_WORDS * 4,
-           PLA_MID::TABLE_WORDS * 4, PLA_SMALL::TABLE_WORDS * 4);
+           "pbft_verify gfx950 PB=%d PA=%d|%d|%d|%d block=%d entry=128B tabB=%zuB tabA/key=%zuB|%zuB|%zuB|%zuB",
+           PLB::P, PLA_HUGE::P, PLA_BIG::P, PLA_MID::P, PLA_SMALL::P, BLOCK, PLB::TABLE_WORDS * 4,
+           PLA_HUGE::TABLE_WORDS * 4, PLA_BIG::TABLE_WORDS * 4, PLA_MID::TABLE_WORDS * 4, PLA_SMALL::TABLE_WORDS * 4);
   return buf;
 }
 
@@ -1120,10 +1136,12 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   // The widest key window whose tables fit the budget (PBFT_KEY_TABLE_BUDGET_MB, default 96 GiB of the
   // 288 GB HBM) and the free memory: 18-bit (252 MB/key, <= 390 keys by default), 16-bit (67 MB/key), else
   // 8-bit (0.5 MB/key).  Entry indices are 32-bit (n * P * E < 2^32).
-  size_t budget_mb = 96 * 1024;
-  if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+  // default budget: 70 % of the HBM still free (after the 30-GB base-point table: ~180 GB on a 288-GB MI355X)
+  size_t budget_mb = free_b / 1048576 * 7 / 10;
+  if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
+  if (c->key_budget_mb) budget_mb = c->key_budget_mb;
   auto fits = [&](size_t table_words, uint64_t entries_per_key) {
     const size_t bytes = table_words * 4 * (size_t)n;
     return (uint64_t)n * entries_per_key < (1ull << 32) && bytes <= budget_mb * (size_t)1048576 &&
@@ -1131,7 +1149,10 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   };
   int pa = PLA_SMALL::P;
   size_t tab_words = PLA_SMALL::TABLE_WORDS;
-  if (fits(PLA_BIG::TABLE_WORDS, PLA_BIG::ENTRIES)) {
+  if (fits(PLA_HUGE::TABLE_WORDS, PLA_HUGE::ENTRIES)) {
+    pa = PLA_HUGE::P;
+    tab_words = PLA_HUGE::TABLE_WORDS;
+  } else if (fits(PLA_BIG::TABLE_WORDS, PLA_BIG::ENTRIES)) {
     pa = PLA_BIG::P;
     tab_words = PLA_BIG::TABLE_WORDS;
   } else if (fits(PLA_MID::TABLE_WORDS, PLA_MID::ENTRIES)) {
@@ -1151,7 +1172,8 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (hipMemcpyAsync(k->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key upload");
   if (!rc)
-    rc = pa == PLA_BIG::P   ? build_tables<PLA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+    rc = pa == PLA_HUGE::P  ? build_tables<PLA_HUGE>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
+         : pa == PLA_BIG::P ? build_tables<PLA_BIG>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
          : pa == PLA_MID::P ? build_tables<PLA_MID>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream)
                             : build_tables<PLA_SMALL>(k->d_keys, n, 1, k->d_tabA, k->d_key_ok, c->stream);
   if (!rc && key_ok && hipMemcpyAsync(key_ok, k->d_key_ok, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
@@ -1414,6 +1436,20 @@ int pbft_verify_reserve(pbft_ctx* c, uint64_t max_n) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
   return ensure_work(c, max_n);
+}
+
+int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  switch (option) {
+    case PBFT_OPT_SPLIT_BELOW: c->split_below = value; return PBFT_OK;
+    case PBFT_OPT_FINISH_WIDTH:
+      if (value != 0 && value != 1 && value != 4 && value != 8 && value != FIN_M)
+        return set_err(PBFT_EINVAL, "finish width");
+      c->fin_m = (int)value;
+      return PBFT_OK;
+    case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
+  }
+  return set_err(PBFT_EINVAL, "unknown option");
 }
 
 int pbft_verify_ctx_info(pbft_ctx* c, uint32_t* pb, uint32_t* pa, uint32_t* n_keys) {

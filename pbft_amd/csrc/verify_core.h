@@ -19,6 +19,7 @@
 //    small-order test on R reduces to a test on y(R') once they are equal.
 #pragma once
 #include "ge25519.h"
+#include "inv25519.h"
 #include "sc25519.h"
 #include "sha512.h"
 
@@ -288,7 +289,7 @@ FE_FN bool verify_lane(const uint32_t r_enc[8], const uint32_t s[8], const uint3
   });
 
   fe zi, x, y;
-  fe_invert(zi, P.Z);
+  fe_invert_gcd(zi, P.Z);
   fe_mul(x, P.X, zi);
   fe_mul(y, P.Y, zi);
   uint32_t xw[8], yw[8], ry[8];
@@ -319,7 +320,7 @@ FE_FN void comb_mul_base(ge& P, const uint32_t k[8], const uint32_t* tabB) {
 
 FE_FN void ge_compress_words(uint32_t enc[8], const ge& P) {
   fe zi, x, y;
-  fe_invert(zi, P.Z);
+  fe_invert_gcd(zi, P.Z);
   fe_mul(x, P.X, zi);
   fe_mul(y, P.Y, zi);
   uint32_t xw[8];

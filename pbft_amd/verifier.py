@@ -152,6 +152,12 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_records(self._ctx, _ptr(rec), n, _ptr(out)))
         return out
 
+    OPT_SPLIT_BELOW, OPT_FINISH_WIDTH, OPT_KEY_TABLE_BUDGET_MB = 1, 2, 3
+
+    def set_option(self, option: int, value: int) -> None:
+        """pbft_verify_set_option: latency-mode threshold, finish width, key-table budget (include/pbft_verify.h)."""
+        check(self._lib.pbft_verify_set_option(self._ctx, option, value))
+
     def positions(self) -> tuple[int, int]:
         """(PB, PA): comb positions (= steps) of the base-point plan and of the installed key set's plan."""
         pb, pa, nk = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()

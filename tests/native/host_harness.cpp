@@ -3,6 +3,7 @@
 // check fields, hashing, scalar reduction, comb tables and the full per-lane
 // verify against the oracle in a container without a GPU.  Never loaded by the
 // product path (pbft_amd/ loads only libpbft_verify.so, which needs a GPU).
+#include "../../pbft_amd/csrc/inv25519.h"
 #include "../../pbft_amd/csrc/verify_core.h"
 #include <sys/mman.h>
 #include <unistd.h>
@@ -78,6 +79,8 @@ void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
     case 11: { fe t; fe_add(t, fa, fb); fe_mulT<true>(fo, t, t); break; }
     case 12: { fe t; fe_sub(t, fa, fb); fe_mulT<true>(fo, t, fb); break; }
     case 13: { fe t, u; fe_sqT<true>(t, fa); fe_sub(u, fb, t); fe_mulT<true>(fo, u, t); break; }  // par output as subtrahend
+    case 14: fe_invert_gcd(fo, fa); break;                            // safegcd (divsteps) inversion
+    case 15: { fe t; fe_add(t, fa, fb); fe_invert_gcd(fo, t); break; } // of an uncarried sum
     default: fo = fa;
   }
   fe_to_words(wo, fo);

@@ -326,12 +326,9 @@ def test_latency_mode_split_kernel_matches_single_lane(golden):
     golden batch (every adversarial class, every message length)."""
     from pbft_amd import GpuBatchVerifier
     results = {}
-    for mode, thr in (("split", "1000000000"), ("single", "0")):
-        os.environ["PBFT_SPLIT_BELOW"] = thr
-        try:
-            v = GpuBatchVerifier(0)
-        finally:
-            del os.environ["PBFT_SPLIT_BELOW"]
+    for mode, thr in (("split", 1_000_000_000), ("single", 0)):
+        v = GpuBatchVerifier(0)
+        v.set_option(v.OPT_SPLIT_BELOW, thr)
         try:
             for ml, b in golden_batches(golden):
                 v.set_keys(b["keys"])
@@ -395,7 +392,7 @@ def test_device_launch_captured_in_hip_graph(gv, golden):
 def test_config2_pipelined_window(gv, coracle):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 Prepare + Commit signatures in one
     window batch (latency-mode kernel), 1 % adversarial, bit-exact with the C oracle; the same batch through the
-    one-lane-per-signature kernels (PBFT_SPLIT_BELOW = 0) gives the same bits."""
+    one-lane-per-signature kernels (PBFT_OPT_SPLIT_BELOW = 0) gives the same bits, with every finish width."""
     from pbft_amd import GpuBatchVerifier
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 4, 1024, tag=2)
     assert len(R) == 8192
@@ -406,26 +403,26 @@ def test_config2_pipelined_window(gv, coracle):
     exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
     assert not got[idx].any() and got.sum() == len(R) - len(idx)
-    os.environ["PBFT_SPLIT_BELOW"] = "0"
-    try:
-        v1 = GpuBatchVerifier(0)
-    finally:
-        del os.environ["PBFT_SPLIT_BELOW"]
+    v1 = gv.clone()
+    v1.set_option(v1.OPT_SPLIT_BELOW, 0)
     try:
         v1.set_keys(pub)
-        got1, _ = verify(v1, R2, S2, K2, M2, 85)
-        assert (got1 == exp).all()
+        for fm in (1, 4, 16):
+            v1.set_option(v1.OPT_FINISH_WIDTH, fm)
+            got1, _ = verify(v1, R2, S2, K2, M2, 85)
+            assert (got1 == exp).all(), fm
+        with pytest.raises(Exception):
+            v1.set_option(v1.OPT_FINISH_WIDTH, 3)
     finally:
         v1.close()
 
 
-@pytest.mark.parametrize("budget_mb,pa", [("1500", 16), ("40", 32)])
+@pytest.mark.parametrize("budget_mb,pa", [("5000", 14), ("1500", 16), ("40", 32)])
 def test_smaller_key_plans(gv, coracle, golden, budget_mb, pa):
-    """The 16- and 32-position key plans (PLA_MID / PLA_SMALL), chosen by pbft_verify_set_keys when the key set does
+    """The 14-, 16- and 32-position key plans (PLA_BIG / PLA_MID / PLA_SMALL), chosen by pbft_verify_set_keys when the key set does
     not fit PBFT_KEY_TABLE_BUDGET_MB: golden corpus (latency kernel) and a config-#3 round (comb kernel) bit-exact."""
-    from pbft_amd import GpuBatchVerifier
-    v = GpuBatchVerifier(0)
-    os.environ["PBFT_KEY_TABLE_BUDGET_MB"] = budget_mb
+    v = gv.clone()
+    v.set_option(v.OPT_KEY_TABLE_BUDGET_MB, int(budget_mb))
     try:
         for ml, b in golden_batches(golden):
             assert (v.set_keys(b["keys"]) == b["key_ok"].astype(bool)).all()
@@ -440,5 +437,4 @@ def test_smaller_key_plans(gv, coracle, golden, budget_mb, pa):
         exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
         assert (got == exp).all(), (pa, np.nonzero(got != exp)[0][:10])
     finally:
-        del os.environ["PBFT_KEY_TABLE_BUDGET_MB"]
         v.close()

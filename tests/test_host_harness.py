@@ -56,11 +56,27 @@ def test_field_ops(hh):
         assert _fe(hh, 11, a, b) == (a + b) ** 2 % P
         assert _fe(hh, 12, a, b) == (a - b) * b % P
         assert _fe(hh, 13, a, b) == (b - a * a) * (a * a) % P
+    for a in vals:
+        assert _fe(hh, 14, a, 0) == pow(a, P - 2, P), a                  # divsteps inversion
+    for i, a in enumerate(vals[:200]):
+        b = vals[(i * 5 + 1) % len(vals)]
+        assert _fe(hh, 15, a, b) == pow(a + b, P - 2, P)
     for a in vals[:60]:
         assert _fe(hh, 2, a, 0) == pow(a, P - 2, P)
         assert _fe(hh, 3, a, 0) == pow(a, (P - 5) // 8, P)
         assert _fe(hh, 9, a, 0) == pow(a, P - 2, P)
         assert _fe(hh, 10, a, 0) == pow(a, (P - 5) // 8, P)
+
+
+def test_divsteps_inversion_extremes(hh):
+    """safegcd inversion (pbft_amd/csrc/inv25519.h) on inputs that stress the divstep count and the limb ranges:
+    powers of two, p - 2^k, all-ones patterns, values just below p and unreduced encodings >= p."""
+    vals = [2**k for k in range(255)] + [P - 2**k for k in range(1, 255)] + [(2**k - 1) for k in range(1, 256)]
+    vals += [P - k for k in range(1, 40)] + [P + k for k in range(0, 19)] + [2**255 - 1 - k for k in range(20)]
+    rnd = random.Random(99)
+    vals += [rnd.getrandbits(rnd.randrange(1, 256)) for _ in range(2000)]
+    for a in vals:
+        assert _fe(hh, 14, a % 2**255, 0) == pow(a % 2**255, P - 2, P), a
 
 
 @pytest.mark.parametrize("ln", [0, 1, 47, 48, 63, 64, 85, 111, 112, 175, 176, 239, 240, 300, 1023])

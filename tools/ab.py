@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--replicas", type=int, default=256)
     ap.add_argument("--seqs", type=int, default=2048)
     ap.add_argument("--per-launch-events", action="store_true", help="also record a torch event pair per launch")
+    ap.add_argument("--sizes", default="", help="comma list of batch sizes (default: the whole round)")
     a = ap.parse_args()
     import torch
     import bench
@@ -57,8 +58,11 @@ def main():
         ok = np.zeros(len(pub), np.uint8)
         assert lib.pbft_verify_set_keys(c, pub.ctypes.data, len(pub), ok.ctypes.data) == 0
         ctxs.append((p, lib, c))
-    res = {p: [] for p in a.libs}
-    for r in range(a.rounds):
+    sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else [n]
+    full = n
+    for n in sizes:
+      res = {p: [] for p in a.libs}
+      for r in range(a.rounds):
         for p, lib, c in ctxs:
             dB.zero_()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -73,10 +77,10 @@ def main():
             res[p].append(e0.elapsed_time(e1) / a.iters)
             if "abl" not in os.path.basename(p):
                 assert bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n).all(), p
-    for p, lib, c in ctxs:
+      for p, lib, c in ctxs:
         t = np.array(res[p])
-        print(f"{os.path.basename(p):32s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
-              f"-> {n / np.median(t) * 1e3 / 1e6:.1f} M verifies/s   [{lib.pbft_build_info().decode()}]")
+        print(f"N={n:8d} {os.path.basename(p):32s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
+              f"-> {n / np.median(t) * 1e3 / 1e6:.1f} M verifies/s   [{lib.pbft_build_info().decode()}]", flush=True)
 
 
 if __name__ == "__main__":
