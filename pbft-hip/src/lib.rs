@@ -1,0 +1,428 @@
+//! pbft-hip: the MI355X batch verifier that gates PBFT's Prepare / Commit quorums
+//! (BASELINE.json north_star), as the crate ameya-deshmukh/pbft would depend on.
+//!
+//! * [`BatchVerifier`]: the trait of SURVEY.md §8(b) -- non-blocking `submit` + `poll`
+//!   (fits `NetworkBehaviour::poll`, /root/reference/src/behavior.rs:416-426) and a
+//!   blocking `verify`.  An invalid signature is a 0 bit, never an error (the reference
+//!   panics through `.unwrap()`, src/behavior.rs:345, :371).
+//! * [`GpuVerifier`]: the HIP implementation (libpbft_verify.so, gfx950).
+//! * [`CpuVerifier`] (feature `cpu`): ed25519-dalek 1.0.1 `PublicKey::verify_strict` per
+//!   signature -- the reference's own crypto (libp2p-core 0.31.1 -> ed25519-dalek 1.0.1,
+//!   Cargo.lock:668-679); bit-exact with the GPU on every vector class (tests/golden).
+//! * [`Replica`]: the native round batcher + quorum state machine
+//!   (include/pbft_replica.h) that replaces `validate_prepare` / `validate_commit`
+//!   (src/behavior.rs:159-195) and keys votes by the authenticated peer
+//!   (src/behavior.rs:346, :380); any `BatchVerifier` can back it.
+//! * [`key_from_peer_id`]: libp2p PeerId -> Ed25519 key (src/main.rs:39-40).
+//!
+//! NOT COMPILED IN THIS REPOSITORY: the build image has no Rust toolchain.  Every C entry
+//! point used here is exercised through ctypes by tests/ (CPU) and tests/ -m gpu (MI355X).
+use std::ffi::CStr;
+use std::fmt;
+use std::os::raw::{c_int, c_void};
+use std::ptr;
+
+pub mod ffi;
+
+/// The 85-byte signed envelope: "PBFT" || kind || view LE || seq LE || digest[64].
+pub type Envelope = [u8; ffi::PBFT_ENVELOPE_BYTES];
+
+#[derive(Debug, Clone, PartialEq, Eq)]
+pub struct Error {
+    pub code: i32,
+    pub message: String,
+}
+
+impl fmt::Display for Error {
+    fn fmt(&self, f: &mut fmt::Formatter<'_>) -> fmt::Result {
+        write!(f, "pbft-hip error {}: {}", self.code, self.message)
+    }
+}
+impl std::error::Error for Error {}
+
+pub type Result<T> = std::result::Result<T, Error>;
+
+fn check(rc: c_int) -> Result<c_int> {
+    if rc >= 0 {
+        return Ok(rc);
+    }
+    let message = unsafe { CStr::from_ptr(ffi::pbft_last_error()) }.to_string_lossy().into_owned();
+    Err(Error { code: rc, message })
+}
+
+/// Encode the signed envelope (the bytes every Prepare / Commit / PrePrepare signature covers).
+pub fn envelope(kind: u8, view: u64, seq: u64, digest: &[u8; 64]) -> Envelope {
+    let mut out = [0u8; ffi::PBFT_ENVELOPE_BYTES];
+    unsafe { ffi::pbft_envelope(out.as_mut_ptr(), kind, view, seq, digest.as_ptr()) };
+    out
+}
+
+/// Struct-of-arrays batch of one or more (view, seq) round windows.
+#[derive(Clone, Default)]
+pub struct SigBatch {
+    pub r: Vec<[u8; 32]>,
+    pub s: Vec<[u8; 32]>,
+    pub key_idx: Vec<u16>,
+    pub msg: Vec<Envelope>,
+}
+
+impl SigBatch {
+    pub fn push(&mut self, key_idx: u16, envelope: Envelope, sig: &[u8; 64]) {
+        let mut r = [0u8; 32];
+        let mut s = [0u8; 32];
+        r.copy_from_slice(&sig[..32]);
+        s.copy_from_slice(&sig[32..]);
+        self.r.push(r);
+        self.s.push(s);
+        self.key_idx.push(key_idx);
+        self.msg.push(envelope);
+    }
+    pub fn len(&self) -> usize {
+        self.r.len()
+    }
+    pub fn is_empty(&self) -> bool {
+        self.r.is_empty()
+    }
+}
+
+/// Accept bits, LSB-first in u64 words; bits past the batch length are 0.
+#[derive(Clone, Debug, Default, PartialEq, Eq)]
+pub struct Bitmap(pub Vec<u64>);
+
+impl Bitmap {
+    pub fn zeros(n: usize) -> Self {
+        Bitmap(vec![0u64; (n + 63) / 64])
+    }
+    pub fn get(&self, i: usize) -> bool {
+        (self.0[i / 64] >> (i % 64)) & 1 == 1
+    }
+    pub fn set(&mut self, i: usize) {
+        self.0[i / 64] |= 1u64 << (i % 64);
+    }
+}
+
+/// Handle of one submitted batch.
+#[derive(Debug, PartialEq, Eq)]
+pub struct Ticket(pub u64);
+
+/// the verifier behind the round batcher.
+pub trait BatchVerifier {
+    /// Install the replica key set (libp2p identity keys of network.json's nodes);
+    /// returns key_ok per key (false: bad encoding or small order -> every signature under it is 0).
+    fn set_keys(&mut self, keys: &[[u8; 32]]) -> Result<Vec<bool>>;
+    /// Non-blocking: enqueue the batch.
+    fn submit(&mut self, batch: SigBatch) -> Result<Ticket>;
+    /// Ok(Some(bitmap)) once the batch is verified, Ok(None) while it runs.
+    fn poll(&mut self, ticket: &Ticket) -> Result<Option<Bitmap>>;
+    /// Blocking verify.
+    fn verify(&mut self, batch: SigBatch) -> Result<Bitmap> {
+        let t = self.submit(batch)?;
+        loop {
+            if let Some(bm) = self.poll(&t)? {
+                return Ok(bm);
+            }
+            std::thread::yield_now();
+        }
+    }
+}
+
+/// One HIP context (one MI355X).  Not `Sync`: one per thread; `try_clone` for more streams.
+pub struct GpuVerifier {
+    ctx: *mut ffi::pbft_ctx,
+    inflight: Option<(u64, SigBatch, Bitmap)>,
+    next: u64,
+}
+
+unsafe impl Send for GpuVerifier {}
+
+impl GpuVerifier {
+    pub fn new(device: i32) -> Result<Self> {
+        let mut ctx = ptr::null_mut();
+        check(unsafe { ffi::pbft_verify_ctx_create(device, &mut ctx) })?;
+        Ok(GpuVerifier { ctx, inflight: None, next: 0 })
+    }
+    /// Another context on the same GPU sharing this one's tables (own HIP stream).
+    pub fn try_clone(&self) -> Result<Self> {
+        let mut ctx = ptr::null_mut();
+        check(unsafe { ffi::pbft_verify_ctx_clone(self.ctx, &mut ctx) })?;
+        Ok(GpuVerifier { ctx, inflight: None, next: 0 })
+    }
+    pub fn set_option(&mut self, option: i32, value: u64) -> Result<()> {
+        check(unsafe { ffi::pbft_verify_set_option(self.ctx, option, value) }).map(|_| ())
+    }
+    /// Blake2b-512 request digests (src/message.rs:209-212), one per item.
+    pub fn blake2b512(&mut self, items: &[&[u8]]) -> Result<Vec<[u8; 64]>> {
+        let (data, offs, lens) = pack(items);
+        let mut out = vec![[0u8; 64]; items.len()];
+        check(unsafe {
+            ffi::pbft_digest_blake2b512(self.ctx, data.as_ptr(), offs.as_ptr(), lens.as_ptr(), items.len() as u64,
+                                        out.as_mut_ptr() as *mut u8)
+        })?;
+        Ok(out)
+    }
+    /// RFC 8032 signatures of this replica's own envelopes.
+    pub fn sign(&mut self, seed: &[u8; 32], msgs: &[Envelope]) -> Result<Vec<[u8; 64]>> {
+        let n = msgs.len();
+        let idx = vec![0u16; n];
+        let mut r = vec![[0u8; 32]; n];
+        let mut s = vec![[0u8; 32]; n];
+        check(unsafe {
+            ffi::pbft_sign_batch(self.ctx, seed.as_ptr(), 1, idx.as_ptr(), msgs.as_ptr() as *const u8,
+                                 ffi::PBFT_ENVELOPE_BYTES as u32, ffi::PBFT_ENVELOPE_BYTES as u32, n as u64,
+                                 r.as_mut_ptr() as *mut u8, s.as_mut_ptr() as *mut u8, ptr::null_mut())
+        })?;
+        Ok(r.iter().zip(s.iter()).map(|(r, s)| {
+            let mut sig = [0u8; 64];
+            sig[..32].copy_from_slice(r);
+            sig[32..].copy_from_slice(s);
+            sig
+        }).collect())
+    }
+    pub fn raw(&self) -> *mut ffi::pbft_ctx {
+        self.ctx
+    }
+}
+
+fn pack(items: &[&[u8]]) -> (Vec<u8>, Vec<u64>, Vec<u32>) {
+    let mut data = Vec::new();
+    let mut offs = Vec::with_capacity(items.len());
+    let mut lens = Vec::with_capacity(items.len());
+    for it in items {
+        offs.push(data.len() as u64);
+        lens.push(it.len() as u32);
+        data.extend_from_slice(it);
+    }
+    data.extend_from_slice(&[0u8; 16]); // the digest kernels read aligned dwords past each item
+    (data, offs, lens)
+}
+
+impl BatchVerifier for GpuVerifier {
+    fn set_keys(&mut self, keys: &[[u8; 32]]) -> Result<Vec<bool>> {
+        let mut ok = vec![0u8; keys.len()];
+        check(unsafe {
+            ffi::pbft_verify_set_keys(self.ctx, keys.as_ptr() as *const u8, keys.len() as u32, ok.as_mut_ptr())
+        })?;
+        Ok(ok.into_iter().map(|b| b == 1).collect())
+    }
+    fn submit(&mut self, batch: SigBatch) -> Result<Ticket> {
+        if self.inflight.is_some() {
+            return Err(Error { code: ffi::PBFT_EBUSY, message: "one batch in flight per context".into() });
+        }
+        let n = batch.len();
+        let mut out = Bitmap::zeros(n);
+        // the host buffers must outlive the async call: they move into `inflight`
+        check(unsafe {
+            ffi::pbft_verify_batch_async(self.ctx, batch.r.as_ptr() as *const u8, batch.s.as_ptr() as *const u8,
+                                         batch.key_idx.as_ptr(), batch.msg.as_ptr() as *const u8,
+                                         ffi::PBFT_ENVELOPE_BYTES as u32, ffi::PBFT_ENVELOPE_BYTES as u32,
+                                         n as u64, out.0.as_mut_ptr())
+        })?;
+        self.next += 1;
+        self.inflight = Some((self.next, batch, out));
+        Ok(Ticket(self.next))
+    }
+    fn poll(&mut self, ticket: &Ticket) -> Result<Option<Bitmap>> {
+        match &self.inflight {
+            Some((id, _, _)) if *id == ticket.0 => {}
+            _ => return Err(Error { code: ffi::PBFT_EINVAL, message: "unknown ticket".into() }),
+        }
+        if check(unsafe { ffi::pbft_verify_poll(self.ctx) })? == 1 {
+            let (_, _, bm) = self.inflight.take().unwrap();
+            return Ok(Some(bm));
+        }
+        Ok(None)
+    }
+}
+
+impl Drop for GpuVerifier {
+    fn drop(&mut self) {
+        unsafe {
+            if self.inflight.is_some() {
+                ffi::pbft_verify_wait(self.ctx);
+            }
+            ffi::pbft_verify_ctx_destroy(self.ctx);
+        }
+    }
+}
+
+/// The reference's CPU crypto path: ed25519-dalek 1.0.1 `verify_strict`, one signature at a time.
+#[cfg(feature = "cpu")]
+pub struct CpuVerifier {
+    keys: Vec<Option<ed25519_dalek::PublicKey>>,
+    done: Option<(u64, Bitmap)>,
+    next: u64,
+}
+
+#[cfg(feature = "cpu")]
+impl CpuVerifier {
+    pub fn new() -> Self {
+        CpuVerifier { keys: Vec::new(), done: None, next: 0 }
+    }
+}
+
+#[cfg(feature = "cpu")]
+impl BatchVerifier for CpuVerifier {
+    fn set_keys(&mut self, keys: &[[u8; 32]]) -> Result<Vec<bool>> {
+        // libp2p decodes the identity key once per peer (PublicKey::from_bytes = decompress);
+        // verify_strict additionally rejects a small-order A at every verification
+        self.keys = keys.iter().map(|k| ed25519_dalek::PublicKey::from_bytes(k).ok()).collect();
+        Ok(self.keys.iter().map(|k| k.is_some()).collect())
+    }
+    fn submit(&mut self, batch: SigBatch) -> Result<Ticket> {
+        use std::convert::TryFrom;
+        let mut bm = Bitmap::zeros(batch.len());
+        for i in 0..batch.len() {
+            let mut sig = [0u8; 64];
+            sig[..32].copy_from_slice(&batch.r[i]);
+            sig[32..].copy_from_slice(&batch.s[i]);
+            let ok = match (self.keys.get(batch.key_idx[i] as usize), ed25519_dalek::Signature::try_from(&sig[..])) {
+                (Some(Some(pk)), Ok(sig)) => pk.verify_strict(&batch.msg[i], &sig).is_ok(),
+                _ => false,
+            };
+            if ok {
+                bm.set(i);
+            }
+        }
+        self.next += 1;
+        self.done = Some((self.next, bm));
+        Ok(Ticket(self.next))
+    }
+    fn poll(&mut self, ticket: &Ticket) -> Result<Option<Bitmap>> {
+        match self.done.take() {
+            Some((id, bm)) if id == ticket.0 => Ok(Some(bm)),
+            other => {
+                self.done = other;
+                Err(Error { code: ffi::PBFT_EINVAL, message: "unknown ticket".into() })
+            }
+        }
+    }
+}
+
+/// libp2p PeerId (38 bytes: 00 24 08 01 12 20 || A) -> the Ed25519 key A.
+pub fn key_from_peer_id(peer_id: &[u8]) -> Result<[u8; 32]> {
+    let mut a = [0u8; 32];
+    check(unsafe { ffi::pbft_key_from_peer_id(peer_id.as_ptr(), peer_id.len(), a.as_mut_ptr()) })?;
+    Ok(a)
+}
+
+/// Round events reported by [`Replica::flush`].
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum RoundEvent {
+    /// The PrePrepare's signature verified: multicast this replica's Prepare.
+    PrePrepared { view: u64, seq: u64 },
+    /// prepared(m, v, n): 2f matching Prepares from distinct backups: multicast the Commit.
+    Prepared { view: u64, seq: u64 },
+    /// committed-local: 2f+1 matching Commits: execute and reply to the client.
+    CommittedLocal { view: u64, seq: u64 },
+}
+
+/// The round batcher + quorum state machine of one replica (include/pbft_replica.h).
+pub struct Replica {
+    raw: *mut ffi::pbft_replica,
+    // a Rust BatchVerifier installed as the batch verify callback (None: the GPU context)
+    verifier: Option<Box<Box<dyn BatchVerifier>>>,
+}
+
+extern "C" fn verify_trampoline(user: *mut c_void, r: *const u8, s: *const u8, key_idx: *const u16,
+                                msg: *const u8, msg_len: u32, msg_stride: u32, n: u64,
+                                bitmap_out: *mut u64) -> c_int {
+    if msg_len as usize != ffi::PBFT_ENVELOPE_BYTES || msg_stride as usize != ffi::PBFT_ENVELOPE_BYTES {
+        return ffi::PBFT_EINVAL;
+    }
+    let v = unsafe { &mut *(user as *mut Box<dyn BatchVerifier>) };
+    let n = n as usize;
+    let mut b = SigBatch::default();
+    unsafe {
+        b.r.extend_from_slice(std::slice::from_raw_parts(r as *const [u8; 32], n));
+        b.s.extend_from_slice(std::slice::from_raw_parts(s as *const [u8; 32], n));
+        b.key_idx.extend_from_slice(std::slice::from_raw_parts(key_idx, n));
+        b.msg.extend_from_slice(std::slice::from_raw_parts(msg as *const Envelope, n));
+    }
+    match v.verify(b) {
+        Ok(bm) => {
+            unsafe { ptr::copy_nonoverlapping(bm.0.as_ptr(), bitmap_out, bm.0.len()) };
+            0
+        }
+        Err(e) => e.code,
+    }
+}
+
+impl Replica {
+    /// `gpu`: the context whose key set is `keys` (pbft_verify_set_keys); replica ids are
+    /// positions in `keys` (network.json's "nodes" order); f = (n - 1) / 3.
+    pub fn new(gpu: Option<&GpuVerifier>, self_id: u32, keys: &[[u8; 32]]) -> Result<Self> {
+        let mut raw = ptr::null_mut();
+        let ctx = gpu.map(|g| g.raw()).unwrap_or(ptr::null_mut());
+        check(unsafe {
+            ffi::pbft_replica_create(ctx, keys.len() as u32, self_id, keys.as_ptr() as *const u8, &mut raw)
+        })?;
+        Ok(Replica { raw, verifier: None })
+    }
+    /// Back the batcher with any BatchVerifier (e.g. CpuVerifier) instead of the GPU context.
+    pub fn set_verifier(&mut self, v: Box<dyn BatchVerifier>) -> Result<()> {
+        let mut boxed: Box<Box<dyn BatchVerifier>> = Box::new(v);
+        let user = &mut *boxed as *mut Box<dyn BatchVerifier> as *mut c_void;
+        check(unsafe { ffi::pbft_replica_set_verifier(self.raw, verify_trampoline, user) })?;
+        self.verifier = Some(boxed);
+        Ok(())
+    }
+    /// PrePrepare ingress (validate_pre_prepare, src/behavior.rs:126-157, plus the signature TODO :127).
+    pub fn on_pre_prepare(&mut self, view: u64, seq: u64, operation: &[u8], digest: &[u8; 64],
+                          primary_sig: &[u8; 64]) -> Result<bool> {
+        let rc = check(unsafe {
+            ffi::pbft_replica_on_pre_prepare(self.raw, view, seq, operation.as_ptr(), operation.len() as u32,
+                                             digest.as_ptr(), primary_sig.as_ptr(), ptr::null_mut())
+        })?;
+        Ok(rc == 1)
+    }
+    /// A Prepare / Commit from the AUTHENTICATED peer `signer` (inject_node_event's peer_id).
+    pub fn push(&mut self, kind: u8, view: u64, seq: u64, digest: &[u8; 64], signer: u32, sig: &[u8; 64])
+                -> Result<bool> {
+        let rc = check(unsafe {
+            ffi::pbft_replica_push(self.raw, kind, view, seq, digest.as_ptr(), signer, sig.as_ptr())
+        })?;
+        Ok(rc == 1)
+    }
+    /// Raw UviBytes/JSON frames read from peer `peer_idx`'s connection; returns bytes consumed
+    /// (keep the rest for the next read).
+    pub fn push_frames(&mut self, peer_idx: u32, stream: &[u8]) -> Result<usize> {
+        let (mut used, mut pushed, mut dropped) = (0u64, 0u64, 0u64);
+        check(unsafe {
+            ffi::pbft_replica_push_frames(self.raw, peer_idx, stream.as_ptr(), stream.len(), &mut used,
+                                          &mut pushed, &mut dropped)
+        })?;
+        Ok(used as usize)
+    }
+    /// Verify every ready sub-window in one batch and report new round events
+    /// (call from NetworkBehaviour::poll; force = the deadline).
+    pub fn flush(&mut self, force: bool) -> Result<Vec<RoundEvent>> {
+        let mut ev = vec![ffi::pbft_round_event::default(); 1024];
+        let mut n = 0u32;
+        check(unsafe { ffi::pbft_replica_flush(self.raw, force as c_int, ev.as_mut_ptr(), ev.len() as u32, &mut n) })?;
+        Ok(ev[..n as usize].iter().filter_map(|e| match e.kind {
+            ffi::PBFT_EVENT_PRE_PREPARED => Some(RoundEvent::PrePrepared { view: e.view, seq: e.seq }),
+            ffi::PBFT_EVENT_PREPARED => Some(RoundEvent::Prepared { view: e.view, seq: e.seq }),
+            ffi::PBFT_EVENT_COMMITTED_LOCAL => Some(RoundEvent::CommittedLocal { view: e.view, seq: e.seq }),
+            _ => None,
+        }).collect())
+    }
+    /// The replica index of an authenticated connection's PeerId (None: not a replica).
+    pub fn peer_index(&self, peer_id: &[u8]) -> Option<u32> {
+        let rc = unsafe { ffi::pbft_replica_peer_index(self.raw, peer_id.as_ptr(), peer_id.len()) };
+        if rc >= 0 { Some(rc as u32) } else { None }
+    }
+    pub fn stable_checkpoint(&mut self, seq: u64) -> Result<()> {
+        check(unsafe { ffi::pbft_replica_stable_checkpoint(self.raw, seq) }).map(|_| ())
+    }
+    pub fn stats(&self) -> ffi::pbft_replica_stats {
+        let mut s = ffi::pbft_replica_stats::default();
+        unsafe { ffi::pbft_replica_get_stats(self.raw, &mut s) };
+        s
+    }
+}
+
+impl Drop for Replica {
+    fn drop(&mut self) {
+        unsafe { ffi::pbft_replica_destroy(self.raw) };
+    }
+}
