@@ -311,6 +311,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="only the headline line (no side legs)")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--settle-s", type=float, default=0.3, help="untimed GPU settle time before the warmup steps")
+    ap.add_argument("--sequential", action="store_true",
+                    help="N > 1: no round pipelining (kernel, finish and all-gather of a round on one stream)")
+    ap.add_argument("--pipeline", action="store_true", help="N = 1: pipeline rounds too (finish under the next comb)")
     args = ap.parse_args()
 
     import torch
@@ -325,7 +328,8 @@ def main():
 
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
     from pbft_amd.dist import allgather_bitmap, round_bitmap, shard_bounds, shard_words
-    from pbft_amd.roofline import INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_per_verify
+    from pbft_amd.roofline import (INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_comb,
+                                   products_per_verify)
 
     n_rep, n_seq = args.replicas, args.seqs
     seeds = key_seeds(n_rep)
@@ -349,19 +353,29 @@ def main():
     d_local = torch.zeros(per_words, dtype=torch.int64, device=dev)   # this rank's bitmap words (padded)
     d_all = torch.zeros(per_words * ws, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
-    stream = torch.cuda.Stream(dev)  # a dedicated stream: kernels, events and the all-gather are ordered on it
+    stream = torch.cuda.Stream(dev)      # comb kernels (and everything, --sequential)
+    fin_stream = torch.cuda.Stream(dev)  # pipelined rounds: finish + bitmap all-gather of round k under comb of k+1
     torch.cuda.set_stream(stream)
+    # N > 1: round k's finish and bitmap all-gather (fin_stream) run under round k+1's comb kernel (stream);
+    # N = 1: measured within 1 % of sequential (the finish competes for the same VALUs), so rounds run in order
+    pipelined = (ws > 1 and not args.sequential) or args.pipeline
 
-    def step(ev=None):
+    def step(ev=None, pipe=pipelined):
         if ev is not None:
             ev[0].record(stream)
         if n:
-            v.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
-                            ENVELOPE, n, d_local.data_ptr(), stream.cuda_stream)
+            if pipe:
+                v.verify_device_pipelined(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(),
+                                          ENVELOPE, ENVELOPE, n, d_local.data_ptr(), stream.cuda_stream,
+                                          fin_stream.cuda_stream)
+            else:
+                v.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                                ENVELOPE, n, d_local.data_ptr(), stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
         if ws > 1:
-            allgather_bitmap(d_local, ws, d_all)
+            with torch.cuda.stream(fin_stream if pipe else stream):
+                allgather_bitmap(d_local, ws, d_all)
 
     def check_round():
         words = round_bitmap(d_local, n_total, ws, d_all)
@@ -391,12 +405,37 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
-    kern_avg = float(np.mean(kern_ms))
+    kern_avg = float(np.mean(kern_ms))  # pipelined: the comb kernel (finish on fin_stream); sequential: the pair
     if ws > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     check_round()  # the bitmap of the last timed step, assembled from every rank's shard
+
+    # the same K rounds without pipelining (labelled figure): kernel, finish and all-gather of a round in order
+    seq = None
+    if pipelined and not args.no_extras:
+        sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+        for _ in range(2):
+            step(pipe=False)
+        if ws > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0s = time.perf_counter()
+        for k in range(args.steps):
+            step(sev[k], pipe=False)
+        torch.cuda.synchronize()
+        if ws > 1:
+            dist.barrier()
+        sdt = time.perf_counter() - t0s
+        if ws > 1:
+            t = torch.tensor([sdt], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            sdt = float(t.item())
+        check_round()
+        seq = {"value": n_total * args.steps / sdt, "ms_per_step": sdt / args.steps * 1e3,
+               "kernel_pair_avg_ms": float(np.mean([a.elapsed_time(b) for a, b in sev])),
+               "note": "rounds not pipelined: comb, finish and all-gather of one round on one stream"}
 
     # weak-scaling figure (labelled, not the headline): every rank verifies the WHOLE round
     weak = None
@@ -433,9 +472,18 @@ def main():
         # the per-GPU shard of an 8-GPU node (131,072 signatures): kernel time with the finish width it selects
         n8 = shard_bounds(n_total, 0, 8)[1]
         k8, w8 = time_device(v, stream, d, n8, 50, torch)
+        # the same shard pipelined over two streams (as bench runs at N = 8, minus the all-gather)
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(50):
+            v.verify_device_pipelined(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(),
+                                      ENVELOPE, ENVELOPE, n8, d["B"].data_ptr(), stream.cuda_stream,
+                                      fin_stream.cuda_stream)
+        torch.cuda.synchronize()
+        p8 = (time.perf_counter() - tp) * 1e3 / 50
         extras["shard_of_8"] = {"sigs": n8, "kernel_ms": k8, "wall_ms_per_launch": w8,
-                                "verifies_per_s_per_gpu": n8 / (k8 * 1e-3),
-                                "note": "device-resident launch over the shard one GPU of 8 verifies"}
+                                "verifies_per_s_per_gpu": n8 / (k8 * 1e-3), "pipelined_wall_ms_per_launch": p8,
+                                "note": "device-resident launches over the shard one GPU of 8 verifies"}
         # p50 latency of a 4096-signature round (config #5 batch size), device-resident
         lat = []
         n4 = min(4096, n)
@@ -458,7 +506,10 @@ def main():
     if rank == 0:
         total = n_total * args.steps
         value = total / dt
-        products = products_per_verify(pb, pa) * n / (kern_avg * 1e-3)
+        # the dominant kernel: comb_kernel alone when pipelined (its launch is what the events bracket),
+        # else the comb + finish pair
+        ppv = products_comb(pb, pa) if pipelined else products_per_verify(pb, pa)
+        products = ppv * n / (kern_avg * 1e-3)
         cpu = {} if args.no_cpu or ws > 1 else cpu_baselines(pub, R, S, key_idx, msg, expect)
         pmc = pmc_traffic(pb, pa, n)
         line = {
@@ -486,9 +537,12 @@ def main():
                          "valu_busy_pct": pmc.get("valu_busy_pct"),
                          "valu_insts_per_sig": pmc.get("valu_insts_per_sig"),
                          "gather_bytes_algorithmic": (gather_bytes_per_verify(pb, pa) + INPUT_BYTES) * n,
-                         "kernel": f"verify launch over this rank's shard: comb_kernel<85, plan PA={pa}> (PB={pb}) "
-                                   f"+ finish", "kernel_avg_ms": kern_avg,
-                         "products_per_verify": products_per_verify(pb, pa)},
+                         "kernel": (f"comb_kernel<85, plan PA={pa}> (PB={pb}) over this rank's shard (HIP events on "
+                                    f"its stream; the finish runs on the second stream)") if pipelined else
+                                   f"comb_kernel<85, plan PA={pa}> (PB={pb}) + finish over this rank's shard",
+                         "kernel_avg_ms": kern_avg, "products_per_verify": ppv},
+            "pipelined": pipelined,
+            "sequential_rounds": seq,
             "weak_scaling": weak,
             "cpu_baseline": cpu.get("port"),
             "cpu_baseline_openssl": cpu.get("openssl"),

@@ -104,6 +104,18 @@ int pbft_verify_batch_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d
                              const uint8_t *d_msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                              uint64_t *d_bitmap, void *stream);
 
+/* Pipelined device form (a stream of rounds): the one-lane-per-signature kernel of this batch runs on
+ * `stream`, its batch-inversion finish (which writes d_bitmap) on `finish_stream` after an event, so the
+ * next call's kernel on `stream` overlaps this finish and whatever the caller enqueues after it on
+ * finish_stream (e.g. the RCCL all-gather of the bitmaps).  The context alternates two workspace halves: a
+ * call waits, on `stream`, for the finish of the call two back.  d_bitmap is complete in finish_stream
+ * order.  Small batches (latency mode) run whole on `stream` and finish_stream waits for them.  The
+ * streams must differ; pbft_last_kernel_ms reports the `stream` kernel. */
+int pbft_verify_batch_device_pipelined(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d_S,
+                                       const uint16_t *d_key_idx, const uint8_t *d_msg, uint32_t msg_len,
+                                       uint32_t msg_stride, uint64_t N, uint64_t *d_bitmap, void *stream,
+                                       void *finish_stream);
+
 /* Pre-size the verify workspace (~230 bytes of HBM per signature) for batches
  * of up to max_n signatures, so that later launches allocate nothing (required
  * before capturing pbft_verify_batch_device into a hipGraph). */

@@ -812,7 +812,13 @@ struct pbft_ctx {
   // verify workspace: R' limbs [30][N] u32 + flags[N]
   uint8_t* d_work = nullptr;
   size_t work_cap = 0;
+  uint64_t work_n = 0;     // signatures the workspace layout is sized for (offsets use this, not the batch N)
+  bool work_two = false;   // two xyz/flags halves (pipelined form)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
+  // pipelined device form: comb on the caller's stream, finish on a second stream, two workspace halves
+  hipEvent_t ev_comb = nullptr, ev_fin[2] = {nullptr, nullptr};
+  bool fin_pending[2] = {false, false};
+  int half = 0;
   // host-buffer pipeline: H2D of chunk c+1 (copy stream) overlaps the kernels of chunk c
   hipStream_t cstream = nullptr;
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
@@ -854,36 +860,64 @@ static constexpr int MAX_STEPS = steps<PLB, PLA_SMALL>::N;  // the smallest key 
 static_assert(steps<PLB, PLA_SMALL>::N >= steps<PLB, PLA_MID>::N && steps<PLB, PLA_MID>::N >= steps<PLB, PLA_BIG>::N,
               "");
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
-static int ensure_work(pbft_ctx* c, uint64_t N) {
+static inline size_t eidx_bytes(uint64_t N) {
   const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
   // (latency mode: SPLIT lanes per signature, 8-byte entry addresses, ceil(steps / SPLIT) per lane)
   const size_t split = 8 * (size_t)((MAX_STEPS + SPLIT - 1) / SPLIT) * (Npad * SPLIT + BLOCK);
-  const size_t need = eidx_offset(N) + (4 * (size_t)MAX_STEPS * Npad > split ? 4 * (size_t)MAX_STEPS * Npad : split) + 256;
-  if (need <= c->work_cap) return PBFT_OK;
+  const size_t comb = 4 * (size_t)MAX_STEPS * Npad;
+  return ((comb > split ? comb : split) + 255) & ~(size_t)255;
+}
+// second xyz/flags half (pipelined form) after the entry-index region
+static inline size_t half1_offset(uint64_t N) { return eidx_offset(N) + eidx_bytes(N); }
+// The layout is a function of c->work_n only, never of the batch at hand: a smaller batch must not move
+// the entry-index region onto the xyz/flags half a pipelined finish may still be reading.
+static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
+  if (N <= c->work_n && (!two_halves || c->work_two)) return PBFT_OK;
+  const uint64_t W = N > c->work_n ? N : c->work_n;
+  const bool two = two_halves || c->work_two;
+  const size_t need = (two ? half1_offset(W) + eidx_offset(W) : half1_offset(W)) + 256;
+  // nothing may still read the old workspace: the finishes of earlier pipelined launches, then this stream
+  for (int h = 0; h < 2; ++h)
+    if (c->fin_pending[h]) { HIP_TRY(hipEventSynchronize(c->ev_fin[h])); c->fin_pending[h] = false; }
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->d_work) HIP_TRY(hipDeviceSynchronize());  // a device-form launch may run on a caller's stream
   if (c->d_work) HIP_TRY(hipFree(c->d_work));
   c->d_work = nullptr;
   c->work_cap = 0;
+  c->work_n = 0;
+  c->work_two = false;
   if (hipMalloc(&c->d_work, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
   c->work_cap = need;
+  c->work_n = W;
+  c->work_two = two;
   return PBFT_OK;
 }
 
+// fst != null: pipelined form -- the finish runs on fst after an event, on one of two
+// workspace halves, so the next launch's comb (on st) overlaps it.
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
-                         uint32_t rs_stride = 32, uint32_t k_stride = 2) {
+                         uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
-  int rc = ensure_work(c, N);
+  int rc = ensure_work(c, N, fst != nullptr);
   if (rc) return rc;
+  int h = 0;
+  if (fst) {
+    h = c->half;
+    c->half ^= 1;
+  }
+  if (c->fin_pending[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));  // a pipelined finish still reading half h
 #if !PBFT_NO_LAUNCH_EVENTS
   HIP_TRY(hipEventRecord(c->ev0, st));
 #endif
   const dim3 g((unsigned)blocks), b(BLOCK);
-  uint32_t* xyz = (uint32_t*)c->d_work;
-  uint8_t* flags = c->d_work + 120 * N;
-  uint32_t* eidx = (uint32_t*)(c->d_work + eidx_offset(N));
+  const uint64_t W = c->work_n;  // layout (>= N)
+  uint8_t* hw = c->d_work + (h ? half1_offset(W) : 0);
+  uint32_t* xyz = (uint32_t*)hw;
+  uint8_t* flags = hw + 120 * N;  // within the half's 121 W bytes
+  uint32_t* eidx = (uint32_t*)(c->d_work + eidx_offset(W));
   const uint64_t Npad = blocks * BLOCK;
 #define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
   hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS,             \
@@ -922,6 +956,14 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
 #undef PBFT_LAUNCH_COMB
 #undef PBFT_LAUNCH_SPLIT
   HIP_TRY(hipGetLastError());
+  if (fst) {
+#if !PBFT_NO_LAUNCH_EVENTS
+    HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
+#endif
+    HIP_TRY(hipEventRecord(c->ev_comb, st));
+    HIP_TRY(hipStreamWaitEvent(fst, c->ev_comb, 0));
+    st = fst;
+  }
   if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
     // signatures per finish lane (one divsteps inversion per lane): measured on MI355X
     // (tools/size_probe.py, profiles/r02_size_probe.md) -- 1 up to 2^16, 4 up to 2^18, then 16
@@ -937,6 +979,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     else PBFT_LAUNCH_FIN(1);
 #undef PBFT_LAUNCH_FIN
     HIP_TRY(hipGetLastError());
+  }
+  if (fst) {
+    HIP_TRY(hipEventRecord(c->ev_fin[h], fst));
+    c->fin_pending[h] = true;
+    return PBFT_OK;
   }
 #if !PBFT_NO_LAUNCH_EVENTS
   HIP_TRY(hipEventRecord(c->ev1, st));
@@ -1087,14 +1134,19 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  HIP_TRY(hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming));
   for (int b = 0; b < 2; ++b) {
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_fin[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_consumed[b], hipEventDisableTiming));
   }
   int rc = acquire_base_table(device, c->stream, &c->d_tabB);
   if (rc) {
     (void)hipEventDestroy(c->ev0); (void)hipEventDestroy(c->ev1); (void)hipEventDestroy(c->ev_done);
-    for (int b = 0; b < 2; ++b) { (void)hipEventDestroy(c->ev_copied[b]); (void)hipEventDestroy(c->ev_consumed[b]); }
+    for (int b = 0; b < 2; ++b) {
+      (void)hipEventDestroy(c->ev_copied[b]); (void)hipEventDestroy(c->ev_consumed[b]); (void)hipEventDestroy(c->ev_fin[b]);
+    }
+    (void)hipEventDestroy(c->ev_comb);
     (void)hipStreamDestroy(c->cstream);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -1117,9 +1169,12 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   for (int b = 0; b < 2; ++b) {
+    if (c->fin_pending[b]) (void)hipEventSynchronize(c->ev_fin[b]);
     if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
     if (c->ev_consumed[b]) (void)hipEventDestroy(c->ev_consumed[b]);
+    if (c->ev_fin[b]) (void)hipEventDestroy(c->ev_fin[b]);
   }
+  if (c->ev_comb) (void)hipEventDestroy(c->ev_comb);
   if (c->cstream) { (void)hipStreamSynchronize(c->cstream); (void)hipStreamDestroy(c->cstream); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1293,6 +1348,19 @@ int pbft_verify_batch_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, 
   return launch_verify(c, dR, dS, dK, dM, msg_len, msg_stride, N, dB, st);
 }
 
+int pbft_verify_batch_device_pipelined(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK,
+                                       const uint8_t* dM, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                                       uint64_t* dB, void* stream, void* finish_stream) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (!stream || !finish_stream || stream == finish_stream)
+    return set_err(PBFT_EINVAL, "two distinct non-null streams required");
+  if (!check_batch_args(dR, dS, dK, dM, msg_len, msg_stride, N, dB)) return set_err(PBFT_EINVAL, "bad batch arguments");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  HIP_TRY(hipSetDevice(c->device));
+  return launch_verify(c, dR, dS, dK, dM, msg_len, msg_stride, N, dB, (hipStream_t)stream, 32, 2,
+                       (hipStream_t)finish_stream);
+}
+
 // Binary wire records (include/pbft_wire.h): R at +0, S at +32, envelope at +64,
 // key index at +150, stride 160 -- read in place by the same kernels.
 int pbft_verify_records_device(pbft_ctx* c, const uint8_t* d_rec, uint64_t N, uint64_t* dB, void* stream) {
@@ -1435,7 +1503,7 @@ int pbft_sign_batch(pbft_ctx* c, const uint8_t* seeds, uint32_t n_seeds, const u
 int pbft_verify_reserve(pbft_ctx* c, uint64_t max_n) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   HIP_TRY(hipSetDevice(c->device));
-  return ensure_work(c, max_n);
+  return ensure_work(c, max_n, true);  // both halves: either device form can then be captured
 }
 
 int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {

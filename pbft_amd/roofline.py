@@ -12,7 +12,7 @@ per lane):
   comb       (PB + PA - 1) mixed additions x 7 field muls x 100 products
              + 1 mul for the first step, built directly from its table entry
              (10 + 14 positions with the default balanced plans)
-  inversion  (254 squarings x 55 + 11 muls x 100) / FIN_M
+  inversion  one divsteps inversion (20 x 90 products) / FIN_M
   batch      3 muls per signature (prefix, 1/Z_m, running inverse) +
              2 affine muls (x, y), x 100
   Barrett    9x9 + 44 word products (k mod L)
@@ -31,8 +31,20 @@ ENTRY_BYTES = 128
 INPUT_BYTES = 32 + 32 + 2 + 85  # R, S, key index, envelope
 
 
+# divsteps inversion (inv25519.h): per batch of 30 divsteps, [f, g] update 4 x 9 and [d, e] update 6 x 9
+# 32x32->64 products; 20 batches
+INV_PRODUCTS = 20 * (4 * 9 + 6 * 9)
+
+
+def products_comb(pb: int, pa: int) -> int:
+    """comb_kernel alone: (PB + PA - 1) mixed additions x 7 muls + 1 mul (first step) + Barrett k mod L."""
+    return ((pb + pa - 1) * 7 + 1) * 100 + (81 + 44)
+
+
 def products_per_verify(pb: int, pa: int) -> int:
-    return ((pb + pa - 1) * 7 + 1) * 100 + (254 * 55 + 11 * 100) // FIN_M + 5 * 100 + (81 + 44)
+    """comb_kernel + finish_kernel<16>: + one divsteps inversion per 16 signatures, 3 batch-inversion muls and 2
+    affine muls per signature."""
+    return products_comb(pb, pa) + INV_PRODUCTS // FIN_M + 5 * 100
 
 
 def gather_bytes_per_verify(pb: int, pa: int) -> int:
@@ -40,14 +52,14 @@ def gather_bytes_per_verify(pb: int, pa: int) -> int:
 
 
 def positions_from_build_info(info: str):
-    """(PB, PA_big) from pbft_build_info(), e.g. 'pbft_verify gfx950 PB=10 PA=14|16|32 ...'."""
+    """(PB, widest PA) from pbft_build_info(), e.g. 'pbft_verify gfx950 PB=10 PA=13|14|16|32 ...'."""
     m = re.search(r"PB=(\d+) PA=(\d+)", info)
     if not m:
         raise ValueError(f"unexpected build info: {info!r}")
     return int(m.group(1)), int(m.group(2))
 
 
-# defaults of the shipped build (base point 10 positions, keys 14 for n <= 360)
+# defaults of the shipped build (base point 10 positions, keys 13 for n = 256 on a 288-GB MI355X)
 PB = 10
-PA = 14
+PA = 13
 PRODUCTS_PER_VERIFY = products_per_verify(PB, PA)

@@ -140,6 +140,12 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_batch_device(self._ctx, d_R, d_S, d_key_idx, d_msg, msg_len, msg_stride, n,
                                                  d_bitmap, stream or None))
 
+    def verify_device_pipelined(self, d_R: int, d_S: int, d_key_idx: int, d_msg: int, msg_len: int,
+                                msg_stride: int, n: int, d_bitmap: int, stream: int, finish_stream: int) -> None:
+        """Kernel on `stream`, finish (bitmap) on `finish_stream`: the next call's kernel overlaps this finish."""
+        check(self._lib.pbft_verify_batch_device_pipelined(self._ctx, d_R, d_S, d_key_idx, d_msg, msg_len, msg_stride,
+                                                           n, d_bitmap, stream, finish_stream))
+
     def reserve(self, max_n: int) -> None:
         """Pre-size the workspace (required before capturing verify_device into a graph)."""
         check(self._lib.pbft_verify_reserve(self._ctx, max_n))

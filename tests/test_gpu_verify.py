@@ -438,3 +438,38 @@ def test_smaller_key_plans(gv, coracle, golden, budget_mb, pa):
         assert (got == exp).all(), (pa, np.nonzero(got != exp)[0][:10])
     finally:
         v.close()
+
+
+def test_pipelined_device_rounds(gv, coracle):
+    """pbft_verify_batch_device_pipelined: consecutive rounds with the comb on one stream and the finish on another
+    (two workspace halves, the comb of round k+1 overlapping the finish of round k); every round's bitmap equals the
+    oracle's, including a latency-mode batch in the middle and a ragged tail."""
+    import torch
+    from pbft_amd import bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 1024, tag=21)    # 131,072 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(21)
+    rounds = []
+    for k in range(5):
+        R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg, frac=0.002)
+        n = (len(R), len(R) - 37, 4096, len(R), 70_001)[k]
+        rounds.append((R2[:n], S2[:n], K2[:n], M2[:n]))
+    dev = torch.device("cuda", 0)
+    import bench
+    dsets = [bench.to_device(torch, dev, *r) for r in rounds]
+    a, b = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    exps = [oracle_bits(coracle, pub, r[0], r[1], r[2], r[3], 85) for r in rounds]
+    torch.cuda.synchronize()
+    for rep in range(2):
+        for ds, r in zip(dsets, rounds):
+            ds["B"].zero_()
+        torch.cuda.synchronize()
+        for ds, r in zip(dsets, rounds):
+            gv.verify_device_pipelined(ds["R"].data_ptr(), ds["S"].data_ptr(), ds["K"].data_ptr(), ds["M"].data_ptr(),
+                                       85, 85, len(r[0]), ds["B"].data_ptr(), a.cuda_stream, b.cuda_stream)
+        torch.cuda.synchronize()
+        for ds, r, exp in zip(dsets, rounds, exps):
+            got = bitmap_to_bool(ds["B"].cpu().numpy().view(np.uint64), len(r[0]))
+            assert (got == exp).all(), (rep, len(r[0]), np.nonzero(got != exp)[0][:8])
+    with pytest.raises(Exception):
+        gv.verify_device_pipelined(0, 0, 0, 0, 85, 85, 1, 0, a.cuda_stream, a.cuda_stream)  # same stream twice
