@@ -152,7 +152,7 @@ def pmc_traffic(pb: int, pa: int, n: int) -> dict:
             continue
         return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
                 "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
-                "valu_insts_per_sig": d["comb_kernel"].get("valu_insts_per_sig"),
+                "valu_insts_per_sig": d.get("valu_insts_per_sig_total"),
                 "source": f"profiles/{rnd}_pmc_comb/derived.json (PMC passes, not this run)"}
     return {}
 

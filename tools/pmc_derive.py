@@ -30,11 +30,14 @@ for k in ("comb_kernel", "finish_kernel"):
     fb, wbytes = 2 * m["FETCH_SIZE"] * 1024, m["WRITE_SIZE"] * 1024
     out[k] = {"fetch_bytes": fb, "write_bytes": wbytes, "valu_busy_pct": m.get("VALUBusy"),
               "valu_lane_utilisation_pct": m.get("VALUUtilization"),
-              "valu_insts_per_lane": m["SQ_INSTS_VALU"] / m["SQ_WAVES"], "waves": m["SQ_WAVES"]}
+              "valu_insts_per_lane": m["SQ_INSTS_VALU"] / m["SQ_WAVES"], "waves": m["SQ_WAVES"],
+              # wave-instructions x 64 lanes / signatures: the VALU instructions one signature costs
+              "valu_insts_per_sig": m["SQ_INSTS_VALU"] * 64 / n}
     tot += fb + wbytes
 out["traffic_bytes_per_launch"] = tot
+out["valu_insts_per_sig_total"] = sum(out[k]["valu_insts_per_sig"] for k in ("comb_kernel", "finish_kernel"))
 out["note"] = ("rocprofv3 --pmc passes (one counter group per run, no tracing) of `python3 bench.py --steps 5 "
-               "--warmup 1 --no-cpu --latency-iters 0` (tools/gpu_pmc_cur.sh); FETCH_SIZE (KB) doubled per the "
+               "--warmup 1 --no-cpu --no-extras` (tools/gpu_pmc_cur.sh); FETCH_SIZE (KB) doubled per the "
                "gfx950 correction of MI355X_MICROARCH.md's HBM section; WRITE_SIZE taken as is")
 json.dump(out, open(os.path.join(d, "derived.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
