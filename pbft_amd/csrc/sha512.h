@@ -26,6 +26,70 @@ __host__ __device__ __forceinline__ uint64_t ror64(uint64_t x, int n) {
   return (x >> n) | (x << (64 - n));
 #endif
 }
+// 3-input VOP3 logic on gfx950: one v_bitop3_b32 instead of two or three VOP2 ops (LLVM keeps the VOP2
+// pairs on its own).  Sigma functions XOR three rotations (table 0x96); Maj is table 0xE8.
+__host__ __device__ __forceinline__ uint32_t xor3_32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));  // gfx950 has no v_xor3
+  return r;
+#else
+  return a ^ b ^ c;
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t maj32(uint32_t a, uint32_t b, uint32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xe8" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+#else
+  return (a & b) | (c & (a | b));
+#endif
+}
+__host__ __device__ __forceinline__ uint32_t ab32(uint32_t hi, uint32_t lo, int n) {  // (hi:lo) >> n, low word
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbit(hi, lo, n);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> n);
+#endif
+}
+#define LO32(x) ((uint32_t)(x))
+#define HI32(x) ((uint32_t)((x) >> 32))
+// pack two halves as a register pair (a bitcast, not shift + or: LLVM would turn "(h << 32) | l" into an add
+// and re-associate it with the round's 64-bit additions, doubling them)
+__host__ __device__ __forceinline__ uint64_t MK64(uint32_t h, uint32_t l) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+  const u32x2 v = {l, h};
+  return __builtin_bit_cast(uint64_t, v);
+#else
+  return ((uint64_t)h << 32) | l;
+#endif
+}
+// Sigma1(e) = ror14 ^ ror18 ^ ror41, Sigma0(a) = ror28 ^ ror34 ^ ror39 (ror41 = ror(9) of the swapped halves...)
+__host__ __device__ __forceinline__ uint64_t big_sigma1(uint64_t x) {
+  const uint32_t l = LO32(x), h = HI32(x);
+  return MK64(xor3_32(ab32(l, h, 14), ab32(l, h, 18), ab32(h, l, 9)),
+              xor3_32(ab32(h, l, 14), ab32(h, l, 18), ab32(l, h, 9)));
+}
+__host__ __device__ __forceinline__ uint64_t big_sigma0(uint64_t x) {
+  const uint32_t l = LO32(x), h = HI32(x);
+  return MK64(xor3_32(ab32(l, h, 28), ab32(h, l, 2), ab32(h, l, 7)),
+              xor3_32(ab32(h, l, 28), ab32(l, h, 2), ab32(l, h, 7)));
+}
+// sigma0(w) = ror1 ^ ror8 ^ (w >> 7), sigma1(w) = ror19 ^ ror61 ^ (w >> 6)
+__host__ __device__ __forceinline__ uint64_t small_sigma0(uint64_t x) {
+  const uint32_t l = LO32(x), h = HI32(x);
+  return MK64(xor3_32(ab32(l, h, 1), ab32(l, h, 8), h >> 7), xor3_32(ab32(h, l, 1), ab32(h, l, 8), ab32(h, l, 7)));
+}
+__host__ __device__ __forceinline__ uint64_t small_sigma1(uint64_t x) {
+  const uint32_t l = LO32(x), h = HI32(x);
+  return MK64(xor3_32(ab32(l, h, 19), ab32(h, l, 29), h >> 6), xor3_32(ab32(h, l, 19), ab32(l, h, 29), ab32(h, l, 6)));
+}
+__host__ __device__ __forceinline__ uint64_t maj64(uint64_t a, uint64_t b, uint64_t c) {
+  return MK64(maj32(HI32(a), HI32(b), HI32(c)), maj32(LO32(a), LO32(b), LO32(c)));
+}
+
 __host__ __device__ __forceinline__ uint32_t bswap32(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
 }
@@ -70,11 +134,11 @@ __constant__ static const uint64_t SHA512_K[80] = SHA512_K_TABLE;
 __host__ __device__ __forceinline__ void sha512_round(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d,
                                                       uint64_t& e, uint64_t& f, uint64_t& g, uint64_t& h,
                                                       uint64_t k, uint64_t w) {
-  const uint64_t S1 = ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41);
+  const uint64_t S1 = big_sigma1(e);
   const uint64_t ch = (e & f) ^ (~e & g);
   const uint64_t T1 = h + S1 + ch + k + w;
-  const uint64_t S0 = ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39);
-  const uint64_t mj = (a & b) ^ (c & (a ^ b));
+  const uint64_t S0 = big_sigma0(a);
+  const uint64_t mj = maj64(a, b, c);
   h = g; g = f; f = e; e = d + T1; d = c; c = b; b = a; a = T1 + S0 + mj;
 }
 
@@ -92,8 +156,8 @@ __host__ __device__ __forceinline__ void sha512_compress(uint64_t H[8], uint64_t
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
-      const uint64_t s0 = ror64(w15, 1) ^ ror64(w15, 8) ^ (w15 >> 7);
-      const uint64_t s1 = ror64(w2, 19) ^ ror64(w2, 61) ^ (w2 >> 6);
+      const uint64_t s0 = small_sigma0(w15);
+      const uint64_t s1 = small_sigma1(w2);
       W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
       sha512_round(a, b, c, d, e, f, g, h, K[t0 + j], W[j]);
     }
