@@ -426,29 +426,32 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 // signature leaves most SIMDs idle, and the round's latency is one lane's
 // serial work: SHA-512, 24 comb steps, then the finish kernel's inversion.
 // comb_latency_kernel (blocks of 4 waves -- one per SIMD, so each may use the
-// whole register file -- and 48 signatures per block) instead
-//  * gives every signature SPLIT = 4 lanes in waves 0-2: each lane computes the
-//    challenge hash itself (it is on the critical path anyway), then the steps
+// whole register file -- and 64 signatures per block) instead
+//  * gives every signature SPLIT = 4 lanes: each lane computes the challenge
+//    hash itself (it is on the critical path anyway), then the steps
 //    j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a step in the
 //    last round add the identity entry), and the 4 partial points are summed
-//    with two shuffle + extended-addition rounds;
-//  * meanwhile wave 3 decompresses the 48 R encodings (dalek's decompress,
-//    ge_decompress) -- the one exponentiation per signature, off the comb's
-//    critical path -- so no inversion is needed: after a block barrier R' is
-//    compared with R projectively (X' == x_R Z', Y' == y_R Z'), R's small order
-//    is read from its canonical y, and each comb wave writes 16 bitmap bits
-//    (the bitmap as u16 pieces: piece 3 * block + wave).
-// Equivalent to the throughput path's compare (R' == decompress(R) as points,
-// DESIGN.md "R check"); ~2.5x lower latency than one lane per signature.
+//    with two shuffle + extended-addition rounds (every lane of the group then
+//    holds R');
+//  * R' is compressed with ONE divsteps inversion (inv25519.h, ~20 us on the
+//    chain) and compared with the canonical R encoding, as the finish kernel
+//    does; each wave writes 16 bitmap bits (u16 pieces: piece 4 * block + wave).
+// Round 1 instead decompressed R on a fourth wave in parallel (z^((p-5)/8):
+// 254 squarings on one wave, ~80 us -- the critical path); PBFT_LAT_DECOMP=1
+// keeps that variant for A/B.  ~2.5x lower latency than one lane per signature.
+#ifndef PBFT_LAT_DECOMP
+#define PBFT_LAT_DECOMP 0
+#endif
 static constexpr int SPLIT = 4;
-static constexpr int LAT_COMB_WAVES = 3;
-static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // 48 signatures per block
-static constexpr int LAT_BLOCK = (LAT_COMB_WAVES + 1) * 64;  // + 1 decompression wave
+static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
+static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // signatures per block
+static constexpr int LAT_BLOCK = 4 * 64;                   // (PBFT_LAT_DECOMP: 3 comb waves + 1 decompression wave)
 #ifndef PBFT_SPLIT_BELOW
 #define PBFT_SPLIT_BELOW 12288  // measured crossover: 8,192 sigs 0.105 ms here vs 0.133 ms one-lane; 16,384: 0.195 vs 0.133
 #endif
 static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_latency_kernel
-static constexpr uint32_t LAT_LDS = LAT_COMB_WAVES * COMB_LDS_PER_WAVE + 21 * 64 * 4;  // entry buffers + x_R, y_R, ok
+static constexpr uint32_t LAT_LDS =
+    LAT_COMB_WAVES * COMB_LDS_PER_WAVE + (PBFT_LAT_DECOMP ? 21 * 64 * 4 : 0);  // entry buffers (+ x_R, y_R, ok)
 
 // Line-coalesced gather with per-lane 64-bit entry addresses (the split kernel's
 // lanes of one wave gather from both tables in the same step).
@@ -485,6 +488,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+#if PBFT_LAT_DECOMP
   uint32_t* rdec = (uint32_t*)(lds + LAT_COMB_WAVES * COMB_LDS_PER_WAVE);  // [21][64]: x_R, y_R limbs, ok
   if (wave == LAT_COMB_WAVES) {
     // ---- decompression wave: R of signature blockIdx * LAT_SIGS + lane (lanes >= LAT_SIGS idle)
@@ -507,6 +511,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     __syncthreads();
     return;
   }
+#endif
   // ---- comb waves: 16 signatures per wave, SPLIT lanes each
   const uint64_t g = (uint64_t)blockIdx.x * (LAT_COMB_WAVES * 64) + threadIdx.x;  // global comb lane, < Lpad
   const uint64_t i = g / SPLIT;
@@ -604,8 +609,9 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
   };
   combine(1);
   combine(2);
-  __syncthreads();  // x_R, y_R of the block's signatures are in LDS
   bool acc = false;
+#if PBFT_LAT_DECOMP
+  __syncthreads();  // x_R, y_R of the block's signatures are in LDS
   if (r == 0 && live) {
     const int l = (int)(threadIdx.x >> 2);  // signature within the block
     fe xr, yr, t1, t2;
@@ -615,6 +621,24 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     fe_mul(t2, yr, P.Z);
     acc = rdec[20 * 64 + l] && s_ok && kok && fe_eq(P.X, t1) && fe_eq(P.Y, t2);
   }
+#else
+  {
+    // compress R' (one divsteps inversion) and compare with the canonical R encoding (DESIGN.md "R check")
+    fe zi, x, y;
+    fe_invert_gcd(zi, P.Z);
+    fe_mul(x, P.X, zi);
+    fe_mul(y, P.Y, zi);
+    uint32_t xw[8], yw[8], rr[8], ry[8];
+    fe_to_words(xw, x);
+    fe_to_words(yw, y);
+    load32(rr, R + (size_t)rs_stride * ii);
+    canon_y(ry, rr);
+    bool eq = (xw[0] & 1u) == (rr[7] >> 31);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) eq = eq && yw[t] == ry[t];
+    acc = r == 0 && live && s_ok && kok && eq && !y_is_small_order(yw);
+  }
+#endif
   // lanes 4j (j = 0..15) hold this wave's 16 results: one 16-bit piece of the block's bitmap word
   const uint64_t vote = __ballot(acc);
   uint32_t bits = 0;
