@@ -254,6 +254,28 @@ def e2e_host_round(v, R, S, key_idx, msg, expect, torch, iters: int = 5):
                     "+ bitmap D2H, pbft_verify_batch", "bytes_h2d_per_sig": 32 + 32 + 2 + ENVELOPE}
 
 
+def e2e_votes_round(v, R, S, key_idx, msg, expect, torch, iters: int = 5):
+    """PCIe-inclusive 2^20 round in the votes form (pbft_verify_votes): per signature R, S, key index and a 4-byte
+    index into the round's 4,096 distinct envelopes (one per (seq, kind)), 70 B instead of 151 B over PCIe."""
+    from pbft_amd import bitmap_to_bool
+    env, inv = np.unique(msg, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()  # noqa: E731
+    Rp, Sp, Kp, Ip, Ep = pin(R), pin(S), pin(key_idx), pin(ei), pin(env)
+    bm = v.verify_votes(Rp, Sp, Kp, Ip, Ep)
+    assert (bitmap_to_bool(bm, len(R)) == expect).all(), "votes path bitmap differs"
+    ts = []
+    for _ in range(iters):
+        t = time.perf_counter()
+        v.verify_votes(Rp, Sp, Kp, Ip, Ep)
+        ts.append(time.perf_counter() - t)
+    ms = float(np.median(ts)) * 1e3
+    return {"value": len(R) / (ms * 1e-3), "unit": "verifies/s", "ms_per_round": ms, "sigs": len(R),
+            "envelopes": len(env), "bytes_h2d_per_sig": 32 + 32 + 2 + 4,
+            "path": "pinned host buffers: pbft_verify_votes (R, S, key index, envelope index per signature + the "
+                    "round's envelope table), chunked H2D overlapped with the kernels, bitmap D2H"}
+
+
 def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 signatures per window batch, one GPU
     (device-resident p50 and host-buffer p50) vs the CPU baselines on the same batch."""
@@ -311,9 +333,9 @@ def main():
     ap.add_argument("--no-extras", action="store_true", help="only the headline line (no side legs)")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--settle-s", type=float, default=0.3, help="untimed GPU settle time before the warmup steps")
-    ap.add_argument("--sequential", action="store_true",
-                    help="N > 1: no round pipelining (kernel, finish and all-gather of a round on one stream)")
-    ap.add_argument("--pipeline", action="store_true", help="N = 1: pipeline rounds too (finish under the next comb)")
+    ap.add_argument("--sequential", action="store_true", help="force rounds in order on one stream (the default)")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="pipeline rounds: finish + all-gather of round k on a second stream under round k+1's comb")
     args = ap.parse_args()
 
     import torch
@@ -356,9 +378,11 @@ def main():
     stream = torch.cuda.Stream(dev)      # comb kernels (and everything, --sequential)
     fin_stream = torch.cuda.Stream(dev)  # pipelined rounds: finish + bitmap all-gather of round k under comb of k+1
     torch.cuda.set_stream(stream)
-    # N > 1: round k's finish and bitmap all-gather (fin_stream) run under round k+1's comb kernel (stream);
-    # N = 1: measured within 1 % of sequential (the finish competes for the same VALUs), so rounds run in order
-    pipelined = (ws > 1 and not args.sequential) or args.pipeline
+    # --pipeline: round k's finish and bitmap all-gather (fin_stream) run under round k+1's comb kernel (stream).
+    # Off by default: measured at N = 1 within 1 % of sequential on a 2^20 round and 15 % SLOWER on the 131k
+    # shard of an 8-GPU node (0.246 vs 0.215 ms: the finish competes for the same VALUs and the cross-stream
+    # events cost more than they hide), so rounds run in order on one stream
+    pipelined = args.pipeline and not args.sequential
 
     def step(ev=None, pipe=pipelined):
         if ev is not None:
@@ -501,6 +525,7 @@ def main():
         extras["stream_4k"] = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21)),
                                "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
         extras["e2e_2^20"] = e2e_host_round(v, R, S, key_idx, msg, expect, torch)
+        extras["e2e_votes_2^20"] = e2e_votes_round(v, R, S, key_idx, msg, expect, torch)
         extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
 
     if rank == 0:

@@ -116,6 +116,18 @@ int pbft_verify_batch_device_pipelined(pbft_ctx *ctx, const uint8_t *d_R, const 
                                        uint32_t msg_stride, uint64_t N, uint64_t *d_bitmap, void *stream,
                                        void *finish_stream);
 
+/* Votes form of a round batch: a PBFT window's Prepares / Commits sign only (kind, view, seq, digest), so the
+ * n_env distinct 85-byte envelopes of the batch (one per (kind, seq) of its windows; pbft_envelope) are passed
+ * once and signature i names its envelope: envelopes[env_idx[i]].  70 bytes per signature cross PCIe instead
+ * of 151.  env_idx[i] >= n_env is bit 0.  Blocking, host buffers (chunked H2D overlapped with the kernels). */
+int pbft_verify_votes(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
+                      const uint32_t *env_idx, const uint8_t *envelopes, uint32_t n_env, uint64_t N,
+                      uint64_t *bitmap_out);
+/* Device-resident votes form; d_envelopes readable for n_env * 85 + 16 bytes.  Enqueue only. */
+int pbft_verify_votes_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d_S, const uint16_t *d_key_idx,
+                             const uint32_t *d_env_idx, const uint8_t *d_envelopes, uint32_t n_env, uint64_t N,
+                             uint64_t *d_bitmap, void *stream);
+
 /* Pre-size the verify workspace (~230 bytes of HBM per signature) for batches
  * of up to max_n signatures, so that later launches allocate nothing (required
  * before capturing pbft_verify_batch_device into a hipGraph). */

@@ -119,6 +119,12 @@ extern "C" {
                                               d_key_idx: *const u16, d_msg: *const u8, msg_len: u32,
                                               msg_stride: u32, n: u64, d_bitmap: *mut u64, stream: *mut c_void,
                                               finish_stream: *mut c_void) -> c_int;
+    pub fn pbft_verify_votes(ctx: *mut pbft_ctx, r: *const u8, s: *const u8, key_idx: *const u16,
+                             env_idx: *const u32, envelopes: *const u8, n_env: u32, n: u64,
+                             bitmap_out: *mut u64) -> c_int;
+    pub fn pbft_verify_votes_device(ctx: *mut pbft_ctx, d_r: *const u8, d_s: *const u8, d_key_idx: *const u16,
+                                    d_env_idx: *const u32, d_envelopes: *const u8, n_env: u32, n: u64,
+                                    d_bitmap: *mut u64, stream: *mut c_void) -> c_int;
     pub fn pbft_verify_reserve(ctx: *mut pbft_ctx, max_n: u64) -> c_int;
     pub fn pbft_digest_blake2b512(ctx: *mut pbft_ctx, data: *const u8, offsets: *const u64, lens: *const u32,
                                   n: u64, out: *mut u8) -> c_int;

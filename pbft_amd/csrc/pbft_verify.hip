@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
-    uint32_t* __restrict__ eidx) {
+    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
   using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -322,6 +322,13 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
       const uint4 k0 = kp[0], k1 = kp[1];
       a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
     }
+    // the signed message: row ii, or the envelope table row msg_idx[ii] (votes form; out of range -> bit 0)
+    uint64_t mrow = ii;
+    if (msg_idx) {
+      mrow = msg_idx[ii];
+      kok = kok && mrow < n_msg;
+      if (mrow >= n_msg) mrow = 0;
+    }
     s_ok = sc_lt_L(s);
     sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
     uint32_t h[16], k[8];
@@ -329,7 +336,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #pragma unroll
     for (int t = 0; t < 16; ++t) h[t] = r[t & 7] ^ a[(t + 3) & 7];
 #else
-    sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * ii, (int)msg_len);
+    sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
 #endif
     sc_reduce512(k, h);
     // per-step entry index (128-B units from the step's table base) and sign
@@ -481,7 +488,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
-    const uint8_t** __restrict__ eaddr) {
+    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
   using ST = steps<PLB, PLA>;
   constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -533,10 +540,16 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
       const uint4 k0 = kp[0], k1 = kp[1];
       a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
     }
+    uint64_t mrow = ii;
+    if (msg_idx) {
+      mrow = msg_idx[ii];
+      kok = kok && mrow < n_msg;
+      if (mrow >= n_msg) mrow = 0;
+    }
     s_ok = sc_lt_L(s);
     sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
     uint32_t h[16], k[8];
-    sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * ii, (int)msg_len);
+    sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
     sc_reduce512(k, h);
     const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * PLA::TABLE_WORDS * 4;
     digits ds, dk;
@@ -921,7 +934,8 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
 // workspace halves, so the next launch's comb (on st) overlaps it.
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
-                         uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr) {
+                         uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
+                         const uint32_t* dMI = nullptr, uint32_t n_msg = 0) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
@@ -945,11 +959,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   const uint64_t Npad = blocks * BLOCK;
 #define PBFT_LAUNCH_COMB(LEN_, WA_)                                                                               \
   hipLaunchKernelGGL((comb_kernel<LEN_, WA_>), g, b, (BLOCK / 64) * COMB_LDS_PER_WAVE, st, dR, dS,             \
-                     (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx)
+                     (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Npad, c->d_tabB, c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, xyz, flags, eidx, dMI, n_msg)
 #define PBFT_LAUNCH_SPLIT(LEN_, WA_)                                                                           \
   hipLaunchKernelGGL((comb_latency_kernel<LEN_, WA_>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, st, dR, dS, \
                      (const uint8_t*)dK, rs_stride, k_stride, dM, msg_len, msg_stride, N, Lpad, c->d_tabB,           \
-                     c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, dB, (const uint8_t**)eidx)
+                     c->d_tabA, c->d_keys, c->d_key_ok, c->n_keys, dB, (const uint8_t**)eidx, dMI, n_msg)
   const bool latency_mode = N < c->split_below;
   if (latency_mode) {
     // enough blocks for every u16 piece of the ceil(N/64) bitmap words (>= ceil(N / LAT_SIGS))
@@ -1077,6 +1091,50 @@ static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
     rc = launch_verify(c, base, base + L.offS, (const uint16_t*)(base + L.offK), base + L.offM, msg_len, msg_stride,
                        n, c->d_bitmap + lo / 64, c->stream);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
+  }
+  return PBFT_OK;
+}
+
+// Votes form (include/pbft_verify.h pbft_verify_votes): R, S, key_idx and a 4-byte envelope index per
+// signature (70 B instead of 151 B over PCIe) + the batch's table of distinct 85-byte envelopes.
+struct votes_layout {
+  size_t offS, offK, offI, bytes;
+  explicit votes_layout(uint64_t n) {
+    offS = 32 * n;
+    offK = 64 * n;
+    offI = (offK + 2 * n + 15) & ~(size_t)15;
+    bytes = (offI + 4 * n + 255) & ~(size_t)255;
+  }
+};
+
+static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K,
+                                  const uint32_t* IDX, const uint8_t* ENV, uint32_t n_env, uint64_t N) {
+  const uint64_t words = (N + 63) / 64;
+  const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
+  const uint64_t ch = N < PIPE_CHUNK ? N : PIPE_CHUNK;
+  const votes_layout L(ch);
+  int rc = ensure_stage(c, env_bytes + (N > PIPE_CHUNK ? 2 : 1) * L.bytes, words);
+  if (rc) return rc;
+  // envelope table first (copy stream), then each chunk's columns; the kernels of chunk c run on the context
+  // stream after its copies, overlapping the copies of chunk c+1
+  HIP_TRY(hipMemcpyAsync(c->d_stage, ENV, (size_t)PBFT_ENVELOPE_LEN * n_env, hipMemcpyHostToDevice, c->cstream));
+  uint64_t chunk = 0;
+  for (uint64_t lo = 0; lo < N; lo += PIPE_CHUNK, ++chunk) {
+    const uint64_t n = N - lo < PIPE_CHUNK ? N - lo : PIPE_CHUNK;
+    const int b = (int)(chunk & 1);
+    uint8_t* base = c->d_stage + env_bytes + (size_t)b * L.bytes;
+    if (chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
+    HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
+    rc = launch_verify(c, base, base + L.offS, (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN,
+                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, 32, 2, nullptr,
+                       (const uint32_t*)(base + L.offI), n_env);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
   }
@@ -1383,6 +1441,36 @@ int pbft_verify_batch_device_pipelined(pbft_ctx* c, const uint8_t* dR, const uin
   HIP_TRY(hipSetDevice(c->device));
   return launch_verify(c, dR, dS, dK, dM, msg_len, msg_stride, N, dB, (hipStream_t)stream, 32, 2,
                        (hipStream_t)finish_stream);
+}
+
+int pbft_verify_votes(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* env_idx,
+                      const uint8_t* envelopes, uint32_t n_env, uint64_t N, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (N && (!R || !S || !K || !env_idx || !out || !envelopes || n_env == 0))
+    return set_err(PBFT_EINVAL, "bad votes arguments");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  if (N == 0) return PBFT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = stage_votes_and_launch(c, R, S, K, env_idx, envelopes, n_env, N);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, (N + 63) / 64 * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memcpy(out, c->h_bitmap, (N + 63) / 64 * 8);
+  return PBFT_OK;
+}
+
+int pbft_verify_votes_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK,
+                             const uint32_t* d_env_idx, const uint8_t* d_envelopes, uint32_t n_env, uint64_t N,
+                             uint64_t* dB, void* stream) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (N && (!dR || !dS || !dK || !d_env_idx || !d_envelopes || !dB || n_env == 0))
+    return set_err(PBFT_EINVAL, "bad votes arguments");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  return launch_verify(c, dR, dS, dK, d_envelopes, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, N, dB, st, 32, 2, nullptr,
+                       d_env_idx, n_env);
 }
 
 // Binary wire records (include/pbft_wire.h): R at +0, S at +32, envelope at +64,

@@ -150,6 +150,25 @@ class GpuBatchVerifier:
         """Pre-size the workspace (required before capturing verify_device into a graph)."""
         check(self._lib.pbft_verify_reserve(self._ctx, max_n))
 
+    def verify_votes(self, R, S, key_idx, env_idx, envelopes) -> np.ndarray:
+        """pbft_verify_votes: signature i signs envelopes[env_idx[i]] (85 B each); returns bitmap words."""
+        R = np.ascontiguousarray(R, np.uint8).reshape(-1, 32)
+        S = np.ascontiguousarray(S, np.uint8).reshape(-1, 32)
+        K = np.ascontiguousarray(key_idx, np.uint16).reshape(-1)
+        I = np.ascontiguousarray(env_idx, np.uint32).reshape(-1)
+        E = np.ascontiguousarray(envelopes, np.uint8).reshape(-1, 85)
+        n = len(R)
+        if not (len(S) == len(K) == len(I) == n):
+            raise ValueError("R, S, key_idx, env_idx must have the same length")
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_votes(self._ctx, _ptr(R), _ptr(S), _ptr(K), _ptr(I), _ptr(E), len(E), n, _ptr(out)))
+        return out
+
+    def verify_votes_device(self, d_R: int, d_S: int, d_key_idx: int, d_env_idx: int, d_envelopes: int,
+                            n_env: int, n: int, d_bitmap: int, stream: int = 0) -> None:
+        check(self._lib.pbft_verify_votes_device(self._ctx, d_R, d_S, d_key_idx, d_env_idx, d_envelopes, n_env, n,
+                                                 d_bitmap, stream or None))
+
     def verify_records(self, records: np.ndarray) -> np.ndarray:
         """Blocking verify of (N, 160) binary wire records (include/pbft_wire.h); returns bitmap words."""
         rec = np.ascontiguousarray(records, dtype=np.uint8).reshape(-1, 160)
