@@ -153,6 +153,7 @@ def pmc_traffic(pb: int, pa: int, n: int) -> dict:
         return {"traffic_bytes_per_launch": d["traffic_bytes_per_launch"],
                 "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
                 "valu_insts_per_sig": d.get("valu_insts_per_sig_total"),
+                "valu_insts_per_sig_comb": d["comb_kernel"].get("valu_insts_per_sig"),
                 "source": f"profiles/{rnd}_pmc_comb/derived.json (PMC passes, not this run)"}
     return {}
 
@@ -561,6 +562,7 @@ def main():
                          "traffic_source": pmc.get("source"),
                          "valu_busy_pct": pmc.get("valu_busy_pct"),
                          "valu_insts_per_sig": pmc.get("valu_insts_per_sig"),
+                         "valu_insts_per_sig_comb": pmc.get("valu_insts_per_sig_comb"),
                          "gather_bytes_algorithmic": (gather_bytes_per_verify(pb, pa) + INPUT_BYTES) * n,
                          "kernel": (f"comb_kernel<85, plan PA={pa}> (PB={pb}) over this rank's shard (HIP events on "
                                     f"its stream; the finish runs on the second stream)") if pipelined else
