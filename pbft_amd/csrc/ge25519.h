@@ -1,8 +1,11 @@
 // Edwards25519 group operations for gfx950 (twisted Edwards, a = -1).
 //
 // Points live in extended coordinates (X:Y:Z:T), x = X/Z, y = Y/Z, xy = T/Z
-// (40 VGPRs).  Table entries are affine Niels triples (y+x, y-x, 2d*x*y), fully
-// reduced, so a comb step is the 7-multiply mixed addition below.  The unified
+// (40 VGPRs).  Table entries are HALVED affine Niels triples ((y+x)/2, (y-x)/2,
+// d*x*y), fully reduced: the mixed addition (verify_core.h) then computes every
+// product at half the usual value and uses D = Z1 instead of 2*Z1, so its four
+// outputs are the usual ones / 4 -- the same projective point, without the
+// doubling of Z1 in every comb step.  The unified
 // formulas are complete for a = -1 and non-square d, so torsion components
 // (mixed-order keys, small-order R) need no special casing -- the same property
 // curve25519-dalek 3.2.1 relies on (Cargo.lock:604-614).
@@ -12,7 +15,7 @@
 namespace pbft {
 
 struct ge { fe X, Y, Z, T; };
-struct niels { fe ypx, ymx, xy2d; };
+struct niels { fe hpx, hmx, dxy; };  // (y+x)/2, (y-x)/2, d*x*y
 
 // 2*d and d in radix 2^25.5 (canonical)
 FE_FN void fe_const_d(fe& h) {
@@ -31,8 +34,15 @@ FE_FN void fe_const_sqrtm1(fe& h) {
   fe_from_words(h, w);
 }
 
+// 1/2 = (p + 1) / 2 = 2^254 - 9
+FE_FN void fe_const_half(fe& h) {
+  const uint32_t w[8] = {0xfffffff7u, 0xffffffffu, 0xffffffffu, 0xffffffffu,
+                         0xffffffffu, 0xffffffffu, 0xffffffffu, 0x3fffffffu};
+  fe_from_words(h, w);
+}
+
 FE_FN void ge_identity(ge& p) { fe_zero(p.X); fe_one(p.Y); fe_one(p.Z); fe_zero(p.T); }
-FE_FN void niels_identity(niels& n) { fe_one(n.ypx); fe_one(n.ymx); fe_zero(n.xy2d); }
+FE_FN void niels_identity(niels& n) { fe_const_half(n.hpx); fe_const_half(n.hmx); fe_zero(n.dxy); }
 
 // r = p + q, both extended (8 multiplies; used in table precomputation)
 FE_FN void ge_add(ge& r, const ge& p, const ge& q) {
@@ -112,22 +122,31 @@ FE_FN bool ge_decompress(ge& p, const uint32_t w[8]) {
   return correct || flipped;
 }
 
-// affine Niels form of p (one inversion), fully reduced limbs
+// Halved affine Niels entry of the affine point (x, y), every coordinate canonical
+// (so table limbs are minimal).
+FE_FN void niels_from_affine(niels& n, const fe& x, const fe& y) {
+  fe t, half, d;
+  fe_const_half(half);
+  fe_const_d(d);
+  fe_add(t, y, x);
+  fe_mul(n.hpx, t, half);
+  fe_sub(t, y, x);
+  fe_mul(n.hmx, t, half);
+  fe_mul(t, x, y);
+  fe_mul(n.dxy, t, d);
+  uint32_t w[8];
+  fe_to_words(w, n.hpx); fe_from_words(n.hpx, w);
+  fe_to_words(w, n.hmx); fe_from_words(n.hmx, w);
+  fe_to_words(w, n.dxy); fe_from_words(n.dxy, w);
+}
+
+// halved affine Niels form of p (one inversion)
 FE_FN void ge_to_niels(niels& n, const ge& p) {
-  fe zi, x, y, k;
+  fe zi, x, y;
   fe_invert(zi, p.Z);
   fe_mul(x, p.X, zi);
   fe_mul(y, p.Y, zi);
-  fe_add(n.ypx, y, x);
-  fe_sub(n.ymx, y, x);
-  fe_const_2d(k);
-  fe_mul(n.xy2d, x, y);
-  fe_mul(n.xy2d, n.xy2d, k);
-  // canonicalize every coordinate so table limbs are minimal
-  uint32_t w[8];
-  fe_to_words(w, n.ypx); fe_from_words(n.ypx, w);
-  fe_to_words(w, n.ymx); fe_from_words(n.ymx, w);
-  fe_to_words(w, n.xy2d); fe_from_words(n.xy2d, w);
+  niels_from_affine(n, x, y);
 }
 
 }  // namespace pbft

@@ -157,8 +157,6 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
   }
   fe inv;
   fe_invert_gcd(inv, pre[cnt - 1]);
-  fe k2d;
-  fe_const_2d(k2d);
   for (int t = (int)cnt - 1; t >= 0; --t) {
     fe zi;
     if (t > 0) { fe_mul(zi, inv, pre[t - 1]); fe_mul(inv, inv, Z[t]); } else { zi = inv; }
@@ -166,14 +164,7 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
     fe_mul(x, X[t], zi);
     fe_mul(y, Y[t], zi);
     niels n;
-    fe_add(n.ypx, y, x);
-    fe_sub(n.ymx, y, x);
-    fe_mul(n.xy2d, x, y);
-    fe_mul(n.xy2d, n.xy2d, k2d);
-    uint32_t w[8];
-    fe_to_words(w, n.ypx); fe_from_words(n.ypx, w);
-    fe_to_words(w, n.ymx); fe_from_words(n.ymx, w);
-    fe_to_words(w, n.xy2d); fe_from_words(n.xy2d, w);
+    niels_from_affine(n, x, y);
     store_niels(out + (size_t)(j0 + t) * 32, n);
   }
 }
@@ -282,6 +273,45 @@ __device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t id
   }
 }
 
+// 8-B LDS read from a 32-bit LDS byte address (ds_read_b64)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 lds_read8(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
+  return *(lds_u32x2*)(uintptr_t)addr;
+#else
+  (void)addr;
+  return u32x2{0, 0};
+#endif
+}
+
+// This lane's entry from its LDS slot (after the DMA landed: vmcnt(0); the ds_reads use integer LDS
+// addresses, so the compiler cannot see that they alias the DMA's writes -- hence the explicit wait), as
+// (qa, qb, k) for ge_madd_ab: the sign picks hmx/hpx by ADDRESS (entry layout, verify_core.h), so the swap
+// costs two XORs instead of 20 masked-select instructions.  Logical byte o of the entry sits at rd0 ^ o
+// (dma_entry_lines' chunk swizzle; o < 128, rd0 16-B aligned).
+__device__ __forceinline__ void lds_entry_signed(uint32_t rd0, bool neg, fe& qa, fe& qb, fe& k) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  asm volatile("" ::: "memory");
+  const uint32_t pos = neg ? 0u : 1u;
+  const uint32_t a0 = rd0 ^ (pos << 5);          // qa[0..7]: hmx (o = 32) or hpx (o = 0)
+  const uint32_t ah = rd0 ^ 64u ^ (pos << 3);    // qa[8..9]: o = 72 or 64
+  const u32x4 a_lo = lds_read16(a0), a_hi = lds_read16(a0 ^ 16u);
+  const u32x4 b_lo = lds_read16(a0 ^ 32u), b_hi = lds_read16(a0 ^ 48u);
+  const u32x2 a_top = lds_read8(ah), b_top = lds_read8(ah ^ 8u);
+  const u32x4 k0 = lds_read16(rd0 ^ 80u), k1 = lds_read16(rd0 ^ 96u);
+  const u32x2 k2 = lds_read8(rd0 ^ 112u);
+  qa.v[0] = a_lo.x; qa.v[1] = a_lo.y; qa.v[2] = a_lo.z; qa.v[3] = a_lo.w;
+  qa.v[4] = a_hi.x; qa.v[5] = a_hi.y; qa.v[6] = a_hi.z; qa.v[7] = a_hi.w;
+  qa.v[8] = a_top.x; qa.v[9] = a_top.y;
+  qb.v[0] = b_lo.x; qb.v[1] = b_lo.y; qb.v[2] = b_lo.z; qb.v[3] = b_lo.w;
+  qb.v[4] = b_hi.x; qb.v[5] = b_hi.y; qb.v[6] = b_hi.z; qb.v[7] = b_hi.w;
+  qb.v[8] = b_top.x; qb.v[9] = b_top.y;
+  k.v[0] = k0.x; k.v[1] = k0.y; k.v[2] = k0.z; k.v[3] = k0.w;
+  k.v[4] = k1.x; k.v[5] = k1.y; k.v[6] = k1.z; k.v[7] = k1.w;
+  k.v[8] = k2.x; k.v[9] = k2.y;
+}
+
 #ifndef PBFT_LAUNDER
 #define PBFT_LAUNDER 1
 #endif
@@ -363,49 +393,34 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   }
   const uint8_t* tB = (const uint8_t*)tabB;
   const uint8_t* tA = (const uint8_t*)tabA;
-  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // chunk c of my entry at rd0 ^ (16 c)
-  // this lane's entry from the LDS buffer (after its DMA landed: vmcnt(0)); the ds_reads use integer LDS
-  // addresses, so the compiler cannot see that they alias the DMA's writes -- hence the explicit wait
-  auto read_entry = [&](niels& q) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    asm volatile("" ::: "memory");
-    uint32_t w[32];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const u32x4 v = lds_read16(rd0 ^ (16u * c));
-      w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-    }
-#pragma unroll
-    for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
-  };
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // logical byte o of my entry at rd0 ^ o
   // (each lane re-reads only the indices it wrote itself: no barrier needed)
   dma_entry_lines(ST::is_a(0) ? tA : tB, eidx[i], lane, ebuf);
   uint32_t nidx = eidx[Npad + i];
   ge P;
   {
     // step 0: P = +-T_B[0][s_0] directly (1 multiplication instead of a 7-multiplication addition)
-    niels q;
-    read_entry(q);
+    fe qa, qb, k;
+    const bool neg = (uint32_t)sgn & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): entry in VGPRs before the DMA reuses the buffer
     dma_entry_lines(ST::is_a(1) ? tA : tB, nidx, lane, ebuf);
     nidx = eidx[2 * Npad + i];
-    ge_from_niels_signed(P, q, (uint32_t)sgn & 1u);
+    ge_from_ab(P, qa, qb, k, neg);
   }
-  for (int j = 1; j < ST::N; ++j) {
-    niels q;
-    read_entry(q);
-    if (j + 1 < ST::N) {
-      // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-      dma_entry_lines(ST::is_a(j + 1) ? tA : tB, nidx, lane, ebuf);
-      if (j + 2 < ST::N) nidx = eidx[(size_t)(j + 2) * Npad + i];
-    }
+  for (int j = 1; j < ST::N - 1; ++j) {
+    fe qa, qb, k;
     const bool neg = (uint32_t)(sgn >> j) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    dma_entry_lines(ST::is_a(j + 1) ? tA : tB, nidx, lane, ebuf);
+    if (j + 2 < ST::N) nidx = eidx[(size_t)(j + 2) * Npad + i];
 #if PBFT_ABL_NOMADD  // ablation: gathers only, no group arithmetic
 #pragma unroll
-    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= q.ypx.v[t]; P.Y.v[t] ^= q.ymx.v[t]; P.Z.v[t] += q.xy2d.v[t] + neg; }
+    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= qa.v[t]; P.Y.v[t] ^= qb.v[t]; P.Z.v[t] += k.v[t] + neg; }
 #else
-    ge_madd_signed(P, P, q, neg);
+    ge_madd_ab<true>(P, P, qa, qb, k, neg);
 #endif
 #if PBFT_LAUNDER
     // Keep the loop-carried limbs opaque 32-bit values: otherwise LLVM carries
@@ -416,6 +431,13 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
       asm("" : "+v"(P.X.v[t]), "+v"(P.Y.v[t]), "+v"(P.Z.v[t]), "+v"(P.T.v[t]));
     }
 #endif
+  }
+  {
+    // last step: R' needs X, Y, Z only (6 multiplications)
+    fe qa, qb, k;
+    const bool neg = (uint32_t)(sgn >> (ST::N - 1)) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    ge_madd_ab<false>(P, P, qa, qb, k, neg);
   }
   if (live) {
 #pragma unroll
@@ -575,39 +597,29 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     });
   }
   const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);
-  auto read_entry = [&](niels& q) {
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the DMA landed (integer LDS addresses, see comb_kernel)
-    asm volatile("" ::: "memory");
-    uint32_t w[32];
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const u32x4 v = lds_read16(rd0 ^ (16u * c));
-      w[4 * c] = v.x; w[4 * c + 1] = v.y; w[4 * c + 2] = v.z; w[4 * c + 3] = v.w;
-    }
-#pragma unroll
-    for (int t = 0; t < 10; ++t) { q.ypx.v[t] = w[t]; q.ymx.v[t] = w[10 + t]; q.xy2d.v[t] = w[20 + t]; }
-  };
   dma_entry_lines64(eaddr[g], lane, ebuf);
   const uint8_t* nadr = eaddr[Lpad + g];
   ge P;
   {
-    niels q;
-    read_entry(q);
+    fe qa, qb, k;
+    const bool neg = sgn & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     dma_entry_lines64(nadr, lane, ebuf);
     if (2 < T) nadr = eaddr[2 * Lpad + g];
-    ge_from_niels_signed(P, q, sgn & 1u);
+    ge_from_ab(P, qa, qb, k, neg);
   }
   for (int t = 1; t < T; ++t) {
-    niels q;
-    read_entry(q);
+    fe qa, qb, k;
+    const bool neg = (sgn >> t) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
     if (t + 1 < T) {
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
       dma_entry_lines64(nadr, lane, ebuf);
       if (t + 2 < T) nadr = eaddr[(size_t)(t + 2) * Lpad + g];
     }
 #if !PBFT_ABL_LAT_NOSTEPS  // ablation: gathers only (timing only)
-    ge_madd_signed(P, P, q, (sgn >> t) & 1u);
+    ge_madd_ab<true>(P, P, qa, qb, k, neg);
 #endif
 #pragma unroll
     for (int u = 0; u < 10; ++u) asm("" : "+v"(P.X.v[u]), "+v"(P.Y.v[u]), "+v"(P.Z.v[u]), "+v"(P.T.v[u]));

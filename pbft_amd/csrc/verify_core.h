@@ -55,10 +55,24 @@ struct comb : plan<(254 + W - 1) / W, W, 0> {
   static constexpr uint32_t E = (1u << (W - 1)) + 1u;
 };
 
+// Table entry layout (128 B = 32 words), arranged so that the comb kernels can
+// pick (hmx, hpx) or (hpx, hmx) -- the entry or its negation -- by LDS address:
+//   words  0..7  hpx[0..7]     words  8..15 hmx[0..7]
+//   words 16..17 hpx[8..9]     words 18..19 hmx[8..9]
+//   words 20..29 dxy[0..9]     words 30..31 zero
+// i.e. hpx and hmx start 32 B apart (low 8 limbs) and 8 B apart (top 2 limbs).
+__host__ __device__ constexpr int hpx_word(int i) { return i < 8 ? i : 8 + i; }
+__host__ __device__ constexpr int hmx_word(int i) { return i < 8 ? 8 + i : 10 + i; }
+
 FE_FN void store_niels(uint32_t* dst, const niels& n) {
 #pragma unroll
-  for (int i = 0; i < 10; ++i) { dst[i] = n.ypx.v[i]; dst[10 + i] = n.ymx.v[i]; dst[20 + i] = n.xy2d.v[i]; }
+  for (int i = 0; i < 10; ++i) { dst[hpx_word(i)] = n.hpx.v[i]; dst[hmx_word(i)] = n.hmx.v[i]; dst[20 + i] = n.dxy.v[i]; }
   dst[30] = 0; dst[31] = 0;
+}
+
+FE_FN void niels_from_entry_words(niels& n, const uint32_t w[32]) {
+#pragma unroll
+  for (int i = 0; i < 10; ++i) { n.hpx.v[i] = w[hpx_word(i)]; n.hmx.v[i] = w[hmx_word(i)]; n.dxy.v[i] = w[20 + i]; }
 }
 
 FE_FN void load_niels(niels& n, const uint32_t* src) {
@@ -70,11 +84,9 @@ FE_FN void load_niels(niels& n, const uint32_t* src) {
     const uint4 v = s4[q];
     w[4 * q] = v.x; w[4 * q + 1] = v.y; w[4 * q + 2] = v.z; w[4 * q + 3] = v.w;
   }
-#pragma unroll
-  for (int i = 0; i < 10; ++i) { n.ypx.v[i] = w[i]; n.ymx.v[i] = w[10 + i]; n.xy2d.v[i] = w[20 + i]; }
+  niels_from_entry_words(n, w);
 #else
-#pragma unroll
-  for (int i = 0; i < 10; ++i) { n.ypx.v[i] = src[i]; n.ymx.v[i] = src[10 + i]; n.xy2d.v[i] = src[20 + i]; }
+  niels_from_entry_words(n, src);
 #endif
 }
 
@@ -100,63 +112,75 @@ FE_FN uint32_t lane_mask(bool c) {
   return m;
 }
 
-// r = p + sign * q  (sign from neg), 7 multiplies + masked swaps
-FE_FN void ge_madd_signed(ge& r, const ge& p, const niels& q, bool neg) {
-  fe a, b, c, d, t, qa, qb;
+// r = p + sign * q for a halved affine Niels entry q given as (qa, qb, k):
+// (hmx, hpx, dxy) for a positive digit, (hpx, hmx, dxy) for a negative one
+// (-q = (-x, y) swaps y+x and y-x and negates d*x*y; the comb kernels select qa
+// and qb by LDS address).  7 multiplies (6 without T3, for the last step):
+//   a = (Y-X) qa, b = (Y+X) qb, c = T k, D = Z  (each half its usual value)
+//   E = b - a, F = D -+ c, G = D +- c, H = b + a
+//   X3 = E F, Y3 = G H, Z3 = F G, T3 = E H  (= the usual outputs / 4)
+template <bool WITH_T = true>
+FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& k, bool neg) {
+  fe a, b, c, t;
   const uint32_t m = lane_mask(neg);
-  qa = q.ymx;
-  qb = q.ypx;
-  fe_cswap_mask(qa, qb, m);
   fe_sub(t, p.Y, p.X);
   fe_mul(a, t, qa);
   fe_add(t, p.Y, p.X);
   fe_mul(b, t, qb);
-  fe_mul(c, p.T, q.xy2d);
-  fe_add(d, p.Z, p.Z);
+  fe_mul(c, p.T, k);
   fe e, f, g, h, dmc, dpc;
   fe_sub(e, b, a);
-  fe_sub(dmc, d, c);
-  fe_add(dpc, d, c);
+  fe_sub(dmc, p.Z, c);
+  fe_add(dpc, p.Z, c);
   f = dmc;
   g = dpc;
   fe_cswap_mask(f, g, m);
   fe_add(h, b, a);
-  // Operand order keeps the 19-premultiplied (second) operand below 2^27.3 for
-  // either sign: d - c (up to 2^28) is always a first operand.  Z3 = F*G is
-  // dmc*dpc whatever the sign.  Checked by tools/limb_bounds.py.
+  // Operand order keeps the 19-premultiplied (second) operand within u32 for
+  // either sign: D - c is always a first operand.  Z3 = F*G is dmc*dpc whatever
+  // the sign.  Checked by tools/limb_bounds.py.
   fe_mul(r.X, f, e);
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, dmc, dpc);
-  fe_mul(r.T, e, h);
+  if constexpr (WITH_T) fe_mul(r.T, e, h);
 }
 
-// P = +-Q for an affine Niels entry Q = (y+x, y-x, 2dxy), as the extended
-// point (2x : 2y : 2 : 2xy) -- the first comb step costs one multiplication
-// (2xy = 2dxy / d) instead of the 7 of a mixed addition to the identity.
-// -Q = (-x, y) swaps y+x and y-x and negates 2xy.  The identity entry
-// (1, 1, 0) gives (0 : 2 : 2 : 0).  Every output limb vector is carried.
+// r = p + sign * q, entry q as stored (the swap by masks)
+FE_FN void ge_madd_signed(ge& r, const ge& p, const niels& q, bool neg) {
+  fe qa = q.hmx, qb = q.hpx;
+  fe_cswap_mask(qa, qb, lane_mask(neg));
+  ge_madd_ab<true>(r, p, qa, qb, q.dxy, neg);
+}
+
+// P = +-q for a halved affine Niels entry given as (qa, qb, k) (see ge_madd_ab),
+// as the extended point (x : y : 1 : xy) -- the first comb step costs one
+// multiplication (xy = dxy / d) instead of the 7 of a mixed addition to the
+// identity.  -q = (-x, y).  The identity entry (1/2, 1/2, 0) gives (0 : 1 : 1 : 0).
+// Every output limb vector is carried.
 FE_FN void fe_const_dinv(fe& h) {
   const uint32_t w[8] = {0xcdc9f843u, 0x25e0f276u, 0x4279542eu, 0x0b5dd698u,
                          0xcdb9cf66u, 0x2b162114u, 0x14d5ce43u, 0x40907ed2u};
   fe_from_words(h, w);
 }
-FE_FN void ge_from_niels_signed(ge& P, const niels& q, bool neg) {
+FE_FN void ge_from_ab(ge& P, const fe& qa, const fe& qb, const fe& k, bool neg) {
   const uint32_t m = lane_mask(neg);
-  fe a = q.ypx, b = q.ymx;
-  fe_cswap_mask(a, b, m);
-  fe_sub(P.X, a, b);  // 2x (table limbs are canonical, so b is carried)
-  fe_add(P.Y, a, b);  // 2y
+  fe_sub(P.X, qb, qa);  // +-x (table limbs are canonical, so qa is carried)
+  fe_add(P.Y, qa, qb);  // y
   fe_carry(P.X);
   fe_carry(P.Y);
   fe dinv, t, nt;
   fe_const_dinv(dinv);
-  fe_mul(t, q.xy2d, dinv);  // 2xy
+  fe_mul(t, k, dinv);  // xy
   fe_neg(nt, t);
   fe_carry(nt);
 #pragma unroll
   for (int i = 0; i < 10; ++i) P.T.v[i] = (t.v[i] & ~m) | (nt.v[i] & m);
-  fe_zero(P.Z);
-  P.Z.v[0] = 2;
+  fe_one(P.Z);
+}
+FE_FN void ge_from_niels_signed(ge& P, const niels& q, bool neg) {
+  fe qa = q.hmx, qb = q.hpx;
+  fe_cswap_mask(qa, qb, lane_mask(neg));
+  ge_from_ab(P, qa, qb, q.dxy, neg);
 }
 
 // Signed-digit stream over a scalar < 2^253 held in 8 words, one window at a

@@ -87,10 +87,21 @@ void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   bytes_from_words(out, wo);
 }
 
-void hh_sha512_ram(const uint8_t* r, const uint8_t* a, const uint8_t* m, int len, uint8_t* out64) {
+// fixed_len: use the compile-time-length specialisation (constant padding words, peeled last block) the
+// kernels instantiate, for the lengths listed; otherwise the runtime-length form
+void hh_sha512_ram(const uint8_t* r, const uint8_t* a, const uint8_t* m, int len, uint8_t* out64, int fixed_len) {
   uint32_t wr[8], wa[8], h[16];
   words_from_bytes(wr, r); words_from_bytes(wa, a);
-  sha512_ram<-1>(h, wr, wa, m, len);
+  switch (fixed_len ? len : -1) {
+    case 0: sha512_ram<0>(h, wr, wa, m, len); break;
+    case 47: sha512_ram<47>(h, wr, wa, m, len); break;
+    case 48: sha512_ram<48>(h, wr, wa, m, len); break;
+    case 85: sha512_ram<85>(h, wr, wa, m, len); break;
+    case 111: sha512_ram<111>(h, wr, wa, m, len); break;
+    case 112: sha512_ram<112>(h, wr, wa, m, len); break;
+    case 240: sha512_ram<240>(h, wr, wa, m, len); break;
+    default: sha512_ram<-1>(h, wr, wa, m, len);
+  }
   for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
 }
 
@@ -252,7 +263,7 @@ extern "C" int hh_guard_verify(const uint8_t* key, const uint8_t* R, const uint8
         const int ad = d < 0 ? -d : d;
         niels q;
         load_niels(q, gB.p + ((size_t)PLAN_H::offset(j) + ad) * 32);
-        sink ^= q.ypx.v[0];
+        sink ^= q.hpx.v[0];
       });
       accept[i] = 0;
     } else {

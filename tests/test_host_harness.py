@@ -85,8 +85,9 @@ def test_sha512_ram(hh, ln):
     r, a, m = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(ln)
     buf = m + bytes(16)
     out = ctypes.create_string_buffer(64)
-    hh.hh_sha512_ram(r, a, buf, ln, out)
-    assert out.raw == hashlib.sha512(r + a + m).digest()
+    for fixed in (0, 1):  # runtime length, and the compile-time specialisation (padding folded, last block peeled)
+        hh.hh_sha512_ram(r, a, buf, ln, out, fixed)
+        assert out.raw == hashlib.sha512(r + a + m).digest(), fixed
 
 
 def test_reduce512(hh):

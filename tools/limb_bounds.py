@@ -37,11 +37,11 @@ def mulmax(f, g):
     return math.log2(worst)
 
 C = CARRIED
-# mixed add (comb step): P3 + affine Niels (ypx, ymx, xy2d) with canonical table limbs
+# mixed add (comb step): P3 + halved affine Niels ((y+x)/2, (y-x)/2, dxy) with canonical table limbs
 ymx = sub(C, C, P2); ypx = add(C, C)
 print("madd a=(Y-X)*ymx   log2 max col:", mulmax(ymx, C))
 print("madd b=(Y+X)*ypx   log2 max col:", mulmax(ypx, C))
-d = add(C, C)
+d = C   # D = Z1: halved table entries (ge25519.h), no doubling of Z1
 e = sub(C, C, P2); f = sub(d, C, P2); g = add(d, C); h = add(C, C)
 # operand order as coded in ge25519.h: the second operand is the one premultiplied by 19
 for neg in (False, True):
