@@ -116,6 +116,19 @@ FE_FN void fe_reduce_par(fe& h, uint64_t c[10]) {
   for (int k = 1; k < 10; ++k) h.v[k] = l[k] + r[k - 1];
 }
 
+// 2x as an addition: v_add_u32_e32 issues at ~2.2 cycles per wave64 on gfx950,
+// the v_lshlrev_b32 LLVM canonicalises x + x into at ~4.0
+// (tools/microbench/valu_mix2.hip, profiles/r02_valu_mix2.txt).
+FE_FN uint32_t dbl32(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t r;
+  asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return 2u * x;
+#endif
+}
+
 // Operand-scanning order: the 10 column accumulators are updated round-robin,
 // so consecutive v_mad_u64_u32 never depend on each other (10-way ILP per lane;
 // the dependent-mad latency is ~17 cycles on gfx950, tools/microbench/mad_latency.hip).
@@ -124,7 +137,7 @@ FE_FN void fe_mul_cols(uint64_t acc[10], const fe& f, const fe& g) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
     g19[i] = 19u * g.v[i];
-    fx[i] = (i & 1) ? 2u * f.v[i] : f.v[i];
+    fx[i] = (i & 1) ? dbl32(f.v[i]) : f.v[i];
   }
 #pragma unroll
   for (int k = 0; k < 10; ++k) acc[k] = MUL64(f.v[0], g.v[k]);
