@@ -31,14 +31,21 @@ fn main() {
             .arg(host.join(format!("{}.cpp", name))));
         objs.push(obj);
     }
-    // HIP kernels + C ABI, gfx950 code objects only (no dual paths, no other targets)
+    // HIP kernels + C ABI, gfx950 code objects only (no dual paths, no other targets): one object per
+    // source (the four key plans' verify kernels are separate units), then one -shared link
+    let hip_sources = ["pbft_verify.hip", "tables.hip", "finish.hip", "sign.hip", "comb_pa13.hip", "comb_pa14.hip", "comb_pa16.hip", "comb_pa32.hip"];
+    for name in hip_sources.iter() {
+        let obj = out.join(name.replace(".hip", ".o"));
+        run(Command::new(&hipcc)
+            .args(&["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-c", "-o"])
+            .arg(&obj)
+            .arg(src.join("pbft_amd/csrc").join(name)));
+        objs.insert(0, obj);
+    }
     let lib = out.join("libpbft_verify.so");
     run(Command::new(&hipcc)
-        .args(&["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-o"])
+        .args(&["--offload-arch=gfx950", "-fPIC", "-shared", "-o"])
         .arg(&lib)
-        .arg(src.join("pbft_amd/csrc/pbft_verify.hip"))
-        .arg("-x")
-        .arg("none")
         .args(&objs));
 
     println!("cargo:rustc-link-search=native={}", out.display());
@@ -46,9 +53,10 @@ fn main() {
     println!("cargo:rustc-link-search=native={}/lib", rocm);
     println!("cargo:rustc-link-lib=dylib=amdhip64");
     println!("cargo:rustc-link-arg=-Wl,-rpath,{}", out.display());
-    for f in ["pbft_amd/csrc/pbft_verify.hip", "pbft_amd/csrc/host/replica.cpp", "pbft_amd/csrc/host/wire.cpp",
+    for f in ["pbft_amd/csrc/pbft_verify.hip", "pbft_amd/csrc/verify_kernels.h", "pbft_amd/csrc/host/replica.cpp", "pbft_amd/csrc/host/wire.cpp",
               "include/pbft_verify.h", "include/pbft_replica.h", "include/pbft_wire.h"].iter() {
         println!("cargo:rerun-if-changed={}", src.join(f).display());
     }
+    println!("cargo:rerun-if-changed={}", src.join("pbft_amd/csrc").display());
     println!("cargo:rerun-if-env-changed=PBFT_SRC");
 }

@@ -1,0 +1,5 @@
+// comb_kernel / comb_latency_kernel instantiated for key plan PLA_MID (16 positions):
+// one translation unit per plan so that the verify kernels compile in parallel.
+#include "verify_kernels.h"
+
+hipError_t launch_comb_mid(const comb_launch_args& a) { return launch_comb_plan<PLA_MID>(a); }

@@ -1,0 +1,111 @@
+// Batch-inversion finish of the one-lane-per-signature verify (comb_kernel ->
+// finish_kernel), its own translation unit.
+#include "verify_kernels.h"
+
+__device__ __forceinline__ void load_fe(fe& f, const uint32_t* __restrict__ base, uint64_t N, uint64_t i) {
+#pragma unroll
+  for (int t = 0; t < 10; ++t) f.v[t] = base[(size_t)t * N + i];
+}
+
+// Compile-time unrolled helpers (keep the prefix-product array in VGPRs: a
+// runtime-indexed array would be placed in scratch, cdna guide §5.4 rule 20).
+template <int M>
+struct fin_unroll {
+  template <class F>
+  __device__ static __forceinline__ void up(F&& f) {
+    fin_unroll<M - 1>::up(f);
+    f(std::integral_constant<int, M - 1>());
+  }
+  template <class F>
+  __device__ static __forceinline__ void down(F&& f) {
+    f(std::integral_constant<int, M - 1>());
+    fin_unroll<M - 1>::down(f);
+  }
+};
+template <>
+struct fin_unroll<0> {
+  template <class F>
+  __device__ static __forceinline__ void up(F&&) {}
+  template <class F>
+  __device__ static __forceinline__ void down(F&&) {}
+};
+
+// M signatures per lane: lane l of wave w handles i = (w * M + m) * 64 + l.
+// M = FIN_M (16) for large rounds; small batches use fewer signatures per lane
+// so that more waves share the latency-bound inversion chains (launch_verify).
+template <int FM>
+__global__ void __launch_bounds__(BLOCK, FIN_WAVES_PER_EU) finish_kernel(const uint8_t* __restrict__ R,
+                                                       uint32_t rs_stride,
+                                                       const uint32_t* __restrict__ xyz,
+                                                       const uint8_t* __restrict__ flags, uint64_t N,
+                                                       uint64_t* __restrict__ bitmap) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
+  const uint64_t base = wave * FM * 64 + lane;
+  if (wave * FM * 64 >= N) return;
+  const uint32_t* Xb = xyz;
+  const uint32_t* Yb = xyz + 10 * N;
+  const uint32_t* Zb = xyz + 20 * N;
+  // prefix products of Z (lanes past N contribute 1)
+  fe pre[FM];
+  fin_unroll<FM>::up([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    const uint64_t i = base + (uint64_t)m * 64;
+    fe z;
+    if (i < N) load_fe(z, Zb, N, i); else fe_one(z);
+    if constexpr (m == 0) pre[0] = z;
+    else fe_mul(pre[m], pre[m - 1], z);
+  });
+  fe inv;
+#if PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
+  fe_invert<true>(inv, pre[FM - 1]);
+#else
+  fe_invert_gcd(inv, pre[FM - 1]);  // divsteps: ~19k instructions instead of ~44k on the serial chain
+#endif
+  fin_unroll<FM>::down([&](auto mc) {
+    constexpr int m = decltype(mc)::value;
+    const uint64_t i = base + (uint64_t)m * 64;
+    const bool live = i < N;
+    const uint64_t ii = live ? i : 0;
+    fe zi;
+    if constexpr (m > 0) {
+      fe_mul(zi, inv, pre[m - 1]);   // 1 / Z_m
+      fe z;
+      if (live) load_fe(z, Zb, N, ii); else fe_one(z);
+      fe_mul(inv, inv, z);           // 1 / (Z_0 ... Z_{m-1})
+    } else {
+      zi = inv;
+    }
+    fe X, Y, x, y;
+    load_fe(X, Xb, N, ii);
+    load_fe(Y, Yb, N, ii);
+    fe_mul(x, X, zi);
+    fe_mul(y, Y, zi);
+    uint32_t xw[8], yw[8], r[8], ry[8];
+    fe_to_words(xw, x);
+    fe_to_words(yw, y);
+    load32(r, R + (size_t)rs_stride * ii);
+    canon_y(ry, r);
+    bool eq = (xw[0] & 1u) == (r[7] >> 31);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) eq = eq && yw[t] == ry[t];
+    const bool ok = live && flags[ii] && eq && !y_is_small_order(yw);
+    const uint64_t vote = __ballot(ok);
+    if (lane == 0 && live) bitmap[(wave * FM + m)] = vote;
+  });
+}
+
+
+hipError_t launch_finish(int fm, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz, const uint8_t* flags,
+                         uint64_t N, uint64_t* bitmap, hipStream_t st) {
+#define PBFT_LAUNCH_FIN(M_)                                                                                 \
+  hipLaunchKernelGGL(finish_kernel<M_>, dim3((unsigned)((((N + 64 * M_ - 1) / (64 * M_)) * 64 + BLOCK - 1) / \
+                                                        BLOCK)),                                           \
+                     dim3(BLOCK), 0, st, R, rs_stride, xyz, flags, N, bitmap)
+  if (fm == FIN_M) PBFT_LAUNCH_FIN(FIN_M);
+  else if (fm == 8) PBFT_LAUNCH_FIN(8);
+  else if (fm == 4) PBFT_LAUNCH_FIN(4);
+  else PBFT_LAUNCH_FIN(1);
+#undef PBFT_LAUNCH_FIN
+  return hipGetLastError();
+}

@@ -1,0 +1,595 @@
+// Verify kernels of the MI355X batch verifier (comb_kernel, comb_latency_kernel)
+// and their per-plan launchers.  Each key plan's kernels are instantiated in
+// their own translation unit (comb_pa13.hip, comb_pa14.hip, comb_pa16.hip,
+// comb_pa32.hip) so that the four compile in parallel; pbft_verify.hip holds
+// the finish, signing, digest and table kernels and the C ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "verify_core.h"
+
+using namespace pbft;
+
+
+#define PBFT_ENVELOPE_LEN 85
+#define BLOCK 256
+// Comb plans (verify_core.h `plan`): balanced windows over the 254 bits of a
+// signed-digit scalar < 2^253, i.e. the fewest positions (= comb steps) for the
+// HBM they take.  Base point: 10 positions (4 x 26 + 6 x 25 bits), 235M entries
+// x 128 B = 30 GB, one copy per device shared by all contexts.  Replica keys:
+// the widest plan whose tables fit the key-table budget (default 70 % of the
+// free HBM, ~180 GB on MI355X; PBFT_OPT_KEY_TABLE_BUDGET_MB): 13 positions
+// (7 x 20 + 6 x 19 bits, 671 MB per key: n <= 268), 14 (2 x 19 + 12 x 18,
+// 268 MB), 16 (14 x 16 + 2 x 15, 63 MB), else 32 (30 x 8 + 2 x 7, 0.5 MB).
+// 23 steps per signature at n = 256.  DESIGN.md §3-4; measured in
+// profiles/r01_ab_log.md, profiles/r02_ab_log.md.
+#ifndef PBFT_PLAN_B
+#define PBFT_PLAN_B 10, 25, 4
+#endif
+#ifndef PBFT_PLAN_A
+#define PBFT_PLAN_A 14, 18, 2
+#endif
+using PLB = plan<PBFT_PLAN_B>;
+using PLA_HUGE = plan<13, 19, 7>;  // 7 x 20 + 6 x 19 bits: 671 MB per key (n = 256: 172 GB)
+using PLA_BIG = plan<PBFT_PLAN_A>;
+using PLA_MID = plan<16, 15, 14>;
+using PLA_SMALL = plan<32, 7, 30>;
+static_assert(PLA_HUGE::P < PLA_BIG::P && PLA_BIG::P < PLA_MID::P && PLA_MID::P < PLA_SMALL::P,
+              "key plans are told apart by P");
+
+__device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
+  const uint4* q = (const uint4*)p;
+  const uint4 a = q[0], b = q[1];
+  w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+  w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+}
+
+// ---- verify, device form ----------------------------------------------------
+// Same arithmetic as verify_lane (verify_core.h), split into two kernels by
+// register footprint:
+//
+//  comb_kernel   (one signature per lane, <= 128 VGPRs, 8 KB LDS per wave:
+//                 4 waves per SIMD)
+//    k = SHA-512(R || A || M) mod L; s < L; signed radix-2^W digits of s and k
+//    turned into one table-entry index per comb step (stored [step][Npad] in
+//    the HBM workspace, coalesced) plus a 32-bit sign mask held in a VGPR;
+//    R' = sum_i T_B[i][s_i] + T_{-A}[i][k_i], every step's 128-B table entry
+//    gathered one step AHEAD by line-coalesced LDS-DMA (dma_entry_lines), so
+//    the random HBM gathers hide under the previous mixed addition.  Writes
+//    R' = (X:Y:Z) limb-major ([limb][N], coalesced) and one flag byte
+//    (s < L and key usable).
+//  finish_kernel (M = FIN_M signatures per lane, small footprint)
+//    Montgomery batch inversion of the M Z's (1 inversion + 3(M-1) muls
+//    instead of M inversions), affine x, y, canonical compare with R,
+//    small-order test on y, ballot -> one bitmap word per (wave, m).
+//
+// Step order of the comb: B_0, A_0, B_1, A_1, ... while both scalars have
+// positions, then the remaining positions of the longer one.
+typedef __attribute__((address_space(3))) void lds_void;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+// 16-B LDS read from a 32-bit LDS byte address (ds_read_b128)
+__device__ __forceinline__ u32x4 lds_read16(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) const u32x4 lds_u32x4;
+  return *(lds_u32x4*)(uintptr_t)addr;
+#else
+  (void)addr;
+  return u32x4{0, 0, 0, 0};
+#endif
+}
+#ifndef FIN_M
+#define FIN_M 16
+#endif
+#ifndef FIN_WAVES_PER_EU
+#define FIN_WAVES_PER_EU 1
+#endif
+
+template <class PLB_, class PLA_>
+struct steps {
+  static constexpr int PB = PLB_::P, PA = PLA_::P;
+  static constexpr int PMIN = PB < PA ? PB : PA;
+  static constexpr int N = PB + PA;
+  static_assert(N <= 64, "sign mask holds one bit per step");
+  using mask_t = typename std::conditional<(N <= 32), uint32_t, uint64_t>::type;
+  // table and position of step j (wave-uniform)
+  __host__ __device__ static constexpr bool is_a(int j) { return j < 2 * PMIN ? (j & 1) : (PA > PB); }
+  __host__ __device__ static constexpr int pos(int j) { return j < 2 * PMIN ? (j >> 1) : j - PMIN; }
+};
+
+// Line-coalesced gather ("transposed" DMA).  A table entry is one 128-B line.
+// Lane-per-entry DMA (each lane fetching its own entry in 8 x 16 B) makes
+// every wave-instruction touch 64 different lines 16 B at a time, the access
+// shape the memory pipeline serves worst (profiles/r01_ab_log.md: the kernel
+// ran as fast without its arithmetic).  Here instruction q fetches the 8
+// entries of lanes 8q..8q+7 WHOLE: lane L reads 16-B chunk c = (L & 7) ^ (L >> 3)
+// of the entry of lane 8q + (L >> 3), so each instruction covers 8 full lines.
+// The DMA lands lane L of instruction q at LDS byte 1024 q + 16 L, i.e. entry e
+// occupies bytes [128 e, 128 e + 128) with chunk c at position c ^ (e & 7) --
+// the XOR swizzle spreads the owner lanes' ds_read_b128 over all banks.
+// idx (entry index in 128-B units from `base`) is fetched from its owner lane
+// with ds_bpermute (one base address + immediate offsets 32 q).
+__device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t idx, int lane, uint32_t ebuf_lds) {
+  const int k = lane >> 3;
+  const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
+  const int baddr = k << 2;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)idx);
+    __builtin_amdgcn_global_load_lds(base + (size_t)e * 128 + coff,
+                                     (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+  }
+}
+
+// 8-B LDS read from a 32-bit LDS byte address (ds_read_b64)
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 lds_read8(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(3))) const u32x2 lds_u32x2;
+  return *(lds_u32x2*)(uintptr_t)addr;
+#else
+  (void)addr;
+  return u32x2{0, 0};
+#endif
+}
+
+// This lane's entry from its LDS slot (after the DMA landed: vmcnt(0); the ds_reads use integer LDS
+// addresses, so the compiler cannot see that they alias the DMA's writes -- hence the explicit wait), as
+// (qa, qb, k) for ge_madd_ab: the sign picks hmx/hpx by ADDRESS (entry layout, verify_core.h), so the swap
+// costs two XORs instead of 20 masked-select instructions.  Logical byte o of the entry sits at rd0 ^ o
+// (dma_entry_lines' chunk swizzle; o < 128, rd0 16-B aligned).
+__device__ __forceinline__ void lds_entry_signed(uint32_t rd0, bool neg, fe& qa, fe& qb, fe& k) {
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  asm volatile("" ::: "memory");
+  const uint32_t pos = neg ? 0u : 1u;
+  const uint32_t a0 = rd0 ^ (pos << 5);          // qa[0..7]: hmx (o = 32) or hpx (o = 0)
+  const uint32_t ah = rd0 ^ 64u ^ (pos << 3);    // qa[8..9]: o = 72 or 64
+  const u32x4 a_lo = lds_read16(a0), a_hi = lds_read16(a0 ^ 16u);
+  const u32x4 b_lo = lds_read16(a0 ^ 32u), b_hi = lds_read16(a0 ^ 48u);
+  const u32x2 a_top = lds_read8(ah), b_top = lds_read8(ah ^ 8u);
+  const u32x4 k0 = lds_read16(rd0 ^ 80u), k1 = lds_read16(rd0 ^ 96u);
+  const u32x2 k2 = lds_read8(rd0 ^ 112u);
+  qa.v[0] = a_lo.x; qa.v[1] = a_lo.y; qa.v[2] = a_lo.z; qa.v[3] = a_lo.w;
+  qa.v[4] = a_hi.x; qa.v[5] = a_hi.y; qa.v[6] = a_hi.z; qa.v[7] = a_hi.w;
+  qa.v[8] = a_top.x; qa.v[9] = a_top.y;
+  qb.v[0] = b_lo.x; qb.v[1] = b_lo.y; qb.v[2] = b_lo.z; qb.v[3] = b_lo.w;
+  qb.v[4] = b_hi.x; qb.v[5] = b_hi.y; qb.v[6] = b_hi.z; qb.v[7] = b_hi.w;
+  qb.v[8] = b_top.x; qb.v[9] = b_top.y;
+  k.v[0] = k0.x; k.v[1] = k0.y; k.v[2] = k0.z; k.v[3] = k0.w;
+  k.v[4] = k1.x; k.v[5] = k1.y; k.v[6] = k1.z; k.v[7] = k1.w;
+  k.v[8] = k2.x; k.v[9] = k2.y;
+}
+
+#ifndef PBFT_LAUNDER
+#define PBFT_LAUNDER 1
+#endif
+#ifndef PBFT_COMB_WAVES_PER_EU
+#define PBFT_COMB_WAVES_PER_EU 4
+#endif
+static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
+
+template <int LEN, class PLA>
+__global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
+    uint32_t rs_stride, uint32_t k_stride,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
+    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
+    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
+  using ST = steps<PLB, PLA>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  // wave-uniform LDS base of this wave's entry buffer (SGPR: the DMA's M0)
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+  const uint64_t i = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;  // < Npad
+  const bool live = i < N;
+  const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
+  typename ST::mask_t sgn = 0;        // bit j: digit of step j is negative
+  bool s_ok, kok;
+  {
+    uint32_t r[8], s[8], a[8];
+    load32(r, R + (size_t)rs_stride * ii);
+    load32(s, S + (size_t)rs_stride * ii);
+    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
+    kok = ki < n_keys;
+    if (!kok) ki = 0;
+    kok = kok && key_ok[ki];
+    {
+      const uint4* kp = (const uint4*)(keys + 8 * ki);
+      const uint4 k0 = kp[0], k1 = kp[1];
+      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+    }
+    // the signed message: row ii, or the envelope table row msg_idx[ii] (votes form; out of range -> bit 0)
+    uint64_t mrow = ii;
+    if (msg_idx) {
+      mrow = msg_idx[ii];
+      kok = kok && mrow < n_msg;
+      if (mrow >= n_msg) mrow = 0;
+    }
+    s_ok = sc_lt_L(s);
+    sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
+    uint32_t h[16], k[8];
+#if PBFT_ABL_NOSHA  // ablation: no challenge hash (k from R and A directly)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) h[t] = r[t & 7] ^ a[(t + 3) & 7];
+#else
+    sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
+#endif
+    sc_reduce512(k, h);
+    // per-step entry index (128-B units from the step's table base) and sign
+    const uint32_t keybase = ki * PLA::ENTRIES;
+    digits ds, dk;
+    ds.init(s);
+    dk.init(k);
+    static_for<ST::N>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      constexpr bool isA = ST::is_a(j);
+      constexpr int pos = ST::pos(j);
+      int d;
+      if constexpr (isA) d = dk.template take_pos<PLA, pos>();
+      else d = ds.template take_pos<PLB, pos>();
+      const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+      sgn |= (typename ST::mask_t)(d < 0 ? 1u : 0u) << j;
+#if PBFT_ABL_FETCH0  // ablation: every lane gathers entry 1 of its position (L2-resident)
+      const uint32_t e = (isA ? PLA::offset(pos) : PLB::offset(pos)) + 1u;
+#else
+      const uint32_t e = isA ? keybase + PLA::offset(pos) + ad : PLB::offset(pos) + ad;
+#endif
+      eidx[(size_t)j * Npad + i] = e;
+    });
+  }
+  const uint8_t* tB = (const uint8_t*)tabB;
+  const uint8_t* tA = (const uint8_t*)tabA;
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // logical byte o of my entry at rd0 ^ o
+  // (each lane re-reads only the indices it wrote itself: no barrier needed)
+  dma_entry_lines(ST::is_a(0) ? tA : tB, eidx[i], lane, ebuf);
+  uint32_t nidx = eidx[Npad + i];
+  ge P;
+  {
+    // step 0: P = +-T_B[0][s_0] directly (1 multiplication instead of a 7-multiplication addition)
+    fe qa, qb, k;
+    const bool neg = (uint32_t)sgn & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): entry in VGPRs before the DMA reuses the buffer
+    dma_entry_lines(ST::is_a(1) ? tA : tB, nidx, lane, ebuf);
+    nidx = eidx[2 * Npad + i];
+    ge_from_ab(P, qa, qb, k, neg);
+  }
+  for (int j = 1; j < ST::N - 1; ++j) {
+    fe qa, qb, k;
+    const bool neg = (uint32_t)(sgn >> j) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    dma_entry_lines(ST::is_a(j + 1) ? tA : tB, nidx, lane, ebuf);
+    if (j + 2 < ST::N) nidx = eidx[(size_t)(j + 2) * Npad + i];
+#if PBFT_ABL_NOMADD  // ablation: gathers only, no group arithmetic
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { P.X.v[t] ^= qa.v[t]; P.Y.v[t] ^= qb.v[t]; P.Z.v[t] += k.v[t] + neg; }
+#else
+    ge_madd_ab<true>(P, P, qa, qb, k, neg);
+#endif
+#if PBFT_LAUNDER
+    // Keep the loop-carried limbs opaque 32-bit values: otherwise LLVM carries
+    // them as the i64 columns they were reduced from and every product with a
+    // P limb becomes a 64x32 multiply (2 mads + moves).
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      asm("" : "+v"(P.X.v[t]), "+v"(P.Y.v[t]), "+v"(P.Z.v[t]), "+v"(P.T.v[t]));
+    }
+#endif
+  }
+  {
+    // last step: R' needs X, Y, Z only (6 multiplications)
+    fe qa, qb, k;
+    const bool neg = (uint32_t)(sgn >> (ST::N - 1)) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    ge_madd_ab<false>(P, P, qa, qb, k, neg);
+  }
+  if (live) {
+#pragma unroll
+    for (int t = 0; t < 10; ++t) {
+      xyz[(size_t)t * N + i] = P.X.v[t];
+      xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
+      xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
+    }
+    flags[i] = (s_ok && kok) ? 1 : 0;
+  }
+}
+
+// ---- latency mode: small batches --------------------------------------------
+// For small batches (BASELINE config #5: 4096-signature rounds) one lane per
+// signature leaves most SIMDs idle, and the round's latency is one lane's
+// serial work: SHA-512, 24 comb steps, then the finish kernel's inversion.
+// comb_latency_kernel (blocks of 4 waves -- one per SIMD, so each may use the
+// whole register file -- and 64 signatures per block) instead
+//  * gives every signature SPLIT = 4 lanes: each lane computes the challenge
+//    hash itself (it is on the critical path anyway), then the steps
+//    j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a step in the
+//    last round add the identity entry), and the 4 partial points are summed
+//    with two shuffle + extended-addition rounds (every lane of the group then
+//    holds R');
+//  * R' is compressed with ONE divsteps inversion (inv25519.h, ~20 us on the
+//    chain) and compared with the canonical R encoding, as the finish kernel
+//    does; each wave writes 16 bitmap bits (u16 pieces: piece 4 * block + wave).
+// Round 1 instead decompressed R on a fourth wave in parallel (z^((p-5)/8):
+// 254 squarings on one wave, ~80 us -- the critical path); PBFT_LAT_DECOMP=1
+// keeps that variant for A/B.  ~2.5x lower latency than one lane per signature.
+#ifndef PBFT_LAT_DECOMP
+#define PBFT_LAT_DECOMP 0
+#endif
+static constexpr int SPLIT = 4;
+static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
+static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // signatures per block
+static constexpr int LAT_BLOCK = 4 * 64;                   // (PBFT_LAT_DECOMP: 3 comb waves + 1 decompression wave)
+#ifndef PBFT_SPLIT_BELOW
+#define PBFT_SPLIT_BELOW 12288  // measured crossover: 8,192 sigs 0.105 ms here vs 0.133 ms one-lane; 16,384: 0.195 vs 0.133
+#endif
+static constexpr uint64_t SPLIT_BELOW = PBFT_SPLIT_BELOW;  // batches below this use comb_latency_kernel
+static constexpr uint32_t LAT_LDS =
+    LAT_COMB_WAVES * COMB_LDS_PER_WAVE + (PBFT_LAT_DECOMP ? 21 * 64 * 4 : 0);  // entry buffers (+ x_R, y_R, ok)
+
+// Line-coalesced gather with per-lane 64-bit entry addresses (the split kernel's
+// lanes of one wave gather from both tables in the same step).
+__device__ __forceinline__ void dma_entry_lines64(const uint8_t* addr, int lane, uint32_t ebuf_lds) {
+  const int k = lane >> 3;
+  const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
+  const int baddr = k << 2;
+  const uint64_t a = (uint64_t)(uintptr_t)addr;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)a);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)(a >> 32));
+    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
+    __builtin_amdgcn_global_load_lds(src + coff, (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+  }
+}
+
+FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
+#pragma unroll
+  for (int t = 0; t < 10; ++t) out.v[t] = (uint32_t)__shfl_xor((int)in.v[t], mask);
+}
+
+template <int LEN, class PLA>
+__global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
+    uint32_t rs_stride, uint32_t k_stride,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
+    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
+    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
+  using ST = steps<PLB, PLA>;
+  constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+#if PBFT_LAT_DECOMP
+  uint32_t* rdec = (uint32_t*)(lds + LAT_COMB_WAVES * COMB_LDS_PER_WAVE);  // [21][64]: x_R, y_R limbs, ok
+  if (wave == LAT_COMB_WAVES) {
+    // ---- decompression wave: R of signature blockIdx * LAT_SIGS + lane (lanes >= LAT_SIGS idle)
+    const uint64_t i = (uint64_t)blockIdx.x * LAT_SIGS + lane;
+    const uint64_t ii = i < N ? i : 0;
+    uint32_t rr[8], ry[8];
+    load32(rr, R + (size_t)rs_stride * ii);
+    ge Rp;
+#if PBFT_ABL_LAT_NODEC  // ablation: no decompression (timing only)
+    bool ok = true;
+    fe_zero(Rp.X); fe_zero(Rp.Y);
+#else
+    bool ok = ge_decompress<true>(Rp, rr);  // dalek 3.2.1 CompressedEdwardsY::decompress (latency-oriented)
+#endif
+    canon_y(ry, rr);
+    ok = ok && !y_is_small_order(ry);  // small-order R (verify_strict)
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { rdec[t * 64 + lane] = Rp.X.v[t]; rdec[(10 + t) * 64 + lane] = Rp.Y.v[t]; }
+    rdec[20 * 64 + lane] = ok ? 1u : 0u;
+    __syncthreads();
+    return;
+  }
+#endif
+  // ---- comb waves: 16 signatures per wave, SPLIT lanes each
+  const uint64_t g = (uint64_t)blockIdx.x * (LAT_COMB_WAVES * 64) + threadIdx.x;  // global comb lane, < Lpad
+  const uint64_t i = g / SPLIT;
+  const int r = (int)(g % SPLIT);
+  const bool live = i < N;
+  const uint64_t ii = live ? i : 0;
+  uint32_t sgn = 0;  // bit t: digit of local step t is negative
+  bool s_ok, kok;
+  {
+    uint32_t rr[8], s[8], a[8];
+    load32(rr, R + (size_t)rs_stride * ii);
+    load32(s, S + (size_t)rs_stride * ii);
+    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
+    kok = ki < n_keys;
+    if (!kok) ki = 0;
+    kok = kok && key_ok[ki];
+    {
+      const uint4* kp = (const uint4*)(keys + 8 * ki);
+      const uint4 k0 = kp[0], k1 = kp[1];
+      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+    }
+    uint64_t mrow = ii;
+    if (msg_idx) {
+      mrow = msg_idx[ii];
+      kok = kok && mrow < n_msg;
+      if (mrow >= n_msg) mrow = 0;
+    }
+    s_ok = sc_lt_L(s);
+    sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
+    uint32_t h[16], k[8];
+    sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
+    sc_reduce512(k, h);
+    const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * PLA::TABLE_WORDS * 4;
+    digits ds, dk;
+    ds.init(s);
+    dk.init(k);
+    static_for<SPLIT * T>([&](auto jc) {
+      constexpr int j = decltype(jc)::value;
+      if constexpr (j < ST::N) {
+        constexpr bool isA = ST::is_a(j);
+        constexpr int pos = ST::pos(j);
+        int d;
+        if constexpr (isA) d = dk.template take_pos<PLA, pos>();
+        else d = ds.template take_pos<PLB, pos>();
+        if (j % SPLIT == r) {
+          const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+          sgn |= (d < 0 ? 1u : 0u) << (j / SPLIT);
+          eaddr[(size_t)(j / SPLIT) * Lpad + g] =
+              isA ? tA + ((size_t)PLA::offset(pos) + ad) * 128 : (const uint8_t*)tabB + ((size_t)PLB::offset(pos) + ad) * 128;
+        }
+      } else if (j % SPLIT == r) {
+        eaddr[(size_t)(j / SPLIT) * Lpad + g] = (const uint8_t*)tabB;  // entry 0 of position 0: the identity
+      }
+    });
+  }
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);
+  dma_entry_lines64(eaddr[g], lane, ebuf);
+  const uint8_t* nadr = eaddr[Lpad + g];
+  ge P;
+  {
+    fe qa, qb, k;
+    const bool neg = sgn & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    dma_entry_lines64(nadr, lane, ebuf);
+    if (2 < T) nadr = eaddr[2 * Lpad + g];
+    ge_from_ab(P, qa, qb, k, neg);
+  }
+  for (int t = 1; t < T; ++t) {
+    fe qa, qb, k;
+    const bool neg = (sgn >> t) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    if (t + 1 < T) {
+      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+      dma_entry_lines64(nadr, lane, ebuf);
+      if (t + 2 < T) nadr = eaddr[(size_t)(t + 2) * Lpad + g];
+    }
+#if !PBFT_ABL_LAT_NOSTEPS  // ablation: gathers only (timing only)
+    ge_madd_ab<true>(P, P, qa, qb, k, neg);
+#endif
+#pragma unroll
+    for (int u = 0; u < 10; ++u) asm("" : "+v"(P.X.v[u]), "+v"(P.Y.v[u]), "+v"(P.Z.v[u]), "+v"(P.T.v[u]));
+  }
+  // sum the SPLIT partial points: lanes r ^ 1, then r ^ 2 (extended addition, complete formulas)
+  static_assert(SPLIT == 4, "two combine rounds");
+  auto combine = [&](int m) {
+    ge Q, Sum;
+    fe_shfl_xor(Q.X, P.X, m); fe_shfl_xor(Q.Y, P.Y, m); fe_shfl_xor(Q.Z, P.Z, m); fe_shfl_xor(Q.T, P.T, m);
+    ge_add(Sum, P, Q);
+    P = Sum;
+  };
+  combine(1);
+  combine(2);
+  bool acc = false;
+#if PBFT_LAT_DECOMP
+  __syncthreads();  // x_R, y_R of the block's signatures are in LDS
+  if (r == 0 && live) {
+    const int l = (int)(threadIdx.x >> 2);  // signature within the block
+    fe xr, yr, t1, t2;
+#pragma unroll
+    for (int t = 0; t < 10; ++t) { xr.v[t] = rdec[t * 64 + l]; yr.v[t] = rdec[(10 + t) * 64 + l]; }
+    fe_mul(t1, xr, P.Z);
+    fe_mul(t2, yr, P.Z);
+    acc = rdec[20 * 64 + l] && s_ok && kok && fe_eq(P.X, t1) && fe_eq(P.Y, t2);
+  }
+#else
+  {
+    // compress R' (one divsteps inversion) and compare with the canonical R encoding (DESIGN.md "R check")
+    fe zi, x, y;
+    fe_invert_gcd(zi, P.Z);
+    fe_mul(x, P.X, zi);
+    fe_mul(y, P.Y, zi);
+    uint32_t xw[8], yw[8], rr[8], ry[8];
+    fe_to_words(xw, x);
+    fe_to_words(yw, y);
+    load32(rr, R + (size_t)rs_stride * ii);
+    canon_y(ry, rr);
+    bool eq = (xw[0] & 1u) == (rr[7] >> 31);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) eq = eq && yw[t] == ry[t];
+    acc = r == 0 && live && s_ok && kok && eq && !y_is_small_order(yw);
+  }
+#endif
+  // lanes 4j (j = 0..15) hold this wave's 16 results: one 16-bit piece of the block's bitmap word
+  const uint64_t vote = __ballot(acc);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bits |= (uint32_t)((vote >> (4 * j)) & 1u) << j;
+  const uint64_t piece = (uint64_t)blockIdx.x * LAT_COMB_WAVES + wave;  // signatures 16 piece .. 16 piece + 15
+  if (lane == 0 && piece < 4 * ((N + 63) / 64)) ((uint16_t*)bitmap)[piece] = (uint16_t)bits;  // bits past N: 0
+}
+
+// ---- per-plan launchers (comb_paNN.hip) ---------------------------------------
+struct comb_launch_args {
+  const uint8_t *R, *S, *K;
+  uint32_t rs_stride, k_stride;
+  const uint8_t* M;
+  uint32_t msg_len, msg_stride;
+  uint64_t N;
+  const uint32_t *tabB, *tabA, *keys;
+  const uint8_t* key_ok;
+  uint32_t n_keys;
+  uint32_t* xyz;           // comb -> finish workspace (one-lane mode)
+  uint8_t* flags;
+  uint32_t* eidx;          // entry-index workspace (latency mode: 64-bit entry addresses)
+  uint64_t* bitmap;        // latency mode writes the bitmap itself
+  const uint32_t* msg_idx; // votes form (null: one message per signature)
+  uint32_t n_msg;
+  bool latency_mode;
+  hipStream_t st;
+};
+
+// Launch the comb (or, in latency mode, the 4-lanes-per-signature kernel) for
+// key plan PLA; LEN 85 (the signed envelope) is a specialised template.
+template <class PLA>
+hipError_t launch_comb_plan(const comb_launch_args& a) {
+  const uint64_t N = a.N;
+  if (a.latency_mode) {
+    // enough blocks for every u16 piece of the ceil(N/64) bitmap words (>= ceil(N / LAT_SIGS))
+    const uint64_t pieces = 4 * ((N + 63) / 64);
+    const uint64_t sblocks = (pieces + LAT_COMB_WAVES - 1) / LAT_COMB_WAVES, Lpad = sblocks * LAT_COMB_WAVES * 64;
+    if (a.msg_len == PBFT_ENVELOPE_LEN)
+      hipLaunchKernelGGL((comb_latency_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)sblocks), dim3(LAT_BLOCK),
+                         LAT_LDS, a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad,
+                         a.tabB, a.tabA, a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx,
+                         a.n_msg);
+    else
+      hipLaunchKernelGGL((comb_latency_kernel<-1, PLA>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, a.st,
+                         a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad, a.tabB,
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg);
+  } else {
+    const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
+    const size_t lds = (BLOCK / 64) * COMB_LDS_PER_WAVE;
+    if (a.msg_len == PBFT_ENVELOPE_LEN)
+      hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
+                         a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
+                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg);
+    else
+      hipLaunchKernelGGL((comb_kernel<-1, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R, a.S, a.K,
+                         a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,
+                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg);
+  }
+  return hipGetLastError();
+}
+
+// defined in comb_pa13.hip / comb_pa14.hip / comb_pa16.hip / comb_pa32.hip
+hipError_t launch_comb_huge(const comb_launch_args& a);
+hipError_t launch_comb_big(const comb_launch_args& a);
+hipError_t launch_comb_mid(const comb_launch_args& a);
+hipError_t launch_comb_small(const comb_launch_args& a);
+
+// tables.hip: comb tables of the base point (pa = 0, plan PLB) or of -A per key (pa = the key plan's positions)
+hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
+                             uint8_t* d_key_ok, hipStream_t st);
+
+// finish.hip: batch-inversion finish (fm signatures per lane) of the one-lane comb
+hipError_t launch_finish(int fm, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz, const uint8_t* flags,
+                         uint64_t N, uint64_t* bitmap, hipStream_t st);
+// sign.hip: RFC 8032 signing, len = 85 (envelope), 0 (public keys only) or -1 (any length)
+void launch_sign(int len, dim3 grid, dim3 block, size_t lds, hipStream_t st, const uint32_t* seeds,
+                 const uint16_t* seed_idx, const uint8_t* msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
+                 const uint32_t* tabB, uint32_t* R, uint32_t* S, uint32_t* pub, uint32_t n_seeds);

@@ -5,9 +5,11 @@ set -e
 cd "$(dirname "$0")/.."
 mkdir -p build/ab
 name=$1; shift
-for h in replica wire; do
-  [ build/$h.o -nt pbft_amd/csrc/host/$h.cpp ] || g++ -O2 -std=c++17 -fPIC -c -o build/$h.o pbft_amd/csrc/host/$h.cpp
-done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared "$@" -o build/ab/libpbft_$name.so \
-  pbft_amd/csrc/pbft_verify.hip -x none build/replica.o build/wire.o
+python3 - "$name" "$@" <<'PY'
+import sys
+sys.path.insert(0, ".")
+from pbft_amd import native_build
+name, defines = sys.argv[1], sys.argv[2:]
+native_build.build_library(f"build/ab/libpbft_{name}.so", defines, objdir=f"build/ab/obj_{name}")
+PY
 echo built build/ab/libpbft_$name.so
