@@ -150,14 +150,18 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 
 /* Tuning options of one context (defaults are chosen by batch size / free HBM):
  *   PBFT_OPT_SPLIT_BELOW          batches below this many signatures use the 4-lanes-per-signature latency
- *                                 kernel (default 65536; env PBFT_SPLIT_BELOW)
- *   PBFT_OPT_FINISH_WIDTH         signatures per lane of the batch-inversion finish kernel: 1, 4 or 16
+ *                                 kernel (default 12288; env PBFT_SPLIT_BELOW)
+ *   PBFT_OPT_FINISH_WIDTH         signatures per lane of the batch-inversion finish kernel: 1, 2, 4, 8 or 16
  *                                 (0 = by batch size)
  *   PBFT_OPT_KEY_TABLE_BUDGET_MB  HBM budget for the replica key tables at the next pbft_verify_set_keys
- *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 96 GiB); selects the key comb plan */
+ *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 70 % of the free HBM); selects the key
+ *                                 comb plan
+ *   PBFT_OPT_FINISH_TREE          cross-lane levels of the finish's batch inversion: 0 (one inversion per lane)
+ *                                 or 6 (one per wave); any other value = by batch size */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
+#define PBFT_OPT_FINISH_TREE 4
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

@@ -164,4 +164,89 @@ __host__ __device__ __forceinline__ void fe_invert_gcd(fe& out, const fe& z) {
   fe_from_words(out, w);
 }
 
+// ---- variable-time form, for a wave-UNIFORM input --------------------------------
+// The finish kernel's cross-lane product tree leaves the same value in every lane
+// of a wave, so data-dependent branches never diverge and the public value needs
+// no constant-time treatment.  Original-delta divsteps (eta = -delta, starting at
+// -1; Bernstein & Yang 2019, the variable-time batching of libsecp256k1's
+// modinv32_var): the zeros of g are shifted out at once (ctz) and, while no swap
+// can occur (eta >= 0), up to min(eta + 1, steps left, 20) low bits of g are
+// cleared in ONE step g += w f with w = -g / f mod 2^limit (f^-1 mod 2^20 by
+// Newton's iteration from (3 f) ^ 2, exact to 5 bits).  The batch ends after 30
+// divsteps with the same transition-matrix convention as divsteps30 (2^30 f' =
+// u f + v g, 2^30 g' = q f + r g), so inv_update_de / inv_update_fg apply
+// unchanged; batches run until g = 0 (at most 25: the 724-divstep bound for
+// 256-bit inputs), then f = +-1 and x^-1 = +-d.  The inverse is unique, so the
+// result is bit-identical to fe_invert_gcd / z^(p-2).
+__host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t f, uint32_t g, int32_t t[4]) {
+  uint32_t u = 1, v = 0, q = 0, r = 1;
+  int i = 30;
+  for (;;) {
+    const int zeros = __builtin_ctz(g | (0xFFFFFFFFu << i));  // i >= 1: the mask has a set bit
+    g >>= zeros;
+    u <<= zeros;
+    v <<= zeros;
+    eta -= zeros;
+    i -= zeros;
+    if (i == 0) break;
+    // f and g odd
+    if (eta < 0) {  // delta > 0: swap (f, g) <- (g, -f), rows alike
+      eta = -eta;
+      uint32_t x = f; f = g; g = 0u - x;
+      x = u; u = q; q = 0u - x;
+      x = v; v = r; r = 0u - x;
+    }
+    int limit = eta + 1 < i ? eta + 1 : i;
+    if (limit > 20) limit = 20;
+    const uint32_t m = 0xFFFFFFFFu >> (32 - limit);
+    uint32_t y = (3u * f) ^ 2u;  // f^-1 mod 2^5
+    y *= 2u - f * y;             // mod 2^10
+    y *= 2u - f * y;             // mod 2^20
+    const uint32_t w = (0u - g * y) & m;  // g + w f = 0 mod 2^limit
+    g += f * w;
+    q += u * w;
+    r += v * w;
+  }
+  t[0] = (int32_t)u; t[1] = (int32_t)v; t[2] = (int32_t)q; t[3] = (int32_t)r;
+  return eta;
+}
+
+// out = z^-1 (0 -> 0) for a wave-uniform z (see above); z as for fe_invert_gcd
+__host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z) {
+  uint32_t w[8];
+  fe_to_words(w, z);
+  s30 f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int b = 30 * i, wi = b >> 5, sh = b & 31;
+    uint64_t x = w[wi] >> sh;
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << (32 - sh);
+    g.v[i] = (int32_t)((uint32_t)x & INV_M30);
+    f.v[i] = p30_limb(i);
+    d.v[i] = 0;
+    e.v[i] = i == 0 ? 1 : 0;
+  }
+  int32_t eta = -1;
+  for (int it = 0; it < 25; ++it) {
+    int32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nz |= g.v[i];
+    if (nz == 0) break;
+    int32_t t[4];
+    eta = divsteps30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+    inv_update_de(d, e, t);
+    inv_update_fg(f, g, t);
+  }
+  inv_normalize(d, f.v[8] >> 31);  // f = +-1
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int b = 32 * j, li = b / 30, sh = b % 30;
+    uint64_t x = (uint64_t)(uint32_t)d.v[li] >> sh;
+    x |= (uint64_t)(uint32_t)d.v[li + 1] << (30 - sh);
+    if (li + 2 < 9 && 60 - sh < 32) x |= (uint64_t)(uint32_t)d.v[li + 2] << (60 - sh);
+    w[j] = (uint32_t)x;
+  }
+  fe_from_words(out, w);
+}
+
 }  // namespace pbft

@@ -103,6 +103,7 @@ struct pbft_ctx {
   int pa = 0;  // comb positions of the installed key tables' plan (PLA_HUGE, PLA_BIG, PLA_MID or PLA_SMALL)
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
+  int fin_tree = -1;                   // finish cross-lane tree levels (0 / 6; -1 = by batch size)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   void adopt(keyset* k) {
     keyset_release(ks);
@@ -249,8 +250,10 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     // signatures per finish lane (one divsteps inversion per lane): measured on MI355X
     // (tools/size_probe.py, profiles/r02_size_probe.md) -- 1 up to 2^16, 4 up to 2^18, then 16
     int fm = N >= ((uint64_t)1 << 19) ? FIN_M : N > ((uint64_t)1 << 16) ? 4 : 1;
+    int lv = 0;
     if (c->fin_m) fm = c->fin_m;
-    HIP_TRY(launch_finish(fm, dR, rs_stride, xyz, flags, N, dB, st));
+    if (c->fin_tree >= 0) lv = c->fin_tree;
+    HIP_TRY(launch_finish(fm, lv, dR, rs_stride, xyz, flags, N, dB, st));
     HIP_TRY(hipGetLastError());
   }
   if (fst) {
@@ -857,10 +860,11 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
   switch (option) {
     case PBFT_OPT_SPLIT_BELOW: c->split_below = value; return PBFT_OK;
     case PBFT_OPT_FINISH_WIDTH:
-      if (value != 0 && value != 1 && value != 4 && value != 8 && value != FIN_M)
+      if (value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16)
         return set_err(PBFT_EINVAL, "finish width");
       c->fin_m = (int)value;
       return PBFT_OK;
+    case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 6) ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");

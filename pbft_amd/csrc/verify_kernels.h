@@ -586,9 +586,10 @@ hipError_t launch_comb_small(const comb_launch_args& a);
 hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
                              uint8_t* d_key_ok, hipStream_t st);
 
-// finish.hip: batch-inversion finish (fm signatures per lane) of the one-lane comb
-hipError_t launch_finish(int fm, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz, const uint8_t* flags,
-                         uint64_t N, uint64_t* bitmap, hipStream_t st);
+// finish.hip: batch-inversion finish of the one-lane comb: fm (1, 2, 4, 8, 16) signatures per lane, lv = 0
+// (one inversion per lane) or 6 (one per wave, cross-lane product tree)
+hipError_t launch_finish(int fm, int lv, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
+                         const uint8_t* flags, uint64_t N, uint64_t* bitmap, hipStream_t st);
 // sign.hip: RFC 8032 signing, len = 85 (envelope), 0 (public keys only) or -1 (any length)
 void launch_sign(int len, dim3 grid, dim3 block, size_t lds, hipStream_t st, const uint32_t* seeds,
                  const uint16_t* seed_idx, const uint8_t* msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,

@@ -81,6 +81,8 @@ void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
     case 13: { fe t, u; fe_sqT<true>(t, fa); fe_sub(u, fb, t); fe_mulT<true>(fo, u, t); break; }  // par output as subtrahend
     case 14: fe_invert_gcd(fo, fa); break;                            // safegcd (divsteps) inversion
     case 15: { fe t; fe_add(t, fa, fb); fe_invert_gcd(fo, t); break; } // of an uncarried sum
+    case 16: fe_invert_var(fo, fa); break;                            // variable-time divsteps (uniform input)
+    case 17: { fe t; fe_add(t, fa, fb); fe_invert_var(fo, t); break; }
     default: fo = fa;
   }
   fe_to_words(wo, fo);

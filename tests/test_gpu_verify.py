@@ -392,7 +392,8 @@ def test_device_launch_captured_in_hip_graph(gv, golden):
 def test_config2_pipelined_window(gv, coracle):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 Prepare + Commit signatures in one
     window batch (latency-mode kernel), 1 % adversarial, bit-exact with the C oracle; the same batch through the
-    one-lane-per-signature kernels (PBFT_OPT_SPLIT_BELOW = 0) gives the same bits, with every finish width."""
+    one-lane-per-signature kernels (PBFT_OPT_SPLIT_BELOW = 0) gives the same bits, with every finish width, with
+    and without the finish's cross-lane product tree, also on a ragged batch (partial last wave)."""
     from pbft_amd import GpuBatchVerifier
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 4, 1024, tag=2)
     assert len(R) == 8192
@@ -407,10 +408,15 @@ def test_config2_pipelined_window(gv, coracle):
     v1.set_option(v1.OPT_SPLIT_BELOW, 0)
     try:
         v1.set_keys(pub)
-        for fm in (1, 4, 16):
-            v1.set_option(v1.OPT_FINISH_WIDTH, fm)
-            got1, _ = verify(v1, R2, S2, K2, M2, 85)
-            assert (got1 == exp).all(), fm
+        n2 = len(R2) - 37
+        for lv in (0, 6):
+            v1.set_option(v1.OPT_FINISH_TREE, lv)
+            for fm in (1, 2, 4, 8, 16):
+                v1.set_option(v1.OPT_FINISH_WIDTH, fm)
+                got1, _ = verify(v1, R2, S2, K2, M2, 85)
+                assert (got1 == exp).all(), (fm, lv)
+                got2, _ = verify(v1, R2[:n2], S2[:n2], K2[:n2], M2[:n2], 85)
+                assert (got2 == exp[:n2]).all(), (fm, lv, n2)
         with pytest.raises(Exception):
             v1.set_option(v1.OPT_FINISH_WIDTH, 3)
     finally:

@@ -69,7 +69,8 @@ def test_field_ops(hh):
 
 
 def test_divsteps_inversion_extremes(hh):
-    """safegcd inversion (pbft_amd/csrc/inv25519.h) on inputs that stress the divstep count and the limb ranges:
+    """safegcd inversion (pbft_amd/csrc/inv25519.h), constant- and variable-time, on inputs that stress the divstep
+    count and the limb ranges:
     powers of two, p - 2^k, all-ones patterns, values just below p and unreduced encodings >= p."""
     vals = [2**k for k in range(255)] + [P - 2**k for k in range(1, 255)] + [(2**k - 1) for k in range(1, 256)]
     vals += [P - k for k in range(1, 40)] + [P + k for k in range(0, 19)] + [2**255 - 1 - k for k in range(20)]
@@ -77,6 +78,10 @@ def test_divsteps_inversion_extremes(hh):
     vals += [rnd.getrandbits(rnd.randrange(1, 256)) for _ in range(2000)]
     for a in vals:
         assert _fe(hh, 14, a % 2**255, 0) == pow(a % 2**255, P - 2, P), a
+        assert _fe(hh, 16, a % 2**255, 0) == pow(a % 2**255, P - 2, P), a  # variable-time form (finish tree)
+    for i, a in enumerate(vals[:300]):
+        b = vals[(i * 7 + 3) % len(vals)] % 2**255
+        assert _fe(hh, 17, a % 2**255, b) == pow(a % 2**255 + b, P - 2, P)
 
 
 @pytest.mark.parametrize("ln", [0, 1, 47, 48, 63, 64, 85, 111, 112, 175, 176, 239, 240, 300, 1023])

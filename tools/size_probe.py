@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--sizes", default="32768,65536,131072,262144,524288,1048576")
     ap.add_argument("--widths", default="1,4,16")
+    ap.add_argument("--trees", default="0", help="finish cross-lane tree levels to sweep (PBFT_OPT_FINISH_TREE)")
     ap.add_argument("--split-below", type=int, default=-1, help="PBFT_OPT_SPLIT_BELOW for this run (-1: default)")
     a = ap.parse_args()
     import torch
@@ -39,14 +40,16 @@ def main():
     bench.time_device(v, st, d, len(R), 20, torch)  # settle
     out = []
     for n in [int(x) for x in a.sizes.split(",")]:
-        for fm in [int(x) for x in a.widths.split(",")]:
+        for fm, lv in [(int(x), int(y)) for y in a.trees.split(",") for x in a.widths.split(",")]:
             v.set_option(v.OPT_FINISH_WIDTH, fm)
+            v.set_option(v.OPT_FINISH_TREE, lv)
             bench.time_device(v, st, d, n, 3, torch)
             ms, wall = bench.time_device(v, st, d, n, a.iters, torch)
             ok = bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), n).all()
-            out.append({"n": n, "fin_m": fm, "split_below": a.split_below, "ms": ms, "wall_ms": wall, "verifies_per_s": n / (ms * 1e-3), "ok": bool(ok)})
+            out.append({"n": n, "fin_m": fm, "fin_tree": lv, "split_below": a.split_below, "ms": ms, "wall_ms": wall, "verifies_per_s": n / (ms * 1e-3), "ok": bool(ok)})
             print(json.dumps(out[-1]), flush=True)
     v.set_option(v.OPT_FINISH_WIDTH, 0)
+    v.set_option(v.OPT_FINISH_TREE, 7)
     v.close()
 
 
