@@ -73,12 +73,18 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
     for (int u = 0; u < 10; ++u) tq[k].v[u] = (uint32_t)__shfl_xor((int)t.v[u], 1 << k);
     fe_mul(t, t, tq[k]);
   });
-#if PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
+#if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
+  inv = t;
+#elif PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
   fe_invert<true>(inv, t);
 #else
   if constexpr (LV == 6) {
     // every lane holds the wave's product: the variable-time divsteps never diverge (inv25519.h)
+#if PBFT_TREE_INV_CT  // A/B: the constant-time divsteps for the wave-uniform product too
+    fe_invert_gcd(inv, t);
+#else
     fe_invert_var(inv, t);
+#endif
   } else {
     fe_invert_gcd(inv, t);  // divsteps: ~19k instructions instead of ~44k on the serial chain
   }

@@ -250,7 +250,10 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     // signatures per finish lane (one divsteps inversion per lane): measured on MI355X
     // (tools/size_probe.py, profiles/r02_size_probe.md) -- 1 up to 2^16, 4 up to 2^18, then 16
     int fm = N >= ((uint64_t)1 << 19) ? FIN_M : N > ((uint64_t)1 << 16) ? 4 : 1;
-    int lv = 0;
+    // cross-lane product tree (one variable-time inversion per wave) where few signatures share a
+    // lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
+    // (profiles/r02_ab_log.md)
+    int lv = fm <= 4 ? 6 : 0;
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
     HIP_TRY(launch_finish(fm, lv, dR, rs_stride, xyz, flags, N, dB, st));

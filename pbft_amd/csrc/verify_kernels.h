@@ -69,6 +69,9 @@ __device__ __forceinline__ void load32(uint32_t w[8], const uint8_t* p) {
 // Step order of the comb: B_0, A_0, B_1, A_1, ... while both scalars have
 // positions, then the remaining positions of the longer one.
 typedef __attribute__((address_space(3))) void lds_void;
+#ifndef PBFT_DMA_BATCH
+#define PBFT_DMA_BATCH 1
+#endif
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // 16-B LDS read from a 32-bit LDS byte address (ds_read_b128)
 __device__ __forceinline__ u32x4 lds_read16(uint32_t addr) {
@@ -115,12 +118,24 @@ __device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t id
   const int k = lane >> 3;
   const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
   const int baddr = k << 2;
+#if PBFT_DMA_BATCH
+  // all 8 index fetches first (distinct registers), then the 8 loads: one lgkm wait per step instead of
+  // one per load -- the stalls matter where few waves share a SIMD (small shards, latency mode)
+  uint32_t e[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) e[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)idx);
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    __builtin_amdgcn_global_load_lds(base + (size_t)e[q] * 128 + coff,
+                                     (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+#else
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)idx);
     __builtin_amdgcn_global_load_lds(base + (size_t)e * 128 + coff,
                                      (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
   }
+#endif
 }
 
 // 8-B LDS read from a 32-bit LDS byte address (ds_read_b64)
@@ -321,6 +336,9 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #ifndef PBFT_LAT_DECOMP
 #define PBFT_LAT_DECOMP 0
 #endif
+#ifndef PBFT_LAT_TREE
+#define PBFT_LAT_TREE 1  // one variable-time inversion per wave (cross-lane product tree)
+#endif
 static constexpr int SPLIT = 4;
 static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
 static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // signatures per block
@@ -339,6 +357,19 @@ __device__ __forceinline__ void dma_entry_lines64(const uint8_t* addr, int lane,
   const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
   const int baddr = k << 2;
   const uint64_t a = (uint64_t)(uintptr_t)addr;
+#if PBFT_DMA_BATCH
+  uint32_t lo[8], hi[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    lo[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)a);
+    hi[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)(a >> 32));
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)hi[q] << 32) | lo[q]);
+    __builtin_amdgcn_global_load_lds(src + coff, (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+  }
+#else
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)(uint32_t)a);
@@ -346,6 +377,7 @@ __device__ __forceinline__ void dma_entry_lines64(const uint8_t* addr, int lane,
     const uint8_t* src = (const uint8_t*)(uintptr_t)(((uint64_t)hi << 32) | lo);
     __builtin_amdgcn_global_load_lds(src + coff, (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
   }
+#endif
 }
 
 FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
@@ -498,9 +530,34 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
   }
 #else
   {
-    // compress R' (one divsteps inversion) and compare with the canonical R encoding (DESIGN.md "R check")
+    // compress R' and compare with the canonical R encoding (DESIGN.md "R check")
     fe zi, x, y;
-    fe_invert_gcd(zi, P.Z);
+#if PBFT_LAT_TREE
+    // One inversion per wave instead of one per lane: butterfly product of the wave's 16 Z's over
+    // lanes ^4, ^8, ^16, ^32 (the 4 lanes of a signature hold the same R'), so every lane holds the
+    // same product and the shorter variable-time divsteps (inv25519.h) never diverge; the down-sweep
+    // peels the partners off again (1 / t_k = (1 / t_{k+1}) q_k).  Z is never 0 (complete formulas
+    // over curve points; invalid keys have identity tables), so no lane poisons the others.
+    fe t = P.Z, tq[4];
+    static_for<4>([&](auto kc) {
+      constexpr int k = decltype(kc)::value;
+      fe_shfl_xor(tq[k], t, SPLIT << k);
+      fe_mul(t, t, tq[k]);
+    });
+#if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
+    zi = t;
+#elif PBFT_TREE_INV_CT  // A/B: the constant-time divsteps for the wave-uniform product too
+    fe_invert_gcd(zi, t);
+#else
+    fe_invert_var(zi, t);
+#endif
+    static_for<4>([&](auto kc) {
+      constexpr int k = 3 - decltype(kc)::value;
+      fe_mul(zi, zi, tq[k]);
+    });
+#else
+    fe_invert_gcd(zi, P.Z);  // one constant-time divsteps inversion per lane
+#endif
     fe_mul(x, P.X, zi);
     fe_mul(y, P.Y, zi);
     uint32_t xw[8], yw[8], rr[8], ry[8];
