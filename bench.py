@@ -326,14 +326,14 @@ def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--seqs", type=int, default=SEQS, help="sequence numbers in the round (2 x replicas x seqs sigs)")
     ap.add_argument("--replicas", type=int, default=N_REPLICAS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the headline line (no side legs)")
     ap.add_argument("--latency-iters", type=int, default=200)
-    ap.add_argument("--settle-s", type=float, default=0.3, help="untimed GPU settle time before the warmup steps")
+    ap.add_argument("--settle-s", type=float, default=1.0, help="untimed GPU settle time before the warmup steps")
     ap.add_argument("--sequential", action="store_true", help="force rounds in order on one stream (the default)")
     ap.add_argument("--pipeline", action="store_true",
                     help="pipeline rounds: finish + all-gather of round k on a second stream under round k+1's comb")

@@ -157,11 +157,14 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 70 % of the free HBM); selects the key
  *                                 comb plan
  *   PBFT_OPT_FINISH_TREE          cross-lane levels of the finish's batch inversion: 0 (one inversion per lane)
- *                                 or 6 (one per wave); any other value = by batch size */
+ *                                 or 6 (one per wave); any other value = by batch size
+ *   PBFT_OPT_LAT_SPLIT            lanes per signature of the latency-mode kernel: 4 or 8; any other value = by
+ *                                 batch size (8 up to 8,192 signatures, else 4) */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
 #define PBFT_OPT_FINISH_TREE 4
+#define PBFT_OPT_LAT_SPLIT 5
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

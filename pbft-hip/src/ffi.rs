@@ -27,6 +27,8 @@ pub const PBFT_EBUSY: c_int = -6;
 pub const PBFT_OPT_SPLIT_BELOW: c_int = 1;
 pub const PBFT_OPT_FINISH_WIDTH: c_int = 2;
 pub const PBFT_OPT_KEY_TABLE_BUDGET_MB: c_int = 3;
+pub const PBFT_OPT_FINISH_TREE: c_int = 4;
+pub const PBFT_OPT_LAT_SPLIT: c_int = 5;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
 pub const PBFT_KIND_PREPARE: u8 = 1;

@@ -104,6 +104,7 @@ struct pbft_ctx {
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
   int fin_tree = -1;                   // finish cross-lane tree levels (0 / 6; -1 = by batch size)
+  int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   void adopt(keyset* k) {
     keyset_release(ks);
@@ -169,8 +170,10 @@ static_assert(steps<PLB, PLA_SMALL>::N >= steps<PLB, PLA_MID>::N && steps<PLB, P
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static inline size_t eidx_bytes(uint64_t N) {
   const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
-  // (latency mode: SPLIT lanes per signature, 8-byte entry addresses, ceil(steps / SPLIT) per lane)
-  const size_t split = 8 * (size_t)((MAX_STEPS + SPLIT - 1) / SPLIT) * (Npad * SPLIT + BLOCK);
+  // (latency mode: 4 or 8 lanes per signature, 8-byte entry addresses, ceil(steps / lanes) per lane)
+  const size_t split4 = 8 * (size_t)((MAX_STEPS + 3) / 4) * (Npad * 4 + BLOCK);
+  const size_t split8 = 8 * (size_t)((MAX_STEPS + 7) / 8) * (Npad * 8 + BLOCK);
+  const size_t split = split4 > split8 ? split4 : split8;
   const size_t comb = 4 * (size_t)MAX_STEPS * Npad;
   return ((comb > split ? comb : split) + 255) & ~(size_t)255;
 }
@@ -230,7 +233,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.xyz = (uint32_t*)hw;
   a.flags = hw + 120 * N;  // within the half's 121 W bytes
   a.eidx = (uint32_t*)(c->d_work + eidx_offset(W));
-  a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.latency_mode = latency_mode; a.st = st;
+  a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
   HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
@@ -868,6 +871,7 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
       c->fin_m = (int)value;
       return PBFT_OK;
     case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 6) ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");

@@ -321,15 +321,16 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 // serial work: SHA-512, 24 comb steps, then the finish kernel's inversion.
 // comb_latency_kernel (blocks of 4 waves -- one per SIMD, so each may use the
 // whole register file -- and 64 signatures per block) instead
-//  * gives every signature SPLIT = 4 lanes: each lane computes the challenge
+//  * gives every signature SPLIT = 4 (or 8) lanes: each lane computes the challenge
 //    hash itself (it is on the critical path anyway), then the steps
 //    j = SPLIT*t + r of the comb (r = lane % SPLIT; lanes without a step in the
-//    last round add the identity entry), and the 4 partial points are summed
-//    with two shuffle + extended-addition rounds (every lane of the group then
-//    holds R');
-//  * R' is compressed with ONE divsteps inversion (inv25519.h, ~20 us on the
-//    chain) and compared with the canonical R encoding, as the finish kernel
-//    does; each wave writes 16 bitmap bits (u16 pieces: piece 4 * block + wave).
+//    last round add the identity entry), and the SPLIT partial points are summed
+//    with log2(SPLIT) shuffle + extended-addition rounds (every lane of the group
+//    then holds R');
+//  * R' is compressed with ONE inversion per wave (product tree over the wave's
+//    signatures + variable-time divsteps, inv25519.h) and compared with the
+//    canonical R encoding, as the finish kernel does; each wave writes its
+//    64 / SPLIT bitmap bits (piece SPLIT-dependent u16 / u8).
 // Round 1 instead decompressed R on a fourth wave in parallel (z^((p-5)/8):
 // 254 squarings on one wave, ~80 us -- the critical path); PBFT_LAT_DECOMP=1
 // keeps that variant for A/B.  ~2.5x lower latency than one lane per signature.
@@ -339,9 +340,14 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #ifndef PBFT_LAT_TREE
 #define PBFT_LAT_TREE 1  // one variable-time inversion per wave (cross-lane product tree)
 #endif
-static constexpr int SPLIT = 4;
+// Lanes per signature: 8 up to PBFT_LAT_WIDE_UPTO signatures (3 comb steps per lane, 3 combine rounds), 4
+// above (the 8-lane grid would exceed one wave per SIMD): 1k 0.0900 -> 0.0861 ms, 4k 0.0919 -> 0.0885, 8k
+// 0.0932 -> 0.0920, 12k 0.0961 -> 0.1280 (profiles/r02_ab_log.md).
+#ifndef PBFT_LAT_WIDE_UPTO
+#define PBFT_LAT_WIDE_UPTO 8192
+#endif
+static constexpr uint64_t LAT_WIDE_UPTO = PBFT_LAT_WIDE_UPTO;
 static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
-static constexpr int LAT_SIGS = LAT_COMB_WAVES * 64 / 4;  // signatures per block
 static constexpr int LAT_BLOCK = 4 * 64;                   // (PBFT_LAT_DECOMP: 3 comb waves + 1 decompression wave)
 #ifndef PBFT_SPLIT_BELOW
 #define PBFT_SPLIT_BELOW 12288  // measured crossover: 8,192 sigs 0.105 ms here vs 0.133 ms one-lane; 16,384: 0.195 vs 0.133
@@ -385,7 +391,7 @@ FE_FN void fe_shfl_xor(fe& out, const fe& in, int mask) {
   for (int t = 0; t < 10; ++t) out.v[t] = (uint32_t)__shfl_xor((int)in.v[t], mask);
 }
 
-template <int LEN, class PLA>
+template <int LEN, class PLA, int SPLIT>
 __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
@@ -393,6 +399,11 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
     const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
+  static_assert(SPLIT == 4 || SPLIT == 8, "2 or 3 combine rounds");
+  static_assert(!PBFT_LAT_DECOMP || SPLIT == 4, "the decompression-wave variant pairs 4 lanes per signature");
+  constexpr int LAT_SW = 64 / SPLIT;                 // signatures per wave (bits of a wave's bitmap piece)
+  constexpr int LAT_SIGS = LAT_COMB_WAVES * LAT_SW;  // signatures per block
+  (void)LAT_SIGS;
   using ST = steps<PLB, PLA>;
   constexpr int T = (ST::N + SPLIT - 1) / SPLIT;  // local steps per lane
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -423,7 +434,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     return;
   }
 #endif
-  // ---- comb waves: 16 signatures per wave, SPLIT lanes each
+  // ---- comb waves: LAT_SW signatures per wave, SPLIT lanes each
   const uint64_t g = (uint64_t)blockIdx.x * (LAT_COMB_WAVES * 64) + threadIdx.x;  // global comb lane, < Lpad
   const uint64_t i = g / SPLIT;
   const int r = (int)(g % SPLIT);
@@ -506,8 +517,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
 #pragma unroll
     for (int u = 0; u < 10; ++u) asm("" : "+v"(P.X.v[u]), "+v"(P.Y.v[u]), "+v"(P.Z.v[u]), "+v"(P.T.v[u]));
   }
-  // sum the SPLIT partial points: lanes r ^ 1, then r ^ 2 (extended addition, complete formulas)
-  static_assert(SPLIT == 4, "two combine rounds");
+  // sum the SPLIT partial points: lanes r ^ 1, r ^ 2 (, r ^ 4) (extended addition, complete formulas)
   auto combine = [&](int m) {
     ge Q, Sum;
     fe_shfl_xor(Q.X, P.X, m); fe_shfl_xor(Q.Y, P.Y, m); fe_shfl_xor(Q.Z, P.Z, m); fe_shfl_xor(Q.T, P.T, m);
@@ -516,6 +526,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
   };
   combine(1);
   combine(2);
+  if constexpr (SPLIT == 8) combine(4);
   bool acc = false;
 #if PBFT_LAT_DECOMP
   __syncthreads();  // x_R, y_R of the block's signatures are in LDS
@@ -533,13 +544,14 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     // compress R' and compare with the canonical R encoding (DESIGN.md "R check")
     fe zi, x, y;
 #if PBFT_LAT_TREE
-    // One inversion per wave instead of one per lane: butterfly product of the wave's 16 Z's over
-    // lanes ^4, ^8, ^16, ^32 (the 4 lanes of a signature hold the same R'), so every lane holds the
+    // One inversion per wave instead of one per lane: butterfly product of the wave's LAT_SW Z's over
+    // lanes ^SPLIT .. ^32 (the SPLIT lanes of a signature hold the same R'), so every lane holds the
     // same product and the shorter variable-time divsteps (inv25519.h) never diverge; the down-sweep
     // peels the partners off again (1 / t_k = (1 / t_{k+1}) q_k).  Z is never 0 (complete formulas
     // over curve points; invalid keys have identity tables), so no lane poisons the others.
-    fe t = P.Z, tq[4];
-    static_for<4>([&](auto kc) {
+    constexpr int LV = SPLIT == 4 ? 4 : 3;  // log2(signatures per wave)
+    fe t = P.Z, tq[LV];
+    static_for<LV>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
       fe_shfl_xor(tq[k], t, SPLIT << k);
       fe_mul(t, t, tq[k]);
@@ -551,8 +563,8 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
 #else
     fe_invert_var(zi, t);
 #endif
-    static_for<4>([&](auto kc) {
-      constexpr int k = 3 - decltype(kc)::value;
+    static_for<LV>([&](auto kc) {
+      constexpr int k = LV - 1 - decltype(kc)::value;
       fe_mul(zi, zi, tq[k]);
     });
 #else
@@ -571,13 +583,17 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     acc = r == 0 && live && s_ok && kok && eq && !y_is_small_order(yw);
   }
 #endif
-  // lanes 4j (j = 0..15) hold this wave's 16 results: one 16-bit piece of the block's bitmap word
+  // lanes SPLIT j (j < LAT_SW) hold this wave's LAT_SW results: one LAT_SW-bit piece of the bitmap
+  // (u16 pieces at 4 lanes per signature, bytes at 8)
   const uint64_t vote = __ballot(acc);
   uint32_t bits = 0;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) bits |= (uint32_t)((vote >> (4 * j)) & 1u) << j;
-  const uint64_t piece = (uint64_t)blockIdx.x * LAT_COMB_WAVES + wave;  // signatures 16 piece .. 16 piece + 15
-  if (lane == 0 && piece < 4 * ((N + 63) / 64)) ((uint16_t*)bitmap)[piece] = (uint16_t)bits;  // bits past N: 0
+  for (int j = 0; j < LAT_SW; ++j) bits |= (uint32_t)((vote >> (SPLIT * j)) & 1u) << j;
+  const uint64_t piece = (uint64_t)blockIdx.x * LAT_COMB_WAVES + wave;  // signatures LAT_SW piece .. + LAT_SW - 1
+  if (lane == 0 && piece < (uint64_t)SPLIT * ((N + 63) / 64)) {            // bits past N: 0
+    if constexpr (LAT_SW == 16) ((uint16_t*)bitmap)[piece] = (uint16_t)bits;
+    else ((uint8_t*)bitmap)[piece] = (uint8_t)bits;
+  }
 }
 
 // ---- per-plan launchers (comb_paNN.hip) ---------------------------------------
@@ -597,6 +613,7 @@ struct comb_launch_args {
   const uint32_t* msg_idx; // votes form (null: one message per signature)
   uint32_t n_msg;
   bool latency_mode;
+  int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
   hipStream_t st;
 };
 
@@ -606,18 +623,22 @@ template <class PLA>
 hipError_t launch_comb_plan(const comb_launch_args& a) {
   const uint64_t N = a.N;
   if (a.latency_mode) {
-    // enough blocks for every u16 piece of the ceil(N/64) bitmap words (>= ceil(N / LAT_SIGS))
-    const uint64_t pieces = 4 * ((N + 63) / 64);
+    const int split = a.lat_split ? a.lat_split : (N <= LAT_WIDE_UPTO ? 8 : 4);
+    // enough blocks for every piece of the ceil(N/64) bitmap words (>= ceil(N / signatures per block))
+    const uint64_t pieces = (uint64_t)split * ((N + 63) / 64);
     const uint64_t sblocks = (pieces + LAT_COMB_WAVES - 1) / LAT_COMB_WAVES, Lpad = sblocks * LAT_COMB_WAVES * 64;
-    if (a.msg_len == PBFT_ENVELOPE_LEN)
-      hipLaunchKernelGGL((comb_latency_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)sblocks), dim3(LAT_BLOCK),
-                         LAT_LDS, a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad,
-                         a.tabB, a.tabA, a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx,
-                         a.n_msg);
-    else
-      hipLaunchKernelGGL((comb_latency_kernel<-1, PLA>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, a.st,
-                         a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad, a.tabB,
-                         a.tabA, a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg);
+#define PBFT_LAUNCH_LAT(LEN_, SPL_)                                                                               \
+  hipLaunchKernelGGL((comb_latency_kernel<LEN_, PLA, SPL_>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, a.st, \
+                     a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad, a.tabB, a.tabA,   \
+                     a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg)
+    if (a.msg_len == PBFT_ENVELOPE_LEN) {
+      if (split == 8 && !PBFT_LAT_DECOMP) PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 8 - 4 * PBFT_LAT_DECOMP);
+      else PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 4);
+    } else {
+      if (split == 8 && !PBFT_LAT_DECOMP) PBFT_LAUNCH_LAT(-1, 8 - 4 * PBFT_LAT_DECOMP);
+      else PBFT_LAUNCH_LAT(-1, 4);
+    }
+#undef PBFT_LAUNCH_LAT
   } else {
     const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
     const size_t lds = (BLOCK / 64) * COMB_LDS_PER_WAVE;

@@ -404,6 +404,17 @@ def test_config2_pipelined_window(gv, coracle):
     exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
     assert (got == exp).all(), np.nonzero(got != exp)[0][:10]
     assert not got[idx].any() and got.sum() == len(R) - len(idx)
+    # the latency kernel with 4 and with 8 lanes per signature (by size: 8 up to 8,192), full and ragged
+    n3 = len(R2) - 1000 - 37
+    try:
+        for sp in (4, 8):
+            gv.set_option(gv.OPT_LAT_SPLIT, sp)
+            got3, _ = verify(gv, R2, S2, K2, M2, 85)
+            assert (got3 == exp).all(), sp
+            got3, _ = verify(gv, R2[:n3], S2[:n3], K2[:n3], M2[:n3], 85)
+            assert (got3 == exp[:n3]).all(), (sp, n3)
+    finally:
+        gv.set_option(gv.OPT_LAT_SPLIT, 0)
     v1 = gv.clone()
     v1.set_option(v1.OPT_SPLIT_BELOW, 0)
     try:
