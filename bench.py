@@ -277,6 +277,40 @@ def e2e_votes_round(v, R, S, key_idx, msg, expect, torch, iters: int = 5):
                     "round's envelope table), chunked H2D overlapped with the kernels, bitmap D2H"}
 
 
+def votes_device_round(v, d, msg, expect, stream, torch, dev, iters: int = 50):
+    """The same 2^20 round device-resident in the votes form (pbft_verify_votes_device): R, S, key index, envelope
+    index per signature + the round's 4,096 envelopes, whose block-2 SHA-512 schedule is expanded once per envelope
+    inside the call (sha512.h sha512_env_sched).  Labelled figure beside `value` (which is the per-signature
+    message form of include/pbft_verify.h pbft_verify_batch_device)."""
+    from pbft_amd import bitmap_to_bool
+    env, inv = np.unique(msg, axis=0, return_inverse=True)
+    ep = np.zeros(len(env) * ENVELOPE + 64, dtype=np.uint8)  # + slack for the aligned tail reads
+    ep[: len(env) * ENVELOPE] = env.reshape(-1)
+    dE = torch.from_numpy(ep).to(dev)
+    dI = torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
+    n = len(msg)
+
+    def run():
+        v.verify_votes_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), dI.data_ptr(), dE.data_ptr(),
+                              len(env), n, d["B"].data_ptr(), stream.cuda_stream)
+
+    run()
+    torch.cuda.synchronize()
+    assert (bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), n) == expect).all(), "votes device bitmap differs"
+    for _ in range(5):
+        run()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record(stream)
+    for _ in range(iters):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    return {"value": n / (ms * 1e-3), "unit": "verifies/s", "ms_per_round": ms, "sigs": n, "envelopes": len(env),
+            "path": "device-resident votes form: envelope-schedule kernel + comb + finish per call"}
+
+
 def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 signatures per window batch, one GPU
     (device-resident p50 and host-buffer p50) vs the CPU baselines on the same batch."""
@@ -527,6 +561,7 @@ def main():
                                "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
         extras["e2e_2^20"] = e2e_host_round(v, R, S, key_idx, msg, expect, torch)
         extras["e2e_votes_2^20"] = e2e_votes_round(v, R, S, key_idx, msg, expect, torch)
+        extras["votes_device_2^20"] = votes_device_round(v, d, msg, expect, stream, torch, dev)
         extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
 
     if rank == 0:

@@ -120,6 +120,9 @@ struct pbft_ctx {
   // verify workspace: R' limbs [30][N] u32 + flags[N]
   uint8_t* d_work = nullptr;
   size_t work_cap = 0;
+  // votes form: per-envelope block-2 SHA-512 schedule (W[t] + K[t], t = 16..79; 512 B per envelope)
+  uint64_t* d_wk = nullptr;
+  uint64_t wk_cap = 0;  // envelopes
   uint64_t work_n = 0;     // signatures the workspace layout is sized for (offsets use this, not the batch N)
   bool work_two = false;   // two xyz/flags halves (pipelined form)
   hipEvent_t ev0 = nullptr, ev1 = nullptr, ev_done = nullptr;
@@ -136,6 +139,10 @@ struct pbft_ctx {
   uint64_t async_words = 0;
   float last_ms = 0.f;
 };
+
+#ifndef PBFT_ENV_SCHED
+#define PBFT_ENV_SCHED 1  // A/B: 0 = every signature expands its own block-2 schedule
+#endif
 
 static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
   if (bytes > c->stage_cap) {
@@ -208,7 +215,7 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
                          uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
-                         const uint32_t* dMI = nullptr, uint32_t n_msg = 0) {
+                         const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
@@ -234,6 +241,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.flags = hw + 120 * N;  // within the half's 121 W bytes
   a.eidx = (uint32_t*)(c->d_work + eidx_offset(W));
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
+  a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
   HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
@@ -341,6 +349,35 @@ static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   return PBFT_OK;
 }
 
+// Votes form, once per call: the block-2 SHA-512 schedule of every 85-byte envelope (sha512.h
+// sha512_env_sched), read by each signature's challenge hash instead of expanding it again.
+__global__ void __launch_bounds__(BLOCK) env_sched_kernel(const uint8_t* __restrict__ env, uint32_t n_env,
+                                                          uint64_t* __restrict__ wk) {
+  const uint64_t e = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (e >= n_env) return;
+  sha512_env_sched(wk + (size_t)SHA_ENV_WORDS * e, env + (size_t)PBFT_ENVELOPE_LEN * e);
+}
+
+// (the buffer grows on first use for a bigger table: not inside a stream capture)
+static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, hipStream_t st, const uint64_t** out) {
+  if (n_env > c->wk_cap) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->d_wk) {
+      HIP_TRY(hipDeviceSynchronize());  // a device-form launch may still read it on a caller's stream
+      HIP_TRY(hipFree(c->d_wk));
+    }
+    c->d_wk = nullptr;
+    c->wk_cap = 0;
+    if (hipMalloc(&c->d_wk, (size_t)SHA_ENV_WORDS * 8 * n_env) != hipSuccess)
+      return set_err(PBFT_ENOMEM, "envelope schedule alloc");
+    c->wk_cap = n_env;
+  }
+  hipLaunchKernelGGL(env_sched_kernel, dim3((n_env + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, dENV, n_env, c->d_wk);
+  HIP_TRY(hipGetLastError());
+  *out = c->d_wk;
+  return PBFT_OK;
+}
+
 // Votes form (include/pbft_verify.h pbft_verify_votes): R, S, key_idx and a 4-byte envelope index per
 // signature (70 B instead of 151 B over PCIe) + the batch's table of distinct 85-byte envelopes.
 struct votes_layout {
@@ -364,6 +401,13 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
   // envelope table first (copy stream), then each chunk's columns; the kernels of chunk c run on the context
   // stream after its copies, overlapping the copies of chunk c+1
   HIP_TRY(hipMemcpyAsync(c->d_stage, ENV, (size_t)PBFT_ENVELOPE_LEN * n_env, hipMemcpyHostToDevice, c->cstream));
+  // the envelopes' block-2 schedule on the context stream once the table has landed (ev_copied[0] is
+  // re-recorded by chunk 0 below)
+  HIP_TRY(hipEventRecord(c->ev_copied[0], c->cstream));
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[0], 0));
+  const uint64_t* dWK = nullptr;
+  rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &dWK);
+  if (rc) return rc;
   uint64_t chunk = 0;
   for (uint64_t lo = 0; lo < N; lo += PIPE_CHUNK, ++chunk) {
     const uint64_t n = N - lo < PIPE_CHUNK ? N - lo : PIPE_CHUNK;
@@ -378,7 +422,7 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
     rc = launch_verify(c, base, base + L.offS, (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN,
                        PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, 32, 2, nullptr,
-                       (const uint32_t*)(base + L.offI), n_env);
+                       (const uint32_t*)(base + L.offI), n_env, dWK);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
   }
@@ -489,7 +533,7 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   release_base_table(c->device);
   c->adopt(nullptr);
-  (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work);
+  (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work); (void)hipFree(c->d_wk);
   if (c->h_bitmap) (void)hipHostFree(c->h_bitmap);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -712,8 +756,12 @@ int pbft_verify_votes_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, 
   if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
   HIP_TRY(hipSetDevice(c->device));
   hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+  if (N == 0) return PBFT_OK;
+  const uint64_t* dWK = nullptr;
+  int rc = prepare_env_sched(c, d_envelopes, n_env, st, &dWK);
+  if (rc) return rc;
   return launch_verify(c, dR, dS, dK, d_envelopes, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, N, dB, st, 32, 2, nullptr,
-                       d_env_idx, n_env);
+                       d_env_idx, n_env, dWK);
 }
 
 // Binary wire records (include/pbft_wire.h): R at +0, S at +32, envelope at +64,

@@ -256,4 +256,82 @@ __host__ __device__ __forceinline__ void sha512_ram(uint32_t out[16], const uint
   sha512_pre<64, LEN>(out, pre, m, len_rt);
 }
 
+// ---- the signed envelope's share of the hash, once per envelope -------------------------------
+// For the 85-byte envelope, R || A || M is 149 bytes: block 2 holds only M[64..84], the 0x80
+// terminator and the length, so its message schedule W[16..79] is a function of the ENVELOPE alone.
+// In a PBFT round every envelope is signed by all n replicas (the votes form, include/pbft_verify.h
+// pbft_verify_votes): env_sched computes W[t] + K[t], t = 16..79, once per envelope (512 B), and the
+// per-signature hash reads them instead of expanding the schedule -- the same SHA-512, ~1.3k fewer
+// VALU instructions per signature.
+#define SHA_ENV_WORDS 64  // W[t] + K[t] for t = 16 .. 79
+__host__ __device__ __forceinline__ void sha512_env_block2(uint64_t W[16], const uint8_t* m) {
+  // bytes 128 .. 148 of R || A || M = M[64 .. 84]; then 0x80, zeros, the 128-bit length 149 * 8
+#pragma unroll
+  for (int t = 0; t < 16; ++t) W[t] = t < 3 ? msg_word(m, 85, 8 + t) : 0u;
+  W[15] = 149u * 8u;
+}
+__host__ __device__ __forceinline__ void sha512_env_sched(uint64_t wk[SHA_ENV_WORDS], const uint8_t* m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t* K = SHA512_K;
+#else
+  const uint64_t K[80] = SHA512_K_TABLE;
+#endif
+  uint64_t W[16];
+  sha512_env_block2(W, m);
+#pragma unroll
+  for (int t = 16; t < 80; ++t) {
+    const int j = t & 15;
+    W[j] = W[j] + small_sigma0(W[(j + 1) & 15]) + W[(j + 9) & 15] + small_sigma1(W[(j + 14) & 15]);
+    wk[t - 16] = W[j] + K[t];
+  }
+}
+// SHA-512(R || A || M) for an 85-byte M whose block-2 schedule (+K) is wk (env_sched)
+__host__ __device__ __forceinline__ void sha512_ram_env(uint32_t out[16], const uint32_t r[8], const uint32_t a[8],
+                                                        const uint8_t* m, const uint64_t* __restrict__ wk) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint64_t* K = SHA512_K;
+#else
+  const uint64_t K[80] = SHA512_K_TABLE;
+#endif
+  uint64_t H[8];
+  sha512_init(H);
+  uint64_t W[16];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    W[t] = ((uint64_t)bswap32(r[2 * t]) << 32) | bswap32(r[2 * t + 1]);
+    W[4 + t] = ((uint64_t)bswap32(a[2 * t]) << 32) | bswap32(a[2 * t + 1]);
+  }
+#pragma unroll
+  for (int t = 8; t < 16; ++t) W[t] = msg_word(m, 85, t - 8);
+  sha512_compress(H, W);
+  sha512_env_block2(W, m);
+  uint64_t a_ = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) sha512_round(a_, b, c, d, e, f, g, h, K[j], W[j]);
+#pragma nounroll
+  for (int t0 = 0; t0 < SHA_ENV_WORDS; t0 += 16) {
+    uint64_t kw[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint4* p4 = (const uint4*)(wk + t0);  // rows are 512-B aligned: 8 x 16-B loads per 16 rounds
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint4 v = p4[q];
+      kw[2 * q] = MK64(v.y, v.x);
+      kw[2 * q + 1] = MK64(v.w, v.z);
+    }
+#else
+#pragma unroll
+    for (int j = 0; j < 16; ++j) kw[j] = wk[t0 + j];
+#endif
+#pragma unroll
+    for (int j = 0; j < 16; ++j) sha512_round(a_, b, c, d, e, f, g, h, 0u, kw[j]);  // T1 = h + S1 + ch + (K + W)
+  }
+  H[0] += a_; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    out[2 * i] = bswap32((uint32_t)(H[i] >> 32));
+    out[2 * i + 1] = bswap32((uint32_t)H[i]);
+  }
+}
+
 }  // namespace pbft

@@ -185,6 +185,20 @@ __device__ __forceinline__ void lds_entry_signed(uint32_t rd0, bool neg, fe& qa,
 #endif
 static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
 
+// The challenge hash k = SHA-512(R || A || M): with the votes form's per-envelope block-2 schedule
+// (wk != null, 85-byte envelopes; sha512_env_sched, env_sched_kernel) or in full.
+template <int LEN>
+__device__ __forceinline__ void sha512_k(uint32_t h[16], const uint32_t r[8], const uint32_t a[8], const uint8_t* m,
+                                         int len, const uint64_t* __restrict__ wk, uint64_t mrow) {
+  if constexpr (LEN == PBFT_ENVELOPE_LEN) {
+    if (wk) {
+      sha512_ram_env(h, r, a, m, wk + (size_t)SHA_ENV_WORDS * mrow);
+      return;
+    }
+  }
+  sha512_ram<LEN>(h, r, a, m, len);
+}
+
 template <int LEN, class PLA>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
@@ -192,7 +206,8 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
-    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
+    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg,
+    const uint64_t* __restrict__ wk) {
   using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -231,7 +246,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #pragma unroll
     for (int t = 0; t < 16; ++t) h[t] = r[t & 7] ^ a[(t + 3) & 7];
 #else
-    sha512_ram<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
+    sha512_k<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len, wk, mrow);
 #endif
     sc_reduce512(k, h);
     // per-step entry index (128-B units from the step's table base) and sign
@@ -398,7 +413,8 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
-    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg) {
+    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg,
+    const uint64_t* __restrict__ wk) {
   static_assert(SPLIT == 4 || SPLIT == 8, "2 or 3 combine rounds");
   static_assert(!PBFT_LAT_DECOMP || SPLIT == 4, "the decompression-wave variant pairs 4 lanes per signature");
   constexpr int LAT_SW = 64 / SPLIT;                 // signatures per wave (bits of a wave's bitmap piece)
@@ -464,7 +480,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     s_ok = sc_lt_L(s);
     sc_clamp_rejected(s, s_ok);  // s >= L: recode 0, never index past the base-point table
     uint32_t h[16], k[8];
-    sha512_ram<LEN>(h, rr, a, msg + (size_t)msg_stride * mrow, (int)msg_len);
+    sha512_k<LEN>(h, rr, a, msg + (size_t)msg_stride * mrow, (int)msg_len, wk, mrow);
     sc_reduce512(k, h);
     const uint8_t* tA = (const uint8_t*)tabA + (size_t)ki * PLA::TABLE_WORDS * 4;
     digits ds, dk;
@@ -612,6 +628,7 @@ struct comb_launch_args {
   uint64_t* bitmap;        // latency mode writes the bitmap itself
   const uint32_t* msg_idx; // votes form (null: one message per signature)
   uint32_t n_msg;
+  const uint64_t* wk;      // votes form, 85-byte envelopes: per-envelope block-2 schedule (null: hash in full)
   bool latency_mode;
   int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
   hipStream_t st;
@@ -630,7 +647,7 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
 #define PBFT_LAUNCH_LAT(LEN_, SPL_)                                                                               \
   hipLaunchKernelGGL((comb_latency_kernel<LEN_, PLA, SPL_>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, a.st, \
                      a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad, a.tabB, a.tabA,   \
-                     a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg)
+                     a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg, a.wk)
     if (a.msg_len == PBFT_ENVELOPE_LEN) {
       if (split == 8 && !PBFT_LAT_DECOMP) PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 8 - 4 * PBFT_LAT_DECOMP);
       else PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 4);
@@ -645,11 +662,11 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
     if (a.msg_len == PBFT_ENVELOPE_LEN)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
                          a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
-                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg);
+                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
     else
       hipLaunchKernelGGL((comb_kernel<-1, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R, a.S, a.K,
                          a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,
-                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg);
+                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
   }
   return hipGetLastError();
 }

@@ -107,6 +107,16 @@ void hh_sha512_ram(const uint8_t* r, const uint8_t* a, const uint8_t* m, int len
   for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
 }
 
+// the votes form's hash: block-2 schedule of the 85-byte envelope once (sha512_env_sched), then per signature
+void hh_sha512_ram_env(const uint8_t* r, const uint8_t* a, const uint8_t* m, uint8_t* out64) {
+  uint32_t wr[8], wa[8], h[16];
+  uint64_t wk[SHA_ENV_WORDS];
+  words_from_bytes(wr, r); words_from_bytes(wa, a);
+  sha512_env_sched(wk, m);
+  sha512_ram_env(h, wr, wa, m, wk);
+  for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
 void hh_reduce512(const uint8_t* x64, uint8_t* out32) {
   uint32_t x[16], o[8];
   for (int i = 0; i < 16; ++i) x[i] = x64[4 * i] | (x64[4 * i + 1] << 8) | (x64[4 * i + 2] << 16) | ((uint32_t)x64[4 * i + 3] << 24);

@@ -95,6 +95,19 @@ def test_sha512_ram(hh, ln):
         assert out.raw == hashlib.sha512(r + a + m).digest(), fixed
 
 
+def test_sha512_ram_envelope_schedule(hh):
+    """Votes form: the 85-byte envelope's block-2 schedule computed once (sha512_env_sched) and the per-signature
+    hash that reads it (sha512_ram_env) give SHA-512(R || A || M)."""
+    rnd = random.Random(85)
+    out = ctypes.create_string_buffer(64)
+    for k in range(300):
+        r, a, m = rnd.randbytes(32), rnd.randbytes(32), rnd.randbytes(85)
+        if k < 4:
+            m = bytes([[0x00, 0xFF, 0x80, 0x7F][k]]) * 85
+        hh.hh_sha512_ram_env(r, a, m + bytes(16), out)
+        assert out.raw == hashlib.sha512(r + a + m).digest(), k
+
+
 def test_reduce512(hh):
     rnd = random.Random(11)
     L = E.L

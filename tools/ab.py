@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--seqs", type=int, default=2048)
     ap.add_argument("--per-launch-events", action="store_true", help="also record a torch event pair per launch")
     ap.add_argument("--sizes", default="", help="comma list of batch sizes (default: the whole round)")
+    ap.add_argument("--votes", action="store_true", help="time the votes form (pbft_verify_votes_device)")
     a = ap.parse_args()
     import torch
     import bench
@@ -42,6 +43,11 @@ def main():
     mp[: n * 85] = msg.reshape(-1)
     dM = torch.from_numpy(mp).to(dev)
     dB = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    env, inv = np.unique(msg, axis=0, return_inverse=True)
+    ep = np.zeros(len(env) * 85 + 64, dtype=np.uint8)
+    ep[: len(env) * 85] = env.reshape(-1)
+    dE = torch.from_numpy(ep).to(dev)
+    dI = torch.from_numpy(inv.reshape(-1).astype(np.int32)).to(dev)
     torch.cuda.synchronize()
     st = torch.cuda.Stream(dev)
     ctxs = []
@@ -52,6 +58,7 @@ def main():
         lib.pbft_verify_set_keys.argtypes = [vp, vp, ctypes.c_uint32, vp]
         lib.pbft_verify_batch_device.argtypes = [vp, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint32,
                                                  ctypes.c_uint64, vp, vp]
+        lib.pbft_verify_votes_device.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_uint32, ctypes.c_uint64, vp, vp]
         lib.pbft_build_info.restype = ctypes.c_char_p
         c = vp()
         assert lib.pbft_verify_ctx_create(0, ctypes.byref(c)) == 0
@@ -70,8 +77,12 @@ def main():
             for _ in range(a.iters):
                 if a.per_launch_events:
                     torch.cuda.Event(enable_timing=True).record(st)
-                assert lib.pbft_verify_batch_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(),
-                                                    85, 85, n, dB.data_ptr(), st.cuda_stream) == 0
+                if a.votes:
+                    assert lib.pbft_verify_votes_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dI.data_ptr(),
+                                                        dE.data_ptr(), len(env), n, dB.data_ptr(), st.cuda_stream) == 0
+                else:
+                    assert lib.pbft_verify_batch_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(),
+                                                        85, 85, n, dB.data_ptr(), st.cuda_stream) == 0
             e1.record(st)
             st.synchronize()
             res[p].append(e0.elapsed_time(e1) / a.iters)

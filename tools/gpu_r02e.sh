@@ -8,7 +8,7 @@ SIZES=${SIZES:-4096,131072,262144}
 i=0
 for pair in "$@"; do
   i=$((i+1))
-  PBFT_KEY_TABLE_BUDGET_MB=90000 timeout -k 10 300 python tools/ab.py ${pair/,/ } --sizes "$SIZES" --rounds 8 > gpurun_out/ab$i.log 2>&1; rc=$?
+  PBFT_KEY_TABLE_BUDGET_MB=90000 timeout -k 10 300 python tools/ab.py ${pair/,/ } --sizes "$SIZES" --rounds 8 $ABARGS > gpurun_out/ab$i.log 2>&1; rc=$?
   grep -E "N=|Error|error" gpurun_out/ab$i.log | cut -c1-110
   [ $rc -ne 0 ] && exit $rc
 done
