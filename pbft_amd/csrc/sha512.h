@@ -285,9 +285,17 @@ __host__ __device__ __forceinline__ void sha512_env_sched(uint64_t wk[SHA_ENV_WO
     wk[t - 16] = W[j] + K[t];
   }
 }
-// SHA-512(R || A || M) for an 85-byte M whose block-2 schedule (+K) is wk (env_sched)
-__host__ __device__ __forceinline__ void sha512_ram_env(uint32_t out[16], const uint32_t r[8], const uint32_t a[8],
-                                                        const uint8_t* m, const uint64_t* __restrict__ wk) {
+// SHA-512(R || A || M) for an 85-byte M.  Block 2 (M[64..84] + padding) needs its message schedule
+// W[16..79], a function of the envelope alone, which comes
+//  * from the SCALAR unit when every lane of the wave signs the same envelope (a round's signatures are
+//    grouped by envelope, n replicas each): the schedule is computed once per wave in SGPRs, beside the
+//    other waves' VALU work, and enters each round as a scalar operand;
+//  * else from wk (the votes form's per-envelope table, env_sched_kernel), if given;
+//  * else per lane, as sha512_compress does.
+// Same hash in every case (host harness: test_sha512_ram_envelope_schedule; GPU: golden + round tests).
+__host__ __device__ __forceinline__ uint64_t rotr64_s(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+__host__ __device__ __forceinline__ void sha512_ram85(uint32_t out[16], const uint32_t r[8], const uint32_t a[8],
+                                                      const uint8_t* m, const uint64_t* __restrict__ wk) {
 #if defined(__HIP_DEVICE_COMPILE__)
   const uint64_t* K = SHA512_K;
 #else
@@ -308,23 +316,68 @@ __host__ __device__ __forceinline__ void sha512_ram_env(uint32_t out[16], const 
   uint64_t a_ = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
 #pragma unroll
   for (int j = 0; j < 16; ++j) sha512_round(a_, b, c, d, e, f, g, h, K[j], W[j]);
-#pragma nounroll
-  for (int t0 = 0; t0 < SHA_ENV_WORDS; t0 += 16) {
-    uint64_t kw[16];
 #if defined(__HIP_DEVICE_COMPILE__)
-    const uint4* p4 = (const uint4*)(wk + t0);  // rows are 512-B aligned: 8 x 16-B loads per 16 rounds
+  const uint32_t w0l = (uint32_t)__builtin_amdgcn_readfirstlane((int)LO32(W[0]));
+  const uint32_t w0h = (uint32_t)__builtin_amdgcn_readfirstlane((int)HI32(W[0]));
+  const uint32_t w1l = (uint32_t)__builtin_amdgcn_readfirstlane((int)LO32(W[1]));
+  const uint32_t w1h = (uint32_t)__builtin_amdgcn_readfirstlane((int)HI32(W[1]));
+  const uint32_t w2l = (uint32_t)__builtin_amdgcn_readfirstlane((int)LO32(W[2]));
+  const uint32_t w2h = (uint32_t)__builtin_amdgcn_readfirstlane((int)HI32(W[2]));
+  const bool same = LO32(W[0]) == w0l && HI32(W[0]) == w0h && LO32(W[1]) == w1l && HI32(W[1]) == w1h &&
+                    LO32(W[2]) == w2l && HI32(W[2]) == w2h;
+#ifndef PBFT_SALU_SCHED
+#define PBFT_SALU_SCHED 1  // A/B: 0 = no wave-uniform scalar schedule
+#endif
+  if (PBFT_SALU_SCHED && __all(same)) {
+    // wave-uniform schedule: plain 64-bit shifts (s_lshr_b64 / s_lshl_b64 / s_or_b64 on the SALU)
+    uint64_t Ws[16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const uint4 v = p4[q];
-      kw[2 * q] = MK64(v.y, v.x);
-      kw[2 * q + 1] = MK64(v.w, v.z);
+    for (int t = 0; t < 16; ++t) Ws[t] = 0;
+    Ws[0] = ((uint64_t)w0h << 32) | w0l;
+    Ws[1] = ((uint64_t)w1h << 32) | w1l;
+    Ws[2] = ((uint64_t)w2h << 32) | w2l;
+    Ws[15] = 149u * 8u;
+#pragma nounroll
+    for (int t0 = 16; t0 < 80; t0 += 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const uint64_t x15 = Ws[(j + 1) & 15], x2 = Ws[(j + 14) & 15];
+        const uint64_t s0 = rotr64_s(x15, 1) ^ rotr64_s(x15, 8) ^ (x15 >> 7);
+        const uint64_t s1 = rotr64_s(x2, 19) ^ rotr64_s(x2, 61) ^ (x2 >> 6);
+        Ws[j] = Ws[j] + s0 + Ws[(j + 9) & 15] + s1;
+        sha512_round(a_, b, c, d, e, f, g, h, 0u, Ws[j] + K[t0 + j]);
+      }
     }
+  } else
+#endif
+  if (wk) {
+#pragma nounroll
+    for (int t0 = 0; t0 < SHA_ENV_WORDS; t0 += 16) {
+      uint64_t kw[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+      const uint4* p4 = (const uint4*)(wk + t0);  // rows are 512-B aligned: 8 x 16-B loads per 16 rounds
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const uint4 v = p4[q];
+        kw[2 * q] = MK64(v.y, v.x);
+        kw[2 * q + 1] = MK64(v.w, v.z);
+      }
 #else
 #pragma unroll
-    for (int j = 0; j < 16; ++j) kw[j] = wk[t0 + j];
+      for (int j = 0; j < 16; ++j) kw[j] = wk[t0 + j];
 #endif
 #pragma unroll
-    for (int j = 0; j < 16; ++j) sha512_round(a_, b, c, d, e, f, g, h, 0u, kw[j]);  // T1 = h + S1 + ch + (K + W)
+      for (int j = 0; j < 16; ++j) sha512_round(a_, b, c, d, e, f, g, h, 0u, kw[j]);  // T1 = h + S1 + ch + (K + W)
+    }
+  } else {
+#pragma nounroll
+    for (int t0 = 16; t0 < 80; t0 += 16) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        W[j] = W[j] + small_sigma0(W[(j + 1) & 15]) + W[(j + 9) & 15] + small_sigma1(W[(j + 14) & 15]);
+        sha512_round(a_, b, c, d, e, f, g, h, K[t0 + j], W[j]);
+      }
+    }
   }
   H[0] += a_; H[1] += b; H[2] += c; H[3] += d; H[4] += e; H[5] += f; H[6] += g; H[7] += h;
 #pragma unroll
@@ -332,6 +385,11 @@ __host__ __device__ __forceinline__ void sha512_ram_env(uint32_t out[16], const 
     out[2 * i] = bswap32((uint32_t)(H[i] >> 32));
     out[2 * i + 1] = bswap32((uint32_t)H[i]);
   }
+}
+// the votes form's entry point (kept for the host harness): the per-envelope table
+__host__ __device__ __forceinline__ void sha512_ram_env(uint32_t out[16], const uint32_t r[8], const uint32_t a[8],
+                                                        const uint8_t* m, const uint64_t* __restrict__ wk) {
+  sha512_ram85(out, r, a, m, wk);
 }
 
 }  // namespace pbft

@@ -185,18 +185,17 @@ __device__ __forceinline__ void lds_entry_signed(uint32_t rd0, bool neg, fe& qa,
 #endif
 static constexpr uint32_t COMB_LDS_PER_WAVE = 8 * 1024;
 
-// The challenge hash k = SHA-512(R || A || M): with the votes form's per-envelope block-2 schedule
-// (wk != null, 85-byte envelopes; sha512_env_sched, env_sched_kernel) or in full.
+// The challenge hash k = SHA-512(R || A || M).  85-byte envelopes: block 2's schedule from the scalar unit
+// when the whole wave signs one envelope, else from the votes form's per-envelope table (wk != null), else
+// per lane (sha512.h sha512_ram85); other lengths in full.
 template <int LEN>
 __device__ __forceinline__ void sha512_k(uint32_t h[16], const uint32_t r[8], const uint32_t a[8], const uint8_t* m,
                                          int len, const uint64_t* __restrict__ wk, uint64_t mrow) {
   if constexpr (LEN == PBFT_ENVELOPE_LEN) {
-    if (wk) {
-      sha512_ram_env(h, r, a, m, wk + (size_t)SHA_ENV_WORDS * mrow);
-      return;
-    }
+    sha512_ram85(h, r, a, m, wk ? wk + (size_t)SHA_ENV_WORDS * mrow : nullptr);
+  } else {
+    sha512_ram<LEN>(h, r, a, m, len);
   }
-  sha512_ram<LEN>(h, r, a, m, len);
 }
 
 template <int LEN, class PLA>

@@ -117,6 +117,14 @@ void hh_sha512_ram_env(const uint8_t* r, const uint8_t* a, const uint8_t* m, uin
   for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
 }
 
+// sha512_ram85 without the per-envelope table (the per-lane schedule path)
+void hh_sha512_ram85(const uint8_t* r, const uint8_t* a, const uint8_t* m, uint8_t* out64) {
+  uint32_t wr[8], wa[8], h[16];
+  words_from_bytes(wr, r); words_from_bytes(wa, a);
+  sha512_ram85(h, wr, wa, m, nullptr);
+  for (int i = 0; i < 16; ++i) for (int j = 0; j < 4; ++j) out64[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
 void hh_reduce512(const uint8_t* x64, uint8_t* out32) {
   uint32_t x[16], o[8];
   for (int i = 0; i < 16; ++i) x[i] = x64[4 * i] | (x64[4 * i + 1] << 8) | (x64[4 * i + 2] << 16) | ((uint32_t)x64[4 * i + 3] << 24);

@@ -97,7 +97,8 @@ def test_sha512_ram(hh, ln):
 
 def test_sha512_ram_envelope_schedule(hh):
     """Votes form: the 85-byte envelope's block-2 schedule computed once (sha512_env_sched) and the per-signature
-    hash that reads it (sha512_ram_env) give SHA-512(R || A || M)."""
+    hash that reads it (sha512_ram_env), and sha512_ram85's per-lane path, give SHA-512(R || A || M) (the
+    wave-uniform scalar path is device-only: the GPU round tests cover it)."""
     rnd = random.Random(85)
     out = ctypes.create_string_buffer(64)
     for k in range(300):
@@ -105,6 +106,8 @@ def test_sha512_ram_envelope_schedule(hh):
         if k < 4:
             m = bytes([[0x00, 0xFF, 0x80, 0x7F][k]]) * 85
         hh.hh_sha512_ram_env(r, a, m + bytes(16), out)
+        assert out.raw == hashlib.sha512(r + a + m).digest(), k
+        hh.hh_sha512_ram85(r, a, m + bytes(16), out)
         assert out.raw == hashlib.sha512(r + a + m).digest(), k
 
 
