@@ -264,6 +264,9 @@ __host__ __device__ __forceinline__ void sha512_ram(uint32_t out[16], const uint
 // per-signature hash reads them instead of expanding the schedule -- the same SHA-512, ~1.3k fewer
 // VALU instructions per signature.
 #define SHA_ENV_WORDS 64  // W[t] + K[t] for t = 16 .. 79
+#ifndef PBFT_SALU_SCHED
+#define PBFT_SALU_SCHED 1  // A/B: 0 = no wave-uniform scalar schedule
+#endif
 __host__ __device__ __forceinline__ void sha512_env_block2(uint64_t W[16], const uint8_t* m) {
   // bytes 128 .. 148 of R || A || M = M[64 .. 84]; then 0x80, zeros, the 128-bit length 149 * 8
 #pragma unroll
@@ -325,9 +328,6 @@ __host__ __device__ __forceinline__ void sha512_ram85(uint32_t out[16], const ui
   const uint32_t w2h = (uint32_t)__builtin_amdgcn_readfirstlane((int)HI32(W[2]));
   const bool same = LO32(W[0]) == w0l && HI32(W[0]) == w0h && LO32(W[1]) == w1l && HI32(W[1]) == w1h &&
                     LO32(W[2]) == w2l && HI32(W[2]) == w2h;
-#ifndef PBFT_SALU_SCHED
-#define PBFT_SALU_SCHED 1  // A/B: 0 = no wave-uniform scalar schedule
-#endif
   if (PBFT_SALU_SCHED && __all(same)) {
     // wave-uniform schedule: plain 64-bit shifts (s_lshr_b64 / s_lshl_b64 / s_or_b64 on the SALU)
     uint64_t Ws[16];
