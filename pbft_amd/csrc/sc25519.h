@@ -2,8 +2,9 @@
 //
 //  * sc_lt_L           : ed25519-dalek 1.0.1 check_scalar (reject s >= L)
 //  * sc_reduce512      : curve25519-dalek 3.2.1 Scalar::from_hash
-//                        (64-byte digest, little-endian, reduced mod L) via
-//                        Barrett reduction in radix 2^32 (HAC 14.42, k = 8)
+//                        (64-byte digest, little-endian, reduced mod L) by
+//                        folding 2^252 = -delta in radix 2^21 (sc_reduce512_fold);
+//                        Barrett in radix 2^32 (HAC 14.42, k = 8) kept for A/B
 //  * sc_muladd         : (a*b + c) mod L, RFC 8032 signing (s = r + k*a)
 // Cargo.lock:604-614 (curve25519-dalek), :668-679 (ed25519-dalek).
 #pragma once
@@ -69,8 +70,8 @@ FE_FN void sc_cond_sub_L(uint32_t r[9]) {
   }
 }
 
-// x: 16 LE words (a 512-bit little-endian integer); out: x mod L, 8 LE words
-FE_FN void sc_reduce512(uint32_t out[8], const uint32_t x[16]) {
+// x: 16 LE words (a 512-bit little-endian integer); out: x mod L, 8 LE words (Barrett; A/B of the fold below)
+FE_FN void sc_reduce512_barrett(uint32_t out[8], const uint32_t x[16]) {
   const uint32_t mu[9] = SC_MU_WORDS;
   const uint32_t Lw[8] = SC_L_WORDS;
   uint32_t q1[9];
@@ -95,6 +96,93 @@ FE_FN void sc_reduce512(uint32_t out[8], const uint32_t x[16]) {
   sc_cond_sub_L(r);
 #pragma unroll
   for (int i = 0; i < 8; ++i) out[i] = r[i];
+}
+
+// x mod L by folding, for the verifier's challenge scalar (the same value as sc_reduce512).
+// 2^252 = -delta (mod L), delta = L - 2^252 < 2^125, and 252 = 12 x 21: the 512-bit input as 25 signed
+// limbs of radix 2^21; every limb at or above 2^252 is multiplied by the signed radix-2^21 digits of -delta
+// (|digit| < 2^20) and added 12 limbs lower.  Signed carries between the folds keep every multiplied limb
+// inside int32 (one v_mad_i64_i32 per product, 90 in all) and every column below 2^50; no 96-bit
+// accumulators and no compare-and-select carries as in the Barrett form.  Bounds: after the fold of limbs
+// 18..24 the limbs 6..16 are < 2^43.6, carried to [-2^20, 2^20) (limb 17 < 2^28.2); after the fold of
+// 12..17 limbs 0..11 are < 2^49; two more folds of limb 12 (< 2^8, then a carry of +-2) and floor carries
+// leave limbs 0..10 in [0, 2^21) and |limb 11| <= 2^20 + 2, so v = sum < 2^252 < L and v > -2^251 > -L:
+// one conditional +L gives the canonical residue.  Host harness: test_reduce512 (3,000 random 512-bit values
+// and edge cases vs Python).
+FE_FN void sc_reduce512_fold(uint32_t out[8], const uint32_t x[16]) {
+  const int32_t C[6] = {666643, 470296, 654183, -997805, 136657, -683901};  // -delta, signed radix 2^21
+  int64_t s[25];
+#pragma unroll
+  for (int i = 0; i < 24; ++i) {
+    const int b = 21 * i, q = b >> 5, sh = b & 31;
+    const uint64_t v = ((uint64_t)(q + 1 < 16 ? x[q + 1] : 0u) << 32) | x[q];
+    s[i] = (int64_t)((v >> sh) & 0x1FFFFFu);
+  }
+  s[24] = (int64_t)(x[15] >> 24);
+  auto fold = [&](int i) {
+    const int32_t si = (int32_t)s[i];
+#pragma unroll
+    for (int j = 0; j < 6; ++j) s[i - 12 + j] += (int64_t)si * C[j];
+    s[i] = 0;
+  };
+  auto carry = [&](int i) {  // signed, rounding: s[i] into [-2^20, 2^20)
+    const int64_t c = (s[i] + (1 << 20)) >> 21;
+    s[i + 1] += c;
+    s[i] -= c * (1 << 21);
+  };
+#pragma unroll
+  for (int i = 24; i >= 18; --i) fold(i);
+#pragma unroll
+  for (int i = 6; i <= 16; ++i) carry(i);
+#pragma unroll
+  for (int i = 17; i >= 12; --i) fold(i);
+#pragma unroll
+  for (int i = 0; i <= 11; ++i) carry(i);
+  fold(12);
+#pragma unroll
+  for (int i = 0; i <= 11; ++i) carry(i);
+  fold(12);
+#pragma unroll
+  for (int i = 0; i <= 10; ++i) {  // floor carries: limbs 0..10 in [0, 2^21)
+    const int64_t c = s[i] >> 21;
+    s[i + 1] += c;
+    s[i] -= c * (1 << 21);
+  }
+  // pack limbs 0..10 (231 bits) + limb 11 * 2^231 into a 288-bit two's complement value
+  uint32_t w[9];
+  uint64_t acc = 0;
+  int nb = 0, k = 0;
+#pragma unroll
+  for (int i = 0; i <= 10; ++i) {
+    acc |= (uint64_t)s[i] << nb;
+    nb += 21;
+    if (nb >= 32) { w[k++] = (uint32_t)acc; acc >>= 32; nb -= 32; }
+  }
+  // k == 7, nb == 7: bits 224..230 in acc
+  w[7] = (uint32_t)acc | (uint32_t)((uint64_t)s[11] << 7);
+  w[8] = (uint32_t)(s[11] >> 25);
+  // negative: + L (then < L)
+  const uint32_t Lw[8] = SC_L_WORDS;
+  const uint32_t m = 0u - (w[8] >> 31);
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t t = (uint64_t)w[i] + (Lw[i] & m) + c;
+    out[i] = (uint32_t)t;
+    c = (uint32_t)(t >> 32);
+  }
+}
+
+#ifndef PBFT_SC_BARRETT
+#define PBFT_SC_BARRETT 0
+#endif
+// x mod L (curve25519-dalek Scalar::from_hash): the fold; PBFT_SC_BARRETT=1 for the Barrett form
+FE_FN void sc_reduce512(uint32_t out[8], const uint32_t x[16]) {
+#if PBFT_SC_BARRETT
+  sc_reduce512_barrett(out, x);
+#else
+  sc_reduce512_fold(out, x);
+#endif
 }
 
 // out = (a*b + c) mod L; all 8-word little-endian, a,b,c < 2^256
