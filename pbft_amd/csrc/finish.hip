@@ -80,11 +80,7 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
 #else
   if constexpr (LV == 6) {
     // every lane holds the wave's product: the variable-time divsteps never diverge (inv25519.h)
-#if PBFT_TREE_INV_CT  // A/B: the constant-time divsteps for the wave-uniform product too
-    fe_invert_gcd(inv, t);
-#else
     fe_invert_var(inv, t);
-#endif
   } else {
     fe_invert_gcd(inv, t);  // divsteps: ~19k instructions instead of ~44k on the serial chain
   }

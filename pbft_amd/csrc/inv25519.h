@@ -47,16 +47,9 @@ __host__ __device__ __forceinline__ int32_t divsteps30(int32_t zeta, uint32_t f,
     // g odd: g += f (zeta >= 0) or g -= f (zeta < 0), and the same on the g row of t.
     // ((x ^ c1) - c1) & c2 == ((x ^ c1) & c2) - c3: one v_bitop3 + one v_add3 per row
     // (18 VALU per divstep instead of 23 -- the chain of every inversion)
-#if PBFT_DIVSTEP23  // A/B: the round-1 formulation (23 VALU per divstep)
-    g += ((f ^ c1) - c1) & c2;
-    q += ((u ^ c1) - c1) & c2;
-    r += ((v ^ c1) - c1) & c2;
-    (void)n3;
-#else
     g = g + ((f ^ c1) & c2) + n3;
     q = q + ((u ^ c1) & c2) + n3;
     r = r + ((v ^ c1) & c2) + n3;
-#endif
     zeta = (zeta ^ (int32_t)c3) - 1;
     f += g & c3;
     u = (u + (q & c3)) << 1;
@@ -219,30 +212,10 @@ __host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t
   return eta;
 }
 
-// Wave-uniform values moved to SGPRs (v_readfirstlane): the code that depends only on them
-// then runs on the scalar unit -- short-latency SALU ops and scalar branches instead of a
-// 64-wide VALU chain.  PBFT_INV_SALU = 1: the divsteps of each batch (the serial part);
-// 2: the whole inversion state (batches, matrix updates, normalisation); 0: none (the default:
-// measured no faster -- 4k latency round 0.0914 ms (0) vs 0.0934 (1) vs 0.0973 (2), profiles/r02_ab_log.md).
-#ifndef PBFT_INV_SALU
-#define PBFT_INV_SALU 0
-#endif
-__host__ __device__ __forceinline__ int32_t inv_uniform(int32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_readfirstlane(x);
-#else
-  return x;
-#endif
-}
-
 // out = z^-1 (0 -> 0) for a wave-uniform z (see above); z as for fe_invert_gcd
 __host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z) {
   uint32_t w[8];
   fe_to_words(w, z);
-#if PBFT_INV_SALU >= 2
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = (uint32_t)inv_uniform((int32_t)w[i]);
-#endif
   s30 f, g, d, e;
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
@@ -259,15 +232,9 @@ __host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z) {
     int32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) nz |= g.v[i];
-#if PBFT_INV_SALU >= 1
-    if (inv_uniform(nz) == 0) break;
-    int32_t t[4];
-    eta = divsteps30_var(eta, (uint32_t)inv_uniform(f.v[0]), (uint32_t)inv_uniform(g.v[0]), t);
-#else
     if (nz == 0) break;
     int32_t t[4];
     eta = divsteps30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
-#endif
     inv_update_de(d, e, t);
     inv_update_fg(f, g, t);
   }

@@ -573,8 +573,6 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     });
 #if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
     zi = t;
-#elif PBFT_TREE_INV_CT  // A/B: the constant-time divsteps for the wave-uniform product too
-    fe_invert_gcd(zi, t);
 #else
     fe_invert_var(zi, t);
 #endif
