@@ -123,7 +123,9 @@ int pbft_verify_batch_device_pipelined(pbft_ctx *ctx, const uint8_t *d_R, const 
 int pbft_verify_votes(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
                       const uint32_t *env_idx, const uint8_t *envelopes, uint32_t n_env, uint64_t N,
                       uint64_t *bitmap_out);
-/* Device-resident votes form; d_envelopes readable for n_env * 85 + 16 bytes.  Enqueue only. */
+/* Device-resident votes form; d_envelopes readable for n_env * 85 + 16 bytes.  Enqueue only.  Both votes forms
+ * first expand each envelope's share of the SHA-512 (block 2's message schedule, 512 B per envelope) into a
+ * context buffer that grows on first use for a bigger table (so not first called inside a stream capture). */
 int pbft_verify_votes_device(pbft_ctx *ctx, const uint8_t *d_R, const uint8_t *d_S, const uint16_t *d_key_idx,
                              const uint32_t *d_env_idx, const uint8_t *d_envelopes, uint32_t n_env, uint64_t N,
                              uint64_t *d_bitmap, void *stream);
