@@ -116,6 +116,12 @@ def test_reduce512(hh):
     L = E.L
     vals = [0, 1, L - 1, L, L + 1, 2 * L, 3 * L - 1, 2**512 - 1, 2**256, 2**253] + [rnd.randrange(2**512)
                                                                                      for _ in range(3000)]
+    # the radix-2^21 fold (sc_reduce512_fold): multiples of L and of 2^252 +- small, limbs all ones / zero,
+    # values whose folds cancel (the result lands just below 0 or just above L before the final +L)
+    vals += [k * L + r for k in (1, 2**7, 2**100, 2**259 - 1) for r in (0, 1, L - 1) if k * L + r < 2**512]
+    vals += [j * 2**252 + r for j in (1, 2, 2**259 - 1) for r in (0, 1, 2**252 - 1)]
+    vals += [(2**(21 * i) - 1) for i in range(1, 25)] + [2**512 - 2**(21 * i) for i in range(1, 25)]
+    vals += [rnd.randrange(2**252) * L % 2**512 for _ in range(200)]
     for x in vals:
         out = ctypes.create_string_buffer(32)
         hh.hh_reduce512(x.to_bytes(64, "little"), out)
