@@ -516,6 +516,13 @@ def test_votes_form_matches_oracle_and_soa(gv, coracle):
     for m in (4096, 1000):                                                # latency-mode kernel
         g3 = bitmap_to_bool(gv.verify_votes(R2[:m], S2[:m], K2[:m], ei[:m], env), m)
         assert (g3 == exp[:m]).all(), m
+    # shuffled: every wave mixes envelopes, so block 2's schedule comes from the per-envelope table (votes form)
+    # or per lane (SoA) instead of the scalar unit -- the same bits
+    perm = rng.permutation(n)
+    g6 = bitmap_to_bool(gv.verify_votes(R2[perm], S2[perm], K2[perm], ei[perm], env), n)
+    assert (g6 == exp[perm]).all()
+    g7 = bitmap_to_bool(gv.verify(SigBatch(R2[perm], S2[perm], K2[perm], M2[perm], 85)), n)
+    assert (g7 == exp[perm]).all()
     # 2^19 + 3 signatures: chunked H2D path; equals the SoA host path on the same rows
     reps = (1 << 19) // n + 1
     RR, SS, KK, II = (np.concatenate([a] * reps)[: (1 << 19) + 3] for a in (R2, S2, K2, ei))
