@@ -65,7 +65,8 @@ int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *k
  * table and its CURRENT key set (reference-counted; a later set_keys on either
  * context replaces only that context's key set), with its own HIP stream,
  * staging and workspace: one context per host thread / in-flight stream for
- * pipelined serving of small batches (BASELINE config #5). */
+ * pipelined serving of small batches (BASELINE config #5).  The clone starts
+ * with the parent's tuning options (pbft_verify_set_option). */
 int pbft_verify_ctx_clone(pbft_ctx *parent, pbft_ctx **out);
 
 /* Blocking batch verify from host buffers (PCIe copies included).
@@ -161,12 +162,15 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *   PBFT_OPT_FINISH_TREE          cross-lane levels of the finish's batch inversion: 0 (one inversion per lane)
  *                                 or 6 (one per wave); any other value = by batch size
  *   PBFT_OPT_LAT_SPLIT            lanes per signature of the latency-mode kernel: 4 or 8; any other value = by
- *                                 batch size (8 up to 8,192 signatures, else 4) */
+ *                                 batch size (8 up to 8,192 signatures, else 4)
+ *   PBFT_OPT_KERNEL_TIMING        1 (default): two HIP events bracket every launch for pbft_last_kernel_ms; 0: none
+ *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers) */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
 #define PBFT_OPT_FINISH_TREE 4
 #define PBFT_OPT_LAT_SPLIT 5
+#define PBFT_OPT_KERNEL_TIMING 7
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

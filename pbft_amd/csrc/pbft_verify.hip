@@ -105,6 +105,7 @@ struct pbft_ctx {
   int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
   int fin_tree = -1;                   // finish cross-lane tree levels (0 / 6; -1 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
+  bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   void adopt(keyset* k) {
     keyset_release(ks);
@@ -227,9 +228,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     c->half ^= 1;
   }
   if (c->fin_pending[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));  // a pipelined finish still reading half h
-#if !PBFT_NO_LAUNCH_EVENTS
-  HIP_TRY(hipEventRecord(c->ev0, st));
-#endif
+  if (c->timing) HIP_TRY(hipEventRecord(c->ev0, st));
   const uint64_t W = c->work_n;  // layout (>= N)
   uint8_t* hw = c->d_work + (h ? half1_offset(W) : 0);
   const bool latency_mode = N < c->split_below;
@@ -250,9 +249,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
                                 : launch_comb_small(a));
   HIP_TRY(hipGetLastError());
   if (fst) {
-#if !PBFT_NO_LAUNCH_EVENTS
-    HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
-#endif
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
     HIP_TRY(hipEventRecord(c->ev_comb, st));
     HIP_TRY(hipStreamWaitEvent(fst, c->ev_comb, 0));
     st = fst;
@@ -275,9 +272,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     c->fin_pending[h] = true;
     return PBFT_OK;
   }
-#if !PBFT_NO_LAUNCH_EVENTS
-  HIP_TRY(hipEventRecord(c->ev1, st));
-#endif
+  if (c->timing) HIP_TRY(hipEventRecord(c->ev1, st));
   return PBFT_OK;
 }
 
@@ -621,6 +616,13 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
     ++parent->ks->refs;
     c->adopt(parent->ks);
   }
+  // the parent's tuning options (pbft_verify_set_option)
+  c->split_below = parent->split_below;
+  c->fin_m = parent->fin_m;
+  c->fin_tree = parent->fin_tree;
+  c->lat_split = parent->lat_split;
+  c->timing = parent->timing;
+  c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
 }
@@ -654,7 +656,9 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
 static int finish_async(pbft_ctx* c) {
   memcpy(c->async_out, c->h_bitmap, c->async_words * 8);
   c->in_flight = false;
-  (void)hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1);
+  // (only with timing events: on events never recorded the call fails and would leave an error that the next
+  // launch's hipGetLastError reports; a failure here is cleared for the same reason)
+  if (c->timing && hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1) != hipSuccess) (void)hipGetLastError();
   return PBFT_OK;
 }
 
@@ -920,6 +924,7 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
       return PBFT_OK;
     case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 6) ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
+    case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");
@@ -934,10 +939,10 @@ int pbft_verify_ctx_info(pbft_ctx* c, uint32_t* pb, uint32_t* pa, uint32_t* n_ke
 }
 
 float pbft_last_kernel_ms(pbft_ctx* c) {
-  if (!c) return -1.f;
+  if (!c || !c->timing) return -1.f;
   float ms = -1.f;
-  if (hipEventSynchronize(c->ev1) != hipSuccess) return -1.f;
-  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) return -1.f;
+  if (hipEventSynchronize(c->ev1) != hipSuccess) { (void)hipGetLastError(); return -1.f; }
+  if (hipEventElapsedTime(&ms, c->ev0, c->ev1) != hipSuccess) { (void)hipGetLastError(); return -1.f; }
   c->last_ms = ms;
   return ms;
 }

@@ -248,6 +248,22 @@ def test_device_entry_point(gv, golden):
         got = bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n)
         assert (got == b["expected"].astype(bool)).all(), stride
         assert gv.last_kernel_ms() > 0
+        # PBFT_OPT_KERNEL_TIMING = 0: no timing events around the launch (same bits, no kernel time)
+        gv.set_option(gv.OPT_KERNEL_TIMING, 0)
+        try:
+            dB.zero_()
+            gv.verify_device(dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(), 85, stride, n,
+                             dB.data_ptr(), st.cuda_stream)
+            st.synchronize()
+            assert (bitmap_to_bool(dB.cpu().numpy().view(np.uint64), n) == b["expected"].astype(bool)).all()
+            assert gv.last_kernel_ms() == -1
+            # the host-buffer path (submit / wait) twice in a row: no stale HIP error from the missing events
+            from pbft_amd import SigBatch
+            for _ in range(2):
+                bm = gv.verify(SigBatch(b["R"], b["S"], b["key_idx"], b["msg"], 85))
+                assert (bitmap_to_bool(bm, n) == b["expected"].astype(bool)).all()
+        finally:
+            gv.set_option(gv.OPT_KERNEL_TIMING, 1)
 
 
 def test_digests_match_hashlib(gv):

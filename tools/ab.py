@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--per-launch-events", action="store_true", help="also record a torch event pair per launch")
     ap.add_argument("--sizes", default="", help="comma list of batch sizes (default: the whole round)")
     ap.add_argument("--votes", action="store_true", help="time the votes form (pbft_verify_votes_device)")
+    ap.add_argument("--latency", action="store_true", help="p50 wall time of single synchronized launches")
     a = ap.parse_args()
     import torch
     import bench
@@ -67,6 +68,23 @@ def main():
         ctxs.append((p, lib, c))
     sizes = [int(x) for x in a.sizes.split(",")] if a.sizes else [n]
     full = n
+    if a.latency:
+        import time
+        for n in sizes:
+            lat = {p: [] for p in a.libs}
+            for r in range(a.rounds * 25):
+                for p, lib, c in ctxs:
+                    torch.cuda.synchronize()
+                    t = time.perf_counter()
+                    assert lib.pbft_verify_batch_device(c, dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(),
+                                                        85, 85, n, dB.data_ptr(), st.cuda_stream) == 0
+                    st.synchronize()
+                    lat[p].append((time.perf_counter() - t) * 1e3)
+            for p, lib, c in ctxs:
+                t = np.array(lat[p][10:])
+                print(f"N={n:8d} {os.path.basename(p):32s} p50 {np.median(t):.4f} ms  p99 {np.percentile(t, 99):.4f}",
+                      flush=True)
+        return
     for n in sizes:
       res = {p: [] for p in a.libs}
       for r in range(a.rounds):
