@@ -119,8 +119,43 @@ FE_FN uint32_t lane_mask(bool c) {
 //   a = (Y-X) qa, b = (Y+X) qb, c = T k, D = Z  (each half its usual value)
 //   E = b - a, F = D -+ c, G = D +- c, H = b + a
 //   X3 = E F, Y3 = G H, Z3 = F G, T3 = E H  (= the usual outputs / 4)
+#ifndef PBFT_MADD_V2
+#define PBFT_MADD_V2 1
+#endif
+// 2p - k per limb for canonical k (the conditional negation of the entry's d*x*y)
+FE_FN void fe_cneg_canon(fe& out, const fe& k, uint32_t m) {
+  fe nk;
+  fe_neg(nk, k);
+#pragma unroll
+  for (int i = 0; i < 10; ++i) out.v[i] = (k.v[i] & ~m) | (nk.v[i] & m);  // one v_bitop3 per limb
+}
 template <bool WITH_T = true>
 FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& k, bool neg) {
+#if PBFT_MADD_V2
+  // r02 form below, re-ordered for fewer VALU instructions per step (profiles/r03_step_hist.txt):
+  //  * the sign of d*x*y is applied to the (canonical) table limbs, k' = +-k (one v_bitop3 + one v_sub per
+  //    limb), so F = D - c and G = D + c never swap (the swap cost a v_bitop3 + two v_xor per limb);
+  //  * the four output products share their 19x-premultiplied operands: X3 = F E, T3 = H E, Y3 = H G,
+  //    Z3 = F G -- {E, G} is a vertex cover of the 4-cycle E-F-G-H, so fe_mul_cols premultiplies 2 vectors
+  //    (not 3) and doubles the odd limbs of 2 (not 4).
+  // Bounds (every 19x operand < 2^32 / 19, every column < 2^64) in tools/limb_bounds.py ("madd v2").
+  fe a, b, c, t, kk;
+  fe_cneg_canon(kk, k, lane_mask(neg));
+  fe_sub(t, p.Y, p.X);
+  fe_mul(a, t, qa);
+  fe_add(t, p.Y, p.X);
+  fe_mul(b, t, qb);
+  fe_mul(c, p.T, kk);
+  fe e, f, g, h;
+  fe_sub(e, b, a);
+  fe_sub(f, p.Z, c);
+  fe_add(g, p.Z, c);
+  fe_add(h, b, a);
+  fe_mul(r.X, f, e);
+  fe_mul(r.Y, h, g);
+  fe_mul(r.Z, f, g);
+  if constexpr (WITH_T) fe_mul(r.T, h, e);
+#else
   fe a, b, c, t;
   const uint32_t m = lane_mask(neg);
   fe_sub(t, p.Y, p.X);
@@ -143,6 +178,7 @@ FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& 
   fe_mul(r.Y, g, h);
   fe_mul(r.Z, dmc, dpc);
   if constexpr (WITH_T) fe_mul(r.T, e, h);
+#endif
 }
 
 // r = p + sign * q, entry q as stored (the swap by masks)

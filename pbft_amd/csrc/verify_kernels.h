@@ -114,11 +114,34 @@ struct steps {
 // the XOR swizzle spreads the owner lanes' ds_read_b128 over all banks.
 // idx (entry index in 128-B units from `base`) is fetched from its owner lane
 // with ds_bpermute (one base address + immediate offsets 32 q).
+#ifndef PBFT_DMA_MAD
+#define PBFT_DMA_MAD 1
+#endif
+// 64-bit entry address base + coff + 128 e as ONE v_mad_u64_u32 (LLVM otherwise emits a zero-extending
+// v_mov, a v_lshlrev_b64 and a v_lshl_add_u64 per entry: 13.5 vs 4.9 cycles per wave-instruction group)
+__device__ __forceinline__ const uint8_t* entry_addr(uint64_t base_coff, uint32_t e) {
+#if defined(__HIP_DEVICE_COMPILE__) && PBFT_DMA_MAD
+  uint64_t a, cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(a), "=s"(cc) : "v"(e), "s"(128u), "v"(base_coff));
+  (void)cc;
+  return (const uint8_t*)(uintptr_t)a;
+#else
+  return (const uint8_t*)(uintptr_t)(base_coff + (uint64_t)e * 128u);
+#endif
+}
 __device__ __forceinline__ void dma_entry_lines(const uint8_t* base, uint32_t idx, int lane, uint32_t ebuf_lds) {
   const int k = lane >> 3;
   const uint32_t coff = (uint32_t)(((lane & 7) ^ k) << 4);
   const int baddr = k << 2;
-#if PBFT_DMA_BATCH
+#if PBFT_DMA_MAD
+  uint32_t e[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) e[q] = (uint32_t)__builtin_amdgcn_ds_bpermute(baddr + 32 * q, (int)idx);
+  const uint64_t bc = (uint64_t)(uintptr_t)base + coff;
+#pragma unroll
+  for (int q = 0; q < 8; ++q)
+    __builtin_amdgcn_global_load_lds(entry_addr(bc, e[q]), (lds_void*)(uintptr_t)(ebuf_lds + 1024u * q), 16, 0, 0);
+#elif PBFT_DMA_BATCH
   // all 8 index fetches first (distinct registers), then the 8 loads: one lgkm wait per step instead of
   // one per load -- the stalls matter where few waves share a SIMD (small shards, latency mode)
   uint32_t e[8];

@@ -48,6 +48,14 @@ for neg in (False, True):
     F, G = (g, f) if neg else (f, g)   # negative digit swaps d-c and d+c
     for nm, (x, y) in {"X3=F*E": (F, e), "Y3=G*H": (G, h), "Z3=dmc*dpc": (f, g), "T3=E*H": (e, h)}.items():
         print("madd neg=%d" % neg, nm, " log2 max col:", mulmax(x, y))
+# madd v2 (PBFT_MADD_V2, verify_core.h): k' = +-k (2p - k for a negative digit), F = D - c, G = D + c never
+# swap; X3 = F*E, T3 = H*E, Y3 = H*G, Z3 = F*G (second operand premultiplied by 19)
+for neg in (False, True):
+    kk = P2 if neg else C            # 2p - k <= 2p limb-wise (k canonical)
+    print("madd v2 neg=%d c=T*k'" % neg, " log2 max col:", mulmax(C, kk))
+e = sub(C, C, P2); F = sub(d, C, P2); G = add(d, C); h = add(C, C)
+for nm, (x, y) in {"X3=F*E": (F, e), "T3=H*E": (h, e), "Y3=H*G": (h, G), "Z3=F*G": (F, G)}.items():
+    print("madd v2", nm, " log2 max col:", mulmax(x, y))
 # doubling (dbl-2008-hwcd, a=-1): A=X^2, B=Y^2, C2=2Z^2, H=A+B, E=H-(X+Y)^2, G=A-B, F=C2+G
 xy = add(C, C)
 print("dbl (X+Y)^2         log2 max col:", mulmax(xy, xy))
