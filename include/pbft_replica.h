@@ -18,10 +18,16 @@
  *                                keys votes by the connection's peer_id, :346, :380)
  *   pbft_replica_push_frames     PbftHandler -> message_to_handler_event
  *                                src/handler.rs:533-548 for one connection
- *   pbft_replica_flush           the batched validation: every ready sub-window's
- *                                signatures in ONE GPU batch, then
- *                                State::insert_prepare/insert_commit
- *                                (src/state.rs:49-67) for accepted ones only
+ *   pbft_replica_flush_submit    the batched validation, non-blocking: every ready
+ *   pbft_replica_flush_poll      sub-window's signatures in ONE GPU batch (votes
+ *                                form, written into the verifier's pinned staging),
+ *                                launched by _submit; _poll, called from the same
+ *                                single-threaded loop as the reference's
+ *                                NetworkBehaviour::poll (src/behavior.rs:416-426),
+ *                                applies State::insert_prepare/insert_commit
+ *                                (src/state.rs:49-67) for accepted ones only once
+ *                                the bitmap is back.  pbft_replica_flush = both,
+ *                                blocking.
  *   pbft_replica_prepared        Pbft::prepared src/behavior.rs:177-182 with the
  *                                paper's 2f threshold (reference: len >= 1, TODO)
  *   pbft_replica_committed_local Pbft::committed_local :214-223 with 2f+1 commits
@@ -41,8 +47,17 @@
  *     its own count, so a phase-ordered run (Commits sent only after PREPARED)
  *     with f silent replicas progresses without a deadline flush;
  *   - flush(force = 1) (the caller's deadline) verifies everything pending;
+ *   - at most one batch is in flight per replica; pushes during the flight are
+ *     queued (a duplicate of an in-flight candidate is a duplicate) and go into
+ *     the next batch;
+ *   - a PrePrepare frame is taken only from the primary's own connection;
+ *   - events are decided when a batch is applied, whether or not the caller's
+ *     event buffer has room: undelivered events wait in the replica's queue for
+ *     the next flush / flush_poll, and GC never waits for delivery;
  *   - every candidate vote of a (kind, signer) is kept until one verifies (at
- *     most PBFT_MAX_CANDIDATES): a forged vote cannot pre-empt the real one;
+ *     most PBFT_MAX_CANDIDATES): a forged vote cannot pre-empt the real one
+ *     (votes are keyed by the authenticated sender, so only the signer's own
+ *     connection can fill its candidate slots);
  *     among accepted votes of one signer the last one wins (src/state.rs:56, :66);
  *   - seqs outside (h, h + log_window] are dropped; a window is erased once it
  *     is committed locally and every lower seq is too (h advances), or by
@@ -100,6 +115,17 @@ typedef int (*pbft_batch_verify_fn)(void *user, const uint8_t *R, const uint8_t 
                                     const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                                     uint64_t *bitmap_out);
 
+/* Optional asynchronous votes-form verifier (tests without a GPU, other backends): submit receives the
+ * batch in the layout of pbft_verify_votes_stage -- sig[N][64] (R || S), key_idx[N], env_idx[N] and
+ * envelopes[n_env][85]; envelopes[env_idx[i]] is signature i's message; buffers owned by the replica, valid
+ * until poll reports completion -- and returns 0 or a negative code; poll returns 1 once bitmap_out is
+ * written, 0 while running, < 0 on failure. */
+typedef int (*pbft_votes_submit_fn)(void *user, const uint8_t *sig, const uint16_t *key_idx, const uint32_t *env_idx,
+                                    const uint8_t *envelopes, uint32_t n_env, uint64_t N, uint64_t *bitmap_out);
+typedef int (*pbft_votes_poll_fn)(void *user);
+/* (pbft_replica_set_verifier / _set_votes_verifier: the last one installed serves the flushes; NULL
+ * uninstalls, and with neither the replica uses its GPU context.) */
+
 /* Optional request-digest override (tests without a GPU): Blake2b-512 of op. */
 typedef int (*pbft_digest_fn)(void *user, const uint8_t *op, uint32_t op_len, uint8_t digest_out[64]);
 
@@ -110,6 +136,8 @@ typedef int (*pbft_digest_fn)(void *user, const uint8_t *op, uint32_t op_len, ui
 int pbft_replica_create(pbft_ctx *ctx, uint32_t n, uint32_t self_id, const uint8_t *keys, pbft_replica **out);
 int pbft_replica_destroy(pbft_replica *r);
 int pbft_replica_set_verifier(pbft_replica *r, pbft_batch_verify_fn fn, void *user);
+int pbft_replica_set_votes_verifier(pbft_replica *r, pbft_votes_submit_fn submit, pbft_votes_poll_fn poll,
+                                    void *user);
 int pbft_replica_set_digest_fn(pbft_replica *r, pbft_digest_fn fn, void *user);
 /* H - h (default PBFT_DEFAULT_LOG_WINDOW; >= 1). */
 int pbft_replica_set_log_window(pbft_replica *r, uint64_t log_window);
@@ -135,6 +163,11 @@ int pbft_replica_on_pre_prepare(pbft_replica *r, uint64_t view, uint64_t seq, co
 int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]);
 
+/* N pushes in one call (kind[i], view[i], seq[i], digests[i][64], signer[i], sigs[i][64]); *queued = how many
+ * were queued.  Returns 0 or the first negative code. */
+int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, const uint64_t *view, const uint64_t *seq,
+                           const uint8_t *digests, const uint32_t *signer, const uint8_t *sigs, uint64_t *queued);
+
 /* Ingress straight from one connection's byte stream (include/pbft_wire.h):
  * decode UviBytes frames (src/protocol_config.rs:50-76 upgrade_inbound); signed
  * Prepare / Commit frames whose "replica" equals peer_idx (the authenticated
@@ -145,15 +178,27 @@ int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq
 int pbft_replica_push_frames(pbft_replica *r, uint32_t peer_idx, const uint8_t *stream, size_t len,
                              uint64_t *consumed, uint64_t *pushed, uint64_t *dropped);
 
-/* Verify every READY sub-window (force = every pending signature) in one batch,
- * insert the accepted votes, report newly reached events, and GC the committed
- * prefix.  *n_events = events written (<= max_events; later ones are dropped). */
+/* Non-blocking flush.  _submit: collect every READY sub-window (force = every pending candidate) into one
+ * batch and launch it; *n_rows = its signatures (0: nothing launched); PBFT_EBUSY while a batch is in flight.
+ * _poll: 1 once no batch is in flight -- the finished batch's accepted votes inserted, the events it
+ * decided queued, the committed prefix garbage-collected, and up to max_events queued events written to
+ * events (*n_events; the rest stay queued for the next call); 0 while the GPU is still working (nothing
+ * written); < 0 if the batch failed (its candidates are pending again).  Call _poll from the event loop
+ * (the reference's NetworkBehaviour::poll, src/behavior.rs:416-426). */
+int pbft_replica_flush_submit(pbft_replica *r, int force, uint64_t *n_rows);
+int pbft_replica_flush_poll(pbft_replica *r, pbft_round_event *events, uint32_t max_events, uint32_t *n_events);
+/* 1 while a batch is in flight, else 0. */
+int pbft_replica_in_flight(pbft_replica *r);
+
+/* Blocking flush: completes a batch still in flight (its events are queued), then _submit + wait + _poll. */
 int pbft_replica_flush(pbft_replica *r, int force, pbft_round_event *events, uint32_t max_events,
                        uint32_t *n_events);
 
 /* Stable checkpoint at seq (PBFT §4.3): h = max(h, seq); windows <= h erased. */
 int pbft_replica_stable_checkpoint(pbft_replica *r, uint64_t seq);
 
+/* Quorum predicates.  A garbage-collected seq reports 1 only if this replica committed it locally (a
+ * stable checkpoint raises h without deciding anything here). */
 int pbft_replica_prepared(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_committed_local(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_get_stats(pbft_replica *r, pbft_replica_stats *out);

@@ -85,14 +85,58 @@ int pbft_verify_batch_multi(pbft_ctx *const *ctxs, uint32_t n_ctx, const uint8_t
                             const uint16_t *key_idx, const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride,
                             uint64_t N, uint64_t *bitmap_out);
 
-/* Non-blocking form: enqueue copies + kernel; the host buffers must stay valid
- * until pbft_verify_wait returns.  One batch in flight per context. */
+/* Single-process multi-GPU round with the bitmap exchange on RCCL (SURVEY.md §8b "Conventions", §8e):
+ * pbft_multi_create takes one context per device (distinct devices, in rank order) and builds an RCCL
+ * communicator over them (ncclCommInitAll; RCCL is loaded at run time: librccl.so.1, the library torch and
+ * /opt/rocm ship).  pbft_verify_batch_device_multi: rank r verifies its shard -- n[r] signatures whose
+ * device-resident columns d_R[r], d_S[r], d_key_idx[r], d_msg[r] live on ctx r's device (the layout of
+ * pbft_verify_batch_device) -- into words [r * words_per_rank, r * words_per_rank + ceil(n[r] / 64)) of
+ * d_bitmap[r], then one ncclAllGather (in place, ncclUint64, words_per_rank words per rank) leaves every
+ * rank's d_bitmap[r] holding all n_ctx * words_per_rank words (rank-major, each rank's slice padded with
+ * zero words to words_per_rank >= ceil(n[r] / 64)).  Enqueued on each context's stream; pbft_multi_sync
+ * waits for all ranks.  (One process per GPU with torch.distributed is the other layout: bench.py.) */
+typedef struct pbft_multi pbft_multi;
+int pbft_multi_create(pbft_ctx *const *ctxs, uint32_t n_ctx, pbft_multi **out);
+int pbft_multi_destroy(pbft_multi *m);
+int pbft_verify_batch_device_multi(pbft_multi *m, const uint8_t *const *d_R, const uint8_t *const *d_S,
+                                   const uint16_t *const *d_key_idx, const uint8_t *const *d_msg, uint32_t msg_len,
+                                   uint32_t msg_stride, const uint64_t *n, uint64_t words_per_rank,
+                                   uint64_t *const *d_bitmap);
+int pbft_multi_sync(pbft_multi *m);
+
+/* Non-blocking form: enqueue copies + kernel, return; pbft_verify_poll / pbft_verify_wait complete it
+ * (bitmap_out is written by the call that observes completion).  One batch in flight per context.
+ * Host buffers in pinned memory (hipHostMalloc / hipHostRegister) are DMA'd in place and must stay valid
+ * until completion; pageable buffers are first copied into the context's pinned staging (a CPU memcpy,
+ * then asynchronous DMA), so they may be reused as soon as the call returns.  Replaces the blocking
+ * validate_prepare / validate_commit call inside inject_node_event (src/behavior.rs:345, :371) with a
+ * submit from, and a poll in, the swarm's single-threaded poll loop (src/behavior.rs:416-426). */
 int pbft_verify_batch_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
                             const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N,
                             uint64_t *bitmap_out);
-/* Returns 1 if the in-flight batch finished (bitmap written), 0 if still running. */
+/* Returns 1 if the in-flight batch finished (bitmap written; also 1 when nothing is in flight), 0 if still
+ * running, < 0 on error (the batch is then dropped). */
 int pbft_verify_poll(pbft_ctx *ctx);
 int pbft_verify_wait(pbft_ctx *ctx);
+
+/* Votes form, non-blocking (see pbft_verify_votes below for the layout): same buffer rules as
+ * pbft_verify_batch_async; complete with pbft_verify_poll / pbft_verify_wait. */
+int pbft_verify_votes_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
+                            const uint32_t *env_idx, const uint8_t *envelopes, uint32_t n_env, uint64_t N,
+                            uint64_t *bitmap_out);
+/* Zero-copy votes form: pbft_verify_votes_stage returns the context's pinned host staging for a batch of N
+ * signatures over n_env envelopes -- sig[N][64] (the 64-byte signature R || S as it travels), key_idx[N],
+ * env_idx[N], envelopes[n_env][85]; valid until the next stage call -- the caller fills it in place and
+ * pbft_verify_votes_submit launches it asynchronously (DMA straight from the staging, the kernels read R and S
+ * at a 64-byte stride).  This is what pbft_replica_flush_submit uses. */
+typedef struct {
+  uint8_t *sig;
+  uint16_t *key_idx;
+  uint32_t *env_idx;
+  uint8_t *envelopes;
+} pbft_votes_staging;
+int pbft_verify_votes_stage(pbft_ctx *ctx, uint64_t N, uint32_t n_env, pbft_votes_staging *out);
+int pbft_verify_votes_submit(pbft_ctx *ctx, uint64_t N, uint32_t n_env, uint64_t *bitmap_out);
 
 /* Device-resident form: all pointers are device pointers on the context's
  * device; stream is a hipStream_t (NULL = the context's stream).  Enqueues the

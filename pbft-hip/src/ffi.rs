@@ -15,6 +15,19 @@ pub struct pbft_ctx {
 pub struct pbft_replica {
     _private: [u8; 0],
 }
+#[repr(C)]
+pub struct pbft_multi {
+    _private: [u8; 0],
+}
+
+/// Pinned host staging of one votes-form batch (pbft_verify_votes_stage): filled in place, then submitted.
+#[repr(C)]
+pub struct pbft_votes_staging {
+    pub sig: *mut u8,
+    pub key_idx: *mut u16,
+    pub env_idx: *mut u32,
+    pub envelopes: *mut u8,
+}
 
 pub const PBFT_OK: c_int = 0;
 pub const PBFT_EINVAL: c_int = -1;
@@ -95,6 +108,17 @@ pub type pbft_batch_verify_fn = extern "C" fn(
     n: u64,
     bitmap_out: *mut u64,
 ) -> c_int;
+pub type pbft_votes_submit_fn = extern "C" fn(
+    user: *mut c_void,
+    sig: *const u8,
+    key_idx: *const u16,
+    env_idx: *const u32,
+    envelopes: *const u8,
+    n_env: u32,
+    n: u64,
+    bitmap_out: *mut u64,
+) -> c_int;
+pub type pbft_votes_poll_fn = extern "C" fn(user: *mut c_void) -> c_int;
 pub type pbft_digest_fn =
     extern "C" fn(user: *mut c_void, op: *const u8, op_len: u32, digest_out: *mut u8) -> c_int;
 
@@ -115,6 +139,18 @@ extern "C" {
                                    bitmap_out: *mut u64) -> c_int;
     pub fn pbft_verify_poll(ctx: *mut pbft_ctx) -> c_int;
     pub fn pbft_verify_wait(ctx: *mut pbft_ctx) -> c_int;
+    pub fn pbft_verify_votes_async(ctx: *mut pbft_ctx, r: *const u8, s: *const u8, key_idx: *const u16,
+                                   env_idx: *const u32, envelopes: *const u8, n_env: u32, n: u64,
+                                   bitmap_out: *mut u64) -> c_int;
+    pub fn pbft_verify_votes_stage(ctx: *mut pbft_ctx, n: u64, n_env: u32, out: *mut pbft_votes_staging) -> c_int;
+    pub fn pbft_verify_votes_submit(ctx: *mut pbft_ctx, n: u64, n_env: u32, bitmap_out: *mut u64) -> c_int;
+    pub fn pbft_multi_create(ctxs: *const *mut pbft_ctx, n_ctx: u32, out: *mut *mut pbft_multi) -> c_int;
+    pub fn pbft_multi_destroy(m: *mut pbft_multi) -> c_int;
+    pub fn pbft_verify_batch_device_multi(m: *mut pbft_multi, d_r: *const *const u8, d_s: *const *const u8,
+                                          d_key_idx: *const *const u16, d_msg: *const *const u8, msg_len: u32,
+                                          msg_stride: u32, n: *const u64, words_per_rank: u64,
+                                          d_bitmap: *const *mut u64) -> c_int;
+    pub fn pbft_multi_sync(m: *mut pbft_multi) -> c_int;
     pub fn pbft_verify_batch_device(ctx: *mut pbft_ctx, d_r: *const u8, d_s: *const u8, d_key_idx: *const u16,
                                     d_msg: *const u8, msg_len: u32, msg_stride: u32, n: u64, d_bitmap: *mut u64,
                                     stream: *mut c_void) -> c_int;
@@ -147,6 +183,8 @@ extern "C" {
                                out: *mut *mut pbft_replica) -> c_int;
     pub fn pbft_replica_destroy(r: *mut pbft_replica) -> c_int;
     pub fn pbft_replica_set_verifier(r: *mut pbft_replica, f: pbft_batch_verify_fn, user: *mut c_void) -> c_int;
+    pub fn pbft_replica_set_votes_verifier(r: *mut pbft_replica, submit: pbft_votes_submit_fn,
+                                           poll: pbft_votes_poll_fn, user: *mut c_void) -> c_int;
     pub fn pbft_replica_set_digest_fn(r: *mut pbft_replica, f: pbft_digest_fn, user: *mut c_void) -> c_int;
     pub fn pbft_replica_set_log_window(r: *mut pbft_replica, log_window: u64) -> c_int;
     pub fn pbft_envelope(out: *mut u8, kind: u8, view: u64, seq: u64, digest: *const u8);
@@ -157,6 +195,13 @@ extern "C" {
                              sig: *const u8) -> c_int;
     pub fn pbft_replica_push_frames(r: *mut pbft_replica, peer_idx: u32, stream: *const u8, len: usize,
                                     consumed: *mut u64, pushed: *mut u64, dropped: *mut u64) -> c_int;
+    pub fn pbft_replica_push_many(r: *mut pbft_replica, n: u64, kind: *const u8, view: *const u64, seq: *const u64,
+                                  digests: *const u8, signer: *const u32, sigs: *const u8,
+                                  queued: *mut u64) -> c_int;
+    pub fn pbft_replica_flush_submit(r: *mut pbft_replica, force: c_int, n_rows: *mut u64) -> c_int;
+    pub fn pbft_replica_flush_poll(r: *mut pbft_replica, events: *mut pbft_round_event, max_events: u32,
+                                   n_events: *mut u32) -> c_int;
+    pub fn pbft_replica_in_flight(r: *mut pbft_replica) -> c_int;
     pub fn pbft_replica_flush(r: *mut pbft_replica, force: c_int, events: *mut pbft_round_event, max_events: u32,
                               n_events: *mut u32) -> c_int;
     pub fn pbft_replica_stable_checkpoint(r: *mut pbft_replica, seq: u64) -> c_int;

@@ -85,6 +85,40 @@ impl SigBatch {
     }
 }
 
+/// Votes form of a round batch: signature i signs `envelopes[env_idx[i]]` (a window's Prepares / Commits
+/// all sign the same (kind, view, seq, digest) envelope), 70 bytes per signature over PCIe instead of 151.
+#[derive(Clone, Default)]
+pub struct VotesBatch {
+    pub r: Vec<[u8; 32]>,
+    pub s: Vec<[u8; 32]>,
+    pub key_idx: Vec<u16>,
+    pub env_idx: Vec<u32>,
+    pub envelopes: Vec<Envelope>,
+}
+
+impl VotesBatch {
+    pub fn len(&self) -> usize {
+        self.r.len()
+    }
+    pub fn is_empty(&self) -> bool {
+        self.r.is_empty()
+    }
+    /// The per-signature form (every signature carrying its own envelope), for verifiers without a votes form.
+    pub fn to_sig_batch(&self) -> SigBatch {
+        let mut b = SigBatch::default();
+        for i in 0..self.len() {
+            let e = self.envelopes.get(self.env_idx[i] as usize).copied().unwrap_or([0u8; ffi::PBFT_ENVELOPE_BYTES]);
+            let mut sig = [0u8; 64];
+            sig[..32].copy_from_slice(&self.r[i]);
+            sig[32..].copy_from_slice(&self.s[i]);
+            // an out-of-range envelope index is a 0 bit: an out-of-range key index gives the same
+            let k = if (self.env_idx[i] as usize) < self.envelopes.len() { self.key_idx[i] } else { u16::MAX };
+            b.push(k, e, &sig);
+        }
+        b
+    }
+}
+
 /// Accept bits, LSB-first in u64 words; bits past the batch length are 0.
 #[derive(Clone, Debug, Default, PartialEq, Eq)]
 pub struct Bitmap(pub Vec<u64>);
@@ -129,7 +163,9 @@ pub trait BatchVerifier {
 /// One HIP context (one MI355X).  Not `Sync`: one per thread; `try_clone` for more streams.
 pub struct GpuVerifier {
     ctx: *mut ffi::pbft_ctx,
-    inflight: Option<(u64, SigBatch, Bitmap)>,
+    // the library copies pageable batches into its pinned staging before the DMA, so only the output
+    // bitmap (written when the batch completes) has to outlive the call
+    inflight: Option<(u64, Bitmap)>,
     next: u64,
 }
 
@@ -140,6 +176,23 @@ impl GpuVerifier {
         let mut ctx = ptr::null_mut();
         check(unsafe { ffi::pbft_verify_ctx_create(device, &mut ctx) })?;
         Ok(GpuVerifier { ctx, inflight: None, next: 0 })
+    }
+    /// Non-blocking votes-form submit (pbft_verify_votes_async); complete it with `poll`.
+    pub fn submit_votes(&mut self, batch: &VotesBatch) -> Result<Ticket> {
+        if self.inflight.is_some() {
+            return Err(Error { code: ffi::PBFT_EBUSY, message: "one batch in flight per context".into() });
+        }
+        let n = batch.len();
+        let mut out = Bitmap::zeros(n);
+        check(unsafe {
+            ffi::pbft_verify_votes_async(self.ctx, batch.r.as_ptr() as *const u8, batch.s.as_ptr() as *const u8,
+                                         batch.key_idx.as_ptr(), batch.env_idx.as_ptr(),
+                                         batch.envelopes.as_ptr() as *const u8, batch.envelopes.len() as u32,
+                                         n as u64, out.0.as_mut_ptr())
+        })?;
+        self.next += 1;
+        self.inflight = Some((self.next, out));
+        Ok(Ticket(self.next))
     }
     /// Another context on the same GPU sharing this one's tables (own HIP stream).
     pub fn try_clone(&self) -> Result<Self> {
@@ -210,7 +263,7 @@ impl BatchVerifier for GpuVerifier {
         }
         let n = batch.len();
         let mut out = Bitmap::zeros(n);
-        // the host buffers must outlive the async call: they move into `inflight`
+        // pageable Vec buffers: copied into the context's pinned staging by the call, then DMA'd asynchronously
         check(unsafe {
             ffi::pbft_verify_batch_async(self.ctx, batch.r.as_ptr() as *const u8, batch.s.as_ptr() as *const u8,
                                          batch.key_idx.as_ptr(), batch.msg.as_ptr() as *const u8,
@@ -218,19 +271,22 @@ impl BatchVerifier for GpuVerifier {
                                          n as u64, out.0.as_mut_ptr())
         })?;
         self.next += 1;
-        self.inflight = Some((self.next, batch, out));
+        self.inflight = Some((self.next, out));
         Ok(Ticket(self.next))
     }
     fn poll(&mut self, ticket: &Ticket) -> Result<Option<Bitmap>> {
         match &self.inflight {
-            Some((id, _, _)) if *id == ticket.0 => {}
+            Some((id, _)) if *id == ticket.0 => {}
             _ => return Err(Error { code: ffi::PBFT_EINVAL, message: "unknown ticket".into() }),
         }
-        if check(unsafe { ffi::pbft_verify_poll(self.ctx) })? == 1 {
-            let (_, _, bm) = self.inflight.take().unwrap();
-            return Ok(Some(bm));
+        match check(unsafe { ffi::pbft_verify_poll(self.ctx) }) {
+            Ok(1) => Ok(Some(self.inflight.take().unwrap().1)),
+            Ok(_) => Ok(None),
+            Err(e) => {
+                self.inflight = None; // the library dropped the failed batch
+                Err(e)
+            }
         }
-        Ok(None)
     }
 }
 
@@ -319,32 +375,70 @@ pub enum RoundEvent {
 /// The round batcher + quorum state machine of one replica (include/pbft_replica.h).
 pub struct Replica {
     raw: *mut ffi::pbft_replica,
-    // a Rust BatchVerifier installed as the batch verify callback (None: the GPU context)
-    verifier: Option<Box<Box<dyn BatchVerifier>>>,
+    // a Rust BatchVerifier installed as the replica's asynchronous votes verifier (None: the GPU context)
+    verifier: Option<Box<Backend>>,
 }
 
-extern "C" fn verify_trampoline(user: *mut c_void, r: *const u8, s: *const u8, key_idx: *const u16,
-                                msg: *const u8, msg_len: u32, msg_stride: u32, n: u64,
-                                bitmap_out: *mut u64) -> c_int {
-    if msg_len as usize != ffi::PBFT_ENVELOPE_BYTES || msg_stride as usize != ffi::PBFT_ENVELOPE_BYTES {
-        return ffi::PBFT_EINVAL;
-    }
-    let v = unsafe { &mut *(user as *mut Box<dyn BatchVerifier>) };
+// A BatchVerifier behind the replica's submit / poll callbacks (pbft_replica_set_votes_verifier).
+struct Backend {
+    v: Box<dyn BatchVerifier>,
+    pending: Option<(Ticket, *mut u64, usize)>,
+}
+
+extern "C" fn votes_submit_trampoline(user: *mut c_void, sig: *const u8, key_idx: *const u16,
+                                      env_idx: *const u32, envelopes: *const u8, n_env: u32, n: u64,
+                                      bitmap_out: *mut u64) -> c_int {
+    let b = unsafe { &mut *(user as *mut Backend) };
     let n = n as usize;
-    let mut b = SigBatch::default();
+    let mut vb = VotesBatch::default();
     unsafe {
-        b.r.extend_from_slice(std::slice::from_raw_parts(r as *const [u8; 32], n));
-        b.s.extend_from_slice(std::slice::from_raw_parts(s as *const [u8; 32], n));
-        b.key_idx.extend_from_slice(std::slice::from_raw_parts(key_idx, n));
-        b.msg.extend_from_slice(std::slice::from_raw_parts(msg as *const Envelope, n));
+        for row in std::slice::from_raw_parts(sig as *const [u8; 64], n) {
+            let mut r = [0u8; 32];
+            let mut s = [0u8; 32];
+            r.copy_from_slice(&row[..32]);
+            s.copy_from_slice(&row[32..]);
+            vb.r.push(r);
+            vb.s.push(s);
+        }
+        vb.key_idx.extend_from_slice(std::slice::from_raw_parts(key_idx, n));
+        vb.env_idx.extend_from_slice(std::slice::from_raw_parts(env_idx, n));
+        vb.envelopes.extend_from_slice(std::slice::from_raw_parts(envelopes as *const Envelope, n_env as usize));
     }
-    match v.verify(b) {
-        Ok(bm) => {
-            unsafe { ptr::copy_nonoverlapping(bm.0.as_ptr(), bitmap_out, bm.0.len()) };
+    match b.v.submit(vb.to_sig_batch()) {
+        Ok(t) => {
+            b.pending = Some((t, bitmap_out, (n + 63) / 64));
             0
         }
         Err(e) => e.code,
     }
+}
+
+extern "C" fn votes_poll_trampoline(user: *mut c_void) -> c_int {
+    let b = unsafe { &mut *(user as *mut Backend) };
+    let (t, out, words) = match b.pending.take() {
+        Some(p) => p,
+        None => return 1,
+    };
+    match b.v.poll(&t) {
+        Ok(Some(bm)) => {
+            unsafe { ptr::copy_nonoverlapping(bm.0.as_ptr(), out, words.min(bm.0.len())) };
+            1
+        }
+        Ok(None) => {
+            b.pending = Some((t, out, words));
+            0
+        }
+        Err(e) => e.code,
+    }
+}
+
+fn round_events(ev: &[ffi::pbft_round_event]) -> Vec<RoundEvent> {
+    ev.iter().filter_map(|e| match e.kind {
+        ffi::PBFT_EVENT_PRE_PREPARED => Some(RoundEvent::PrePrepared { view: e.view, seq: e.seq }),
+        ffi::PBFT_EVENT_PREPARED => Some(RoundEvent::Prepared { view: e.view, seq: e.seq }),
+        ffi::PBFT_EVENT_COMMITTED_LOCAL => Some(RoundEvent::CommittedLocal { view: e.view, seq: e.seq }),
+        _ => None,
+    }).collect()
 }
 
 impl Replica {
@@ -358,11 +452,14 @@ impl Replica {
         })?;
         Ok(Replica { raw, verifier: None })
     }
-    /// Back the batcher with any BatchVerifier (e.g. CpuVerifier) instead of the GPU context.
+    /// Back the batcher with any BatchVerifier (e.g. CpuVerifier) instead of the GPU context; its
+    /// submit / poll become the replica's flush_submit / flush_poll.
     pub fn set_verifier(&mut self, v: Box<dyn BatchVerifier>) -> Result<()> {
-        let mut boxed: Box<Box<dyn BatchVerifier>> = Box::new(v);
-        let user = &mut *boxed as *mut Box<dyn BatchVerifier> as *mut c_void;
-        check(unsafe { ffi::pbft_replica_set_verifier(self.raw, verify_trampoline, user) })?;
+        let mut boxed = Box::new(Backend { v, pending: None });
+        let user = &mut *boxed as *mut Backend as *mut c_void;
+        check(unsafe {
+            ffi::pbft_replica_set_votes_verifier(self.raw, votes_submit_trampoline, votes_poll_trampoline, user)
+        })?;
         self.verifier = Some(boxed);
         Ok(())
     }
@@ -374,6 +471,21 @@ impl Replica {
                                              digest.as_ptr(), primary_sig.as_ptr(), ptr::null_mut())
         })?;
         Ok(rc == 1)
+    }
+    /// Many pushes at once (e.g. one decoded read of every connection); returns how many were queued.
+    pub fn push_many(&mut self, kind: &[u8], view: &[u64], seq: &[u64], digests: &[[u8; 64]], signer: &[u32],
+                     sigs: &[[u8; 64]]) -> Result<u64> {
+        let n = kind.len();
+        if view.len() != n || seq.len() != n || digests.len() != n || signer.len() != n || sigs.len() != n {
+            return Err(Error { code: ffi::PBFT_EINVAL, message: "push_many: column lengths differ".into() });
+        }
+        let mut q = 0u64;
+        check(unsafe {
+            ffi::pbft_replica_push_many(self.raw, n as u64, kind.as_ptr(), view.as_ptr(), seq.as_ptr(),
+                                        digests.as_ptr() as *const u8, signer.as_ptr(), sigs.as_ptr() as *const u8,
+                                        &mut q)
+        })?;
+        Ok(q)
     }
     /// A Prepare / Commit from the AUTHENTICATED peer `signer` (inject_node_event's peer_id).
     pub fn push(&mut self, kind: u8, view: u64, seq: u64, digest: &[u8; 64], signer: u32, sig: &[u8; 64])
@@ -393,18 +505,30 @@ impl Replica {
         })?;
         Ok(used as usize)
     }
-    /// Verify every ready sub-window in one batch and report new round events
-    /// (call from NetworkBehaviour::poll; force = the deadline).
+    /// Launch one batch of every ready sub-window (force = the deadline: everything pending) without
+    /// waiting for it; returns its signatures (0: nothing launched).  Err(PBFT_EBUSY) while one is in flight.
+    pub fn flush_submit(&mut self, force: bool) -> Result<u64> {
+        let mut n = 0u64;
+        check(unsafe { ffi::pbft_replica_flush_submit(self.raw, force as c_int, &mut n) })?;
+        Ok(n)
+    }
+    /// Call from NetworkBehaviour::poll (src/behavior.rs:416-426): None while the GPU works, else the round
+    /// events decided by the finished batch (and any still queued).
+    pub fn flush_poll(&mut self) -> Result<Option<Vec<RoundEvent>>> {
+        let mut ev = vec![ffi::pbft_round_event::default(); 4096];
+        let mut n = 0u32;
+        let rc = check(unsafe { ffi::pbft_replica_flush_poll(self.raw, ev.as_mut_ptr(), ev.len() as u32, &mut n) })?;
+        if rc == 0 {
+            return Ok(None);
+        }
+        Ok(Some(round_events(&ev[..n as usize])))
+    }
+    /// Blocking: verify every ready sub-window in one batch and report new round events.
     pub fn flush(&mut self, force: bool) -> Result<Vec<RoundEvent>> {
-        let mut ev = vec![ffi::pbft_round_event::default(); 1024];
+        let mut ev = vec![ffi::pbft_round_event::default(); 4096];
         let mut n = 0u32;
         check(unsafe { ffi::pbft_replica_flush(self.raw, force as c_int, ev.as_mut_ptr(), ev.len() as u32, &mut n) })?;
-        Ok(ev[..n as usize].iter().filter_map(|e| match e.kind {
-            ffi::PBFT_EVENT_PRE_PREPARED => Some(RoundEvent::PrePrepared { view: e.view, seq: e.seq }),
-            ffi::PBFT_EVENT_PREPARED => Some(RoundEvent::Prepared { view: e.view, seq: e.seq }),
-            ffi::PBFT_EVENT_COMMITTED_LOCAL => Some(RoundEvent::CommittedLocal { view: e.view, seq: e.seq }),
-            _ => None,
-        }).collect())
+        Ok(round_events(&ev[..n as usize]))
     }
     /// The replica index of an authenticated connection's PeerId (None: not a replica).
     pub fn peer_index(&self, peer_id: &[u8]) -> Option<u32> {
@@ -423,6 +547,42 @@ impl Replica {
 
 impl Drop for Replica {
     fn drop(&mut self) {
+        // destroy completes a batch in flight (through the installed verifier) before `verifier` is dropped
         unsafe { ffi::pbft_replica_destroy(self.raw) };
+    }
+}
+
+/// Several GPUs of this process with the round's bitmap words all-gathered on RCCL
+/// (pbft_multi_create / pbft_verify_batch_device_multi).
+pub struct MultiGpu {
+    raw: *mut ffi::pbft_multi,
+}
+
+impl MultiGpu {
+    /// One context per device, in rank order.
+    pub fn new(gpus: &[&GpuVerifier]) -> Result<Self> {
+        let ctxs: Vec<*mut ffi::pbft_ctx> = gpus.iter().map(|g| g.raw()).collect();
+        let mut raw = ptr::null_mut();
+        check(unsafe { ffi::pbft_multi_create(ctxs.as_ptr(), ctxs.len() as u32, &mut raw) })?;
+        Ok(MultiGpu { raw })
+    }
+    /// Enqueue: rank r verifies its device-resident shard; every rank's `d_bitmap[r]` then holds the round
+    /// (rank-major, `words_per_rank` words per rank).  # Safety: device pointers as in include/pbft_verify.h.
+    pub unsafe fn verify_device(&mut self, d_r: &[*const u8], d_s: &[*const u8], d_key_idx: &[*const u16],
+                                d_msg: &[*const u8], n: &[u64], words_per_rank: u64,
+                                d_bitmap: &[*mut u64]) -> Result<()> {
+        check(ffi::pbft_verify_batch_device_multi(self.raw, d_r.as_ptr(), d_s.as_ptr(), d_key_idx.as_ptr(),
+                                                  d_msg.as_ptr(), ffi::PBFT_ENVELOPE_BYTES as u32,
+                                                  ffi::PBFT_ENVELOPE_BYTES as u32, n.as_ptr(), words_per_rank,
+                                                  d_bitmap.as_ptr())).map(|_| ())
+    }
+    pub fn sync(&mut self) -> Result<()> {
+        check(unsafe { ffi::pbft_multi_sync(self.raw) }).map(|_| ())
+    }
+}
+
+impl Drop for MultiGpu {
+    fn drop(&mut self) {
+        unsafe { ffi::pbft_multi_destroy(self.raw) };
     }
 }

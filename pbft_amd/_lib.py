@@ -19,6 +19,8 @@ EXPORTS = (
     "pbft_verify_batch_device", "pbft_verify_reserve", "pbft_digest_blake2b512", "pbft_digest_sha256",
     "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms", "pbft_verify_ctx_info",
     "pbft_verify_set_option", "pbft_verify_batch_device_pipelined", "pbft_verify_votes", "pbft_verify_votes_device",
+    "pbft_verify_votes_async", "pbft_verify_votes_stage", "pbft_verify_votes_submit",
+    "pbft_multi_create", "pbft_multi_destroy", "pbft_verify_batch_device_multi", "pbft_multi_sync",
     # include/pbft_wire.h
     "pbft_uvi_encode", "pbft_uvi_decode", "pbft_wire_encode_json", "pbft_wire_encode_frame",
     "pbft_wire_decode_json", "pbft_wire_decode_votes", "pbft_records_pack", "pbft_verify_records_device",
@@ -80,6 +82,13 @@ def load() -> ctypes.CDLL:
         "pbft_verify_batch_device_pipelined": (i32, [vp, vp, vp, vp, vp, u32, u32, u64, vp, vp, vp]),
         "pbft_verify_votes": (i32, [vp, vp, vp, vp, vp, vp, u32, u64, vp]),
         "pbft_verify_votes_device": (i32, [vp, vp, vp, vp, vp, vp, u32, u64, vp, vp]),
+        "pbft_verify_votes_async": (i32, [vp, vp, vp, vp, vp, vp, u32, u64, vp]),
+        "pbft_verify_votes_stage": (i32, [vp, u64, u32, vp]),
+        "pbft_verify_votes_submit": (i32, [vp, u64, u32, vp]),
+        "pbft_multi_create": (i32, [vp, u32, ctypes.POINTER(vp)]),
+        "pbft_multi_destroy": (i32, [vp]),
+        "pbft_multi_sync": (i32, [vp]),
+        "pbft_verify_batch_device_multi": (i32, [vp, vp, vp, vp, vp, u32, u32, vp, u64, vp]),
         "pbft_uvi_encode": (ctypes.c_size_t, [u64, u8p]),
         "pbft_uvi_decode": (i32, [u8p, ctypes.c_size_t, vp, vp]),
         "pbft_wire_encode_json": (i32, [vp, vp, ctypes.c_size_t, vp]),

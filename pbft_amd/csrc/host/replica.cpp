@@ -1,19 +1,28 @@
 // Host-side PBFT verification state machine (include/pbft_replica.h): signed
 // envelopes, a (view, seq) round batcher that hands ready sub-windows of many
-// rounds to the GPU verifier in one batch, the quorum predicates, a
-// watermark-bounded log with garbage collection, and the PeerId -> key binding.
+// rounds to the GPU verifier in one NON-BLOCKING batch (votes form: one 85-byte
+// envelope per (kind, view, seq, digest), an envelope index per signature,
+// written straight into the verifier's pinned staging), the quorum predicates,
+// a watermark-bounded log with garbage collection, and the PeerId -> key binding.
 //
 // Mirrors src/state.rs (State: logs keyed by (view, seq), one vote per peer,
 // last write wins :56, :66) and src/behavior.rs (validate_* :126-195, prepared
 // :177-182, committed_local :214-223, the caller inject_node_event :304-412)
 // with the paper's thresholds (2f, 2f+1), commits keyed by (view, seq) instead of
 // view only (src/state.rs:22-23), and the signature checks the reference leaves
-// as TODOs (src/behavior.rs:127, :185).
+// as TODOs (src/behavior.rs:127, :185).  The reference calls its validators
+// synchronously from a single-threaded poll loop (inject_node_event :304, poll
+// :416-426); here a flush is split into pbft_replica_flush_submit (build the batch,
+// launch, return) and pbft_replica_flush_poll (apply the bitmap, emit events) so
+// that the loop never blocks on the GPU.
+#include <algorithm>
 #include <array>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <set>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -26,25 +35,96 @@ namespace {
 using Key = std::pair<uint64_t, uint64_t>;  // (view, seq)
 using Digest = std::array<uint8_t, 64>;
 
-struct Cand {
-  Digest digest;
-  uint8_t sig[64];
-};
+enum : uint8_t { V_PENDING = 0, V_IN_FLIGHT = 1 };
 
-// Votes of one kind in one round window.  Candidates stay pending per signer
-// until verified; an accepted vote replaces the signer's previous one
-// (HashMap<PeerId, _>::insert in src/state.rs:49-67).
+// Candidates of one kind in one round window, as columns in push order (a candidate leaves when its batch
+// completes, so between batches every candidate is pending and a batch takes a whole phase): the 64-byte
+// signatures are copied into the verifier's staging with one memcpy per phase.  Per signer: the candidate
+// count (flood bound) and the accepted digest (HashMap<PeerId, _>::insert, src/state.rs:49-67: the last
+// accepted vote of a signer wins).  Phase 0 of a window holds its PrePrepare candidates (signer = primary).
 struct Phase {
-  std::map<uint32_t, std::vector<Cand>> pending;
-  std::map<uint32_t, Digest> accepted;
+  std::vector<uint8_t> sig;   // [k][64] R || S
+  std::vector<uint16_t> who;  // signer
+  std::vector<uint32_t> dix;  // index into digs
+  std::vector<uint8_t> st;    // V_PENDING / V_IN_FLIGHT
+  std::vector<Digest> digs;   // distinct digests of the candidates (honest rounds: one)
+  std::vector<uint8_t> cnt;   // per signer: candidates
+  std::vector<uint32_t> acc;  // per signer: 1 + index into acc_digs (0: none)
+  std::vector<Digest> acc_digs;
+  std::vector<uint32_t> acc_cnt;  // signers per accepted digest
+  uint32_t distinct = 0;          // signers with an accepted vote or a candidate
+  uint32_t n_pending = 0;         // candidates not yet in a batch
+  size_t size() const { return who.size(); }
+  void init(uint32_t n) {
+    if (cnt.empty()) {
+      cnt.assign(n, 0);
+      acc.assign(n, 0);
+    }
+  }
+  bool has(uint32_t s) const { return !cnt.empty() && (cnt[s] || acc[s]); }
+  int64_t find_dig(const uint8_t* d) const {
+    for (size_t j = 0; j < digs.size(); ++j)
+      if (memcmp(digs[j].data(), d, 64) == 0) return (int64_t)j;
+    return -1;
+  }
+  void append(const uint8_t* d, int64_t j, uint32_t signer, const uint8_t* sg) {
+    if (j < 0) {
+      digs.emplace_back();
+      memcpy(digs.back().data(), d, 64);
+      j = (int64_t)digs.size() - 1;
+    }
+    sig.insert(sig.end(), sg, sg + 64);
+    who.push_back((uint16_t)signer);
+    dix.push_back((uint32_t)j);
+    st.push_back(V_PENDING);
+    ++n_pending;
+  }
+  // drop the first k candidates (a completed batch); re-index the digests of the rest
+  void drop_front(size_t k) {
+    if (k >= size()) {
+      sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
+      return;
+    }
+    sig.erase(sig.begin(), sig.begin() + 64 * k);
+    who.erase(who.begin(), who.begin() + k);
+    dix.erase(dix.begin(), dix.begin() + k);
+    st.erase(st.begin(), st.begin() + k);
+    std::vector<Digest> nd;
+    for (uint32_t& x : dix) {
+      size_t j = 0;
+      while (j < nd.size() && nd[j] != digs[x]) ++j;
+      if (j == nd.size()) nd.push_back(digs[x]);
+      x = (uint32_t)j;
+    }
+    digs.swap(nd);
+  }
+  void clear_candidates() {
+    sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
+    n_pending = 0;
+  }
+  uint32_t acc_index(const Digest& d) {  // index into acc_digs (appended if new)
+    for (size_t j = 0; j < acc_digs.size(); ++j)
+      if (acc_digs[j] == d) return (uint32_t)j;
+    acc_digs.push_back(d);
+    acc_cnt.push_back(0);
+    return (uint32_t)acc_digs.size() - 1;
+  }
 };
 
 struct Window {
-  std::vector<Cand> pp_pending;  // signed PrePrepare candidates (signer = primary of the view)
+  Phase ph[3];  // [0] PrePrepare candidates, [1] Prepare, [2] Commit
   bool have_pre_prepare = false;
   Digest digest{};
-  Phase ph[2];  // [0] Prepare, [1] Commit
   bool pre_prepared_reported = false, prepared_reported = false, committed_reported = false;
+};
+
+// One phase of the in-flight batch: rows [row0, row0 + count) are its first `count` candidates.
+struct Seg {
+  Key key;
+  uint64_t row0;
+  uint32_t count;
+  uint32_t env0;  // its envelopes: env0 + index into the phase's digs
+  uint8_t kind;   // 0 PrePrepare, 1 Prepare, 2 Commit
 };
 
 }  // namespace
@@ -54,87 +134,261 @@ struct pbft_replica {
   uint32_t n = 0, f = 0, self = 0;
   uint64_t current_view = 1;  // src/view.rs:5-8: the view starts at 1 (no view change)
   uint64_t h = 0;             // low watermark: every seq <= h is done (committed prefix or checkpoint)
-  uint64_t h_commit = 0;      // highest seq of the committed prefix
   uint64_t log_window = PBFT_DEFAULT_LOG_WINDOW;
   std::vector<uint8_t> keys;
   std::unordered_map<std::string, uint32_t> key_index;
   std::map<Key, Window> windows;
-  std::set<Key> dirty;  // windows whose events must be (re-)evaluated
+  std::set<Key> dirty;                    // windows whose events must be (re-)evaluated
+  std::deque<pbft_round_event> evq;       // decided, not yet delivered
+  std::map<uint64_t, uint64_t> done;      // seqs of current_view committed locally and GC'd: [lo, hi]
+  Key last_key{~0ull, ~0ull};             // push fast path: the last window looked up
+  Window* last_w = nullptr;
   pbft_batch_verify_fn verify_fn = nullptr;
   void* verify_user = nullptr;
+  pbft_votes_submit_fn vsub = nullptr;
+  pbft_votes_poll_fn vpoll = nullptr;
+  void* vuser = nullptr;
   pbft_digest_fn digest_fn = nullptr;
   void* digest_user = nullptr;
   pbft_replica_stats stats{};
+  // the batch in flight (at most one)
+  bool in_flight = false;
+  int in_flight_via = 0;  // 0 GPU context, 1 votes override, 2 SoA override (already complete)
+  std::vector<Seg> segs;
+  uint64_t rows = 0;
+  std::vector<uint64_t> bitmap;
+  // host buffers of the verifier overrides (the GPU path fills the context's pinned staging instead)
+  std::vector<uint8_t> hSig, hR, hS, hM, hE;
+  std::vector<uint16_t> hK;
+  std::vector<uint32_t> hI;
 };
 
 static uint32_t primary_of(const pbft_replica* r, uint64_t view) { return (uint32_t)(view % r->n); }
 
 static bool in_log(const pbft_replica* r, uint64_t seq) { return seq > r->h && seq - r->h <= r->log_window; }
 
-static uint32_t matching(const Window& w, const std::map<uint32_t, Digest>& votes, int64_t exclude = -1) {
+// accepted votes of phase p matching the window's digest (optionally not counting one signer)
+static uint32_t matching(const Window& w, const Phase& p, int64_t exclude = -1) {
   if (!w.have_pre_prepare) return 0;
-  uint32_t c = 0;
-  for (const auto& kv : votes)
-    if ((int64_t)kv.first != exclude && kv.second == w.digest) ++c;
-  return c;
+  for (size_t j = 0; j < p.acc_digs.size(); ++j) {
+    if (p.acc_digs[j] != w.digest) continue;
+    uint32_t c = p.acc_cnt[j];
+    if (exclude >= 0 && !p.acc.empty() && p.acc[exclude] == j + 1) --c;
+    return c;
+  }
+  return 0;
 }
 
 // prepared(m, v, n, i): pre-prepare + 2f matching prepares from distinct backups
 static bool is_prepared(const pbft_replica* r, uint64_t view, const Window& w) {
-  return w.have_pre_prepare && matching(w, w.ph[0].accepted, primary_of(r, view)) >= 2 * r->f;
+  return w.have_pre_prepare && matching(w, w.ph[1], primary_of(r, view)) >= 2 * r->f;
 }
 
 // committed-local(m, v, n, i): prepared + 2f+1 matching commits (possibly own)
 static bool is_committed_local(const pbft_replica* r, uint64_t view, const Window& w) {
-  return is_prepared(r, view, w) && matching(w, w.ph[1].accepted) >= 2 * r->f + 1;
-}
-
-// Distinct signers with an accepted or pending vote of this phase (optionally
-// excluding one signer, the primary for Prepares).
-static uint32_t distinct_signers(const Phase& p, int64_t exclude) {
-  uint32_t c = 0;
-  for (const auto& kv : p.accepted)
-    if ((int64_t)kv.first != exclude) ++c;
-  for (const auto& kv : p.pending)
-    if ((int64_t)kv.first != exclude && !kv.second.empty() && !p.accepted.count(kv.first)) ++c;
-  return c;
+  return is_prepared(r, view, w) && matching(w, w.ph[2]) >= 2 * r->f + 1;
 }
 
 // A sub-window closes on its own count: enough distinct signers for the quorum
 // (2f backups' Prepares / 2f+1 Commits) or every possible signer.
 static bool prepare_ready(const pbft_replica* r, uint64_t view, const Window& w) {
-  if (w.ph[0].pending.empty() || w.prepared_reported) return false;
-  const uint32_t c = distinct_signers(w.ph[0], primary_of(r, view));
+  const Phase& p = w.ph[1];
+  if (p.n_pending == 0 || w.prepared_reported) return false;
+  const uint32_t c = p.distinct - (p.has(primary_of(r, view)) ? 1 : 0);
   return c >= 2 * r->f || c + 1 >= r->n;
 }
 static bool commit_ready(const pbft_replica* r, const Window& w) {
-  if (w.ph[1].pending.empty() || w.committed_reported) return false;
-  const uint32_t c = distinct_signers(w.ph[1], -1);
-  return c >= 2 * r->f + 1 || c >= r->n;
+  const Phase& p = w.ph[2];
+  if (p.n_pending == 0 || w.committed_reported) return false;
+  return p.distinct >= 2 * r->f + 1 || p.distinct >= r->n;
 }
 
 static std::string key_str(const uint8_t* A) { return std::string((const char*)A, 32); }
 
+static Window& window_at(pbft_replica* r, const Key& k) {
+  if (r->last_w && r->last_key == k) return *r->last_w;
+  Window& w = r->windows[k];
+  r->last_key = k;
+  r->last_w = &w;
+  return w;
+}
+
+// seqs of the current view committed locally whose windows are gone (interval set)
+static void record_done(pbft_replica* r, uint64_t seq) {
+  auto it = r->done.upper_bound(seq);  // first interval starting after seq
+  if (it != r->done.begin()) {
+    auto p = std::prev(it);
+    if (seq <= p->second) return;  // already in
+    if (p->second + 1 == seq) {
+      p->second = seq;
+      if (it != r->done.end() && it->first == seq + 1) {
+        p->second = it->second;
+        r->done.erase(it);
+      }
+      return;
+    }
+  }
+  if (it != r->done.end() && it->first == seq + 1) {
+    const uint64_t hi = it->second;
+    r->done.erase(it);
+    r->done[seq] = hi;
+    return;
+  }
+  r->done[seq] = seq;
+}
+static bool is_done(const pbft_replica* r, uint64_t view, uint64_t seq) {
+  if (view != r->current_view) return false;
+  auto it = r->done.upper_bound(seq);
+  if (it == r->done.begin()) return false;
+  return seq <= std::prev(it)->second;
+}
+
 static void gc(pbft_replica* r) {
+  r->last_w = nullptr;  // windows may go away
   // committed prefix: h advances over consecutive committed windows of the current view
   for (;;) {
     auto it = r->windows.find({r->current_view, r->h + 1});
     if (it == r->windows.end() || !it->second.committed_reported) break;
+    record_done(r, r->h + 1);
     r->dirty.erase(it->first);
     r->windows.erase(it);
     ++r->h;
-    r->h_commit = r->h;
     ++r->stats.windows_gc;
   }
-  // anything at or below h (stable checkpoint, or stale views)
+  // anything at or below h (stable checkpoint, or stale views); the in-flight rows of an erased window are
+  // skipped when the batch completes
   for (auto it = r->windows.begin(); it != r->windows.end();) {
     if (it->first.second <= r->h) {
+      if (it->second.committed_reported && it->first.first == r->current_view) record_done(r, it->first.second);
       r->dirty.erase(it->first);
       it = r->windows.erase(it);
       ++r->stats.windows_gc;
     } else {
       ++it;
     }
+  }
+}
+
+// Events (pre-prepared, prepared :177-182, committed_local :214-223) of every dirty window, in (view, seq)
+// order, into the replica's queue: the decision is recorded whether or not the caller has room for it.
+static void evaluate(pbft_replica* r) {
+  for (const Key& k : r->dirty) {
+    auto wi = r->windows.find(k);
+    if (wi == r->windows.end()) continue;
+    Window& w = wi->second;
+    const uint64_t view = k.first, seq = k.second;
+    if (!w.pre_prepared_reported && w.have_pre_prepare) {
+      w.pre_prepared_reported = true;
+      r->evq.push_back({view, seq, PBFT_EVENT_PRE_PREPARED});
+    }
+    if (!w.prepared_reported && is_prepared(r, view, w)) {
+      w.prepared_reported = true;
+      r->evq.push_back({view, seq, PBFT_EVENT_PREPARED});
+    }
+    if (!w.committed_reported && is_committed_local(r, view, w)) {
+      w.committed_reported = true;
+      r->evq.push_back({view, seq, PBFT_EVENT_COMMITTED_LOCAL});
+      // decided: stragglers are never needed (nothing is in flight while events are evaluated)
+      for (Phase& p : w.ph) p.clear_candidates();
+    }
+  }
+  r->dirty.clear();
+}
+
+static void drain(pbft_replica* r, pbft_round_event* events, uint32_t max_events, uint32_t* n_events) {
+  uint32_t ne = 0;
+  while (events && ne < max_events && !r->evq.empty()) {
+    events[ne++] = r->evq.front();
+    r->evq.pop_front();
+  }
+  if (n_events) *n_events = ne;
+}
+
+// Put every in-flight candidate back to pending (the batch failed: nothing was applied).
+static void revert_segs(pbft_replica* r) {
+  for (const Seg& g : r->segs) {
+    auto wi = r->windows.find(g.key);
+    if (wi == r->windows.end()) continue;
+    Phase& p = wi->second.ph[g.kind];
+    for (uint32_t i = 0; i < g.count && i < p.size(); ++i)
+      if (p.st[i] == V_IN_FLIGHT) { p.st[i] = V_PENDING; ++p.n_pending; }
+  }
+  r->segs.clear();
+  r->in_flight = false;
+}
+
+// The finished batch: State::insert_* for accepted candidates (in push order: the last accepted vote of a signer
+// wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
+// candidates leave the windows.
+static void apply_segs(pbft_replica* r) {
+  ++r->stats.batches;
+  r->stats.verified += r->rows;
+  std::vector<int64_t> amap;
+  std::vector<uint8_t> mism;
+  for (const Seg& g : r->segs) {
+    auto wi = r->windows.find(g.key);
+    if (wi == r->windows.end()) continue;  // window erased (stable checkpoint) while the batch was in flight
+    Window& w = wi->second;
+    Phase& p = w.ph[g.kind];
+    amap.assign(p.digs.size(), -1);
+    bool any = false;
+    for (uint32_t i = 0; i < g.count; ++i) {
+      const uint64_t row = g.row0 + i;
+      const bool ok = (r->bitmap[row >> 6] >> (row & 63)) & 1;
+      const uint32_t d = p.dix[i];
+      if (!ok) {
+        ++r->stats.rejected_sig;
+      } else {
+        ++r->stats.accepted;
+        any = true;
+      }
+      if (g.kind == 0) {
+        if (!ok) continue;
+        if (!w.have_pre_prepare) {
+          w.have_pre_prepare = true;
+          w.digest = p.digs[d];
+        } else if (w.digest != p.digs[d]) {
+          ++r->stats.rejected_digest;
+        }
+        continue;
+      }
+      const uint32_t s = p.who[i];
+      if (ok) {
+        if (amap[d] < 0) amap[d] = p.acc_index(p.digs[d]);
+        const uint32_t a = (uint32_t)amap[d];
+        if (p.acc[s] != a + 1) {
+          if (p.acc[s]) --p.acc_cnt[p.acc[s] - 1];
+          p.acc[s] = a + 1;
+          ++p.acc_cnt[a];
+        }
+        if (w.have_pre_prepare && p.digs[d] != w.digest) ++r->stats.rejected_digest;
+      }
+      if (--p.cnt[s] == 0 && !p.acc[s]) --p.distinct;
+    }
+    p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
+    if (any) r->dirty.insert(g.key);
+  }
+  r->segs.clear();
+  r->in_flight = false;
+}
+
+// Copy the candidates of segments [s0, s1) into the batch (pinned staging or the overrides' buffers).
+static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV) {
+  for (size_t gi = s0; gi < s1; ++gi) {
+    const Seg& g = r->segs[gi];
+    Phase& p = r->windows.find(g.key)->second.ph[g.kind];
+    memcpy(SIG + 64 * g.row0, p.sig.data(), 64 * (size_t)g.count);
+    memcpy(K + g.row0, p.who.data(), 2 * (size_t)g.count);
+    if (p.digs.size() == 1) {
+      std::fill(IDX + g.row0, IDX + g.row0 + g.count, g.env0);
+    } else {
+      for (uint32_t i = 0; i < g.count; ++i) IDX[g.row0 + i] = g.env0 + p.dix[i];
+    }
+    for (size_t j = 0; j < p.digs.size(); ++j)
+      pbft_envelope(ENV + PBFT_ENVELOPE_BYTES * (size_t)(g.env0 + j), g.kind, g.key.first, g.key.second,
+                    p.digs[j].data());
+    memset(p.st.data(), V_IN_FLIGHT, g.count);
+    p.n_pending = 0;
   }
 }
 
@@ -163,14 +417,31 @@ int pbft_replica_create(pbft_ctx* ctx, uint32_t n, uint32_t self_id, const uint8
 }
 
 int pbft_replica_destroy(pbft_replica* r) {
+  if (!r) return PBFT_OK;
+  if (r->in_flight && r->in_flight_via == 0 && r->ctx) (void)pbft_verify_wait(r->ctx);
+  if (r->in_flight && r->in_flight_via == 1 && r->vpoll)
+    while (r->vpoll(r->vuser) == 0) std::this_thread::yield();
   delete r;
   return PBFT_OK;
 }
 
 int pbft_replica_set_verifier(pbft_replica* r, pbft_batch_verify_fn fn, void* user) {
   if (!r) return PBFT_EINVAL;
+  if (r->in_flight) return PBFT_EBUSY;
   r->verify_fn = fn;
   r->verify_user = user;
+  if (fn) r->vsub = nullptr, r->vpoll = nullptr;  // the last installed verifier serves the flushes
+  return PBFT_OK;
+}
+
+int pbft_replica_set_votes_verifier(pbft_replica* r, pbft_votes_submit_fn submit, pbft_votes_poll_fn poll,
+                                    void* user) {
+  if (!r || (!submit) != (!poll)) return PBFT_EINVAL;
+  if (r->in_flight) return PBFT_EBUSY;
+  r->vsub = submit;
+  r->vpoll = poll;
+  r->vuser = user;
+  if (submit) r->verify_fn = nullptr;
   return PBFT_OK;
 }
 
@@ -209,18 +480,18 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint64_t view, uint64_t seq, co
   if (memcmp(d, claimed_digest, 64) != 0) { ++r->stats.rejected_digest; return 0; }  // validate_digest :139-145
   if (view != r->current_view) { ++r->stats.rejected_view; return 0; }                // :134-141
   if (!in_log(r, seq)) { ++r->stats.rejected_watermark; return 0; }                   // h/H TODO :154
-  Window& w = r->windows[{view, seq}];
-  Cand c;
-  memcpy(c.digest.data(), d, 64);
-  memcpy(c.sig, primary_sig, 64);
-  if (w.have_pre_prepare) {                                                          // :144-151
-    if (w.digest != c.digest) ++r->stats.rejected_digest; else ++r->stats.duplicates;
+  Window& w = window_at(r, {view, seq});
+  if (w.have_pre_prepare) {                                                           // :144-151
+    if (memcmp(w.digest.data(), d, 64) != 0) ++r->stats.rejected_digest; else ++r->stats.duplicates;
     return 0;
   }
-  for (const Cand& o : w.pp_pending)
-    if (o.digest == c.digest && memcmp(o.sig, c.sig, 64) == 0) { ++r->stats.duplicates; return 0; }
-  if (w.pp_pending.size() >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
-  w.pp_pending.push_back(c);
+  Phase& p = w.ph[0];
+  const int64_t j = p.find_dig(d);
+  if (j >= 0)
+    for (size_t i = 0; i < p.size(); ++i)
+      if (p.dix[i] == (uint32_t)j && memcmp(&p.sig[64 * i], primary_sig, 64) == 0) { ++r->stats.duplicates; return 0; }
+  if (p.size() >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
+  p.append(d, j, primary_of(r, view), primary_sig);
   return 1;
 }
 
@@ -231,19 +502,153 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
   ++r->stats.pushed;
   if (signer >= r->n || view != r->current_view) { ++r->stats.rejected_view; return 0; }  // validate_commit :187-190
   if (!in_log(r, seq)) { ++r->stats.rejected_watermark; return 0; }
-  Window& w = r->windows[{view, seq}];
+  Window& w = window_at(r, {view, seq});
   if (w.committed_reported) { ++r->stats.duplicates; return 0; }  // late vote for a decided round
-  Phase& p = w.ph[kind - 1];
-  Cand c;
-  memcpy(c.digest.data(), digest, 64);
-  memcpy(c.sig, sig, 64);
-  auto acc = p.accepted.find(signer);
-  if (acc != p.accepted.end() && acc->second == c.digest) { ++r->stats.duplicates; return 0; }
-  std::vector<Cand>& cands = p.pending[signer];
-  for (const Cand& o : cands)
-    if (o.digest == c.digest && memcmp(o.sig, c.sig, 64) == 0) { ++r->stats.duplicates; return 0; }
-  if (cands.size() >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
-  cands.push_back(c);
+  Phase& p = w.ph[kind];
+  p.init(r->n);
+  if (p.acc[signer] && memcmp(p.acc_digs[p.acc[signer] - 1].data(), digest, 64) == 0) {
+    ++r->stats.duplicates;
+    return 0;
+  }
+  const int64_t j = p.find_dig(digest);
+  if (p.cnt[signer]) {
+    if (j >= 0)
+      for (size_t i = 0; i < p.size(); ++i)
+        if (p.who[i] == signer && p.dix[i] == (uint32_t)j && memcmp(&p.sig[64 * i], sig, 64) == 0) {
+          ++r->stats.duplicates;
+          return 0;
+        }
+    if (p.cnt[signer] >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
+  } else if (!p.acc[signer]) {
+    ++p.distinct;
+  }
+  if (p.sig.capacity() == 0) {  // one allocation per phase for the common case (every signer votes once)
+    const size_t c = r->n < 1024 ? r->n : 1024;
+    p.sig.reserve(64 * c); p.who.reserve(c); p.dix.reserve(c); p.st.reserve(c);
+  }
+  p.append(digest, j, signer, sig);
+  ++p.cnt[signer];
+  return 1;
+}
+
+int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
+                           const uint8_t* digests, const uint32_t* signer, const uint8_t* sigs, uint64_t* queued) {
+  if (!r || (N && (!kind || !view || !seq || !digests || !signer || !sigs))) return PBFT_EINVAL;
+  uint64_t q = 0;
+  for (uint64_t i = 0; i < N; ++i) {
+    const int rc = pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
+    if (rc < 0) {
+      if (queued) *queued = q;
+      return rc;
+    }
+    q += (uint64_t)rc;
+  }
+  if (queued) *queued = q;
+  return PBFT_OK;
+}
+
+// Verify every READY sub-window (force: every pending candidate) in one batch, asynchronously.
+int pbft_replica_flush_submit(pbft_replica* r, int force, uint64_t* n_rows) {
+  if (!r) return PBFT_EINVAL;
+  if (n_rows) *n_rows = 0;
+  if (r->in_flight) return PBFT_EBUSY;
+  if (!r->verify_fn && !r->vsub && !r->ctx) return PBFT_ENODEV;
+  // 1. one segment per ready phase: its candidates (all pending between batches) and its envelopes, one per
+  //    distinct (kind, view, seq, digest)
+  r->segs.clear();
+  uint64_t N = 0;
+  uint32_t E = 0;
+  for (auto& kv : r->windows) {
+    Window& w = kv.second;
+    const uint64_t view = kv.first.first;
+    const bool rd[3] = {w.ph[0].n_pending > 0, force ? w.ph[1].n_pending > 0 : prepare_ready(r, view, w),
+                        force ? w.ph[2].n_pending > 0 : commit_ready(r, w)};
+    for (int kind = 0; kind < 3; ++kind) {
+      if (!rd[kind]) continue;
+      Phase& p = w.ph[kind];
+      r->segs.push_back({kv.first, N, (uint32_t)p.size(), E, (uint8_t)kind});
+      N += p.size();
+      E += (uint32_t)p.digs.size();
+    }
+  }
+  r->rows = N;
+  if (n_rows) *n_rows = N;
+  if (N == 0) { r->segs.clear(); return PBFT_OK; }
+  r->bitmap.assign((N + 63) / 64, 0);
+  // 2. fill the batch: the GPU context's pinned staging (zero-copy votes form) or the overrides' buffers; large
+  //    batches with several threads (a memcpy per phase: the replica's side is memory-bound)
+  int rc = PBFT_OK;
+  uint8_t *SIG, *ENV;
+  uint16_t* K;
+  uint32_t* IDX;
+  if (r->verify_fn || r->vsub) {
+    r->hSig.resize(64 * N); r->hK.resize(N); r->hI.resize(N);
+    r->hE.assign(PBFT_ENVELOPE_BYTES * (size_t)E + 16, 0);
+    SIG = r->hSig.data(); K = r->hK.data(); IDX = r->hI.data(); ENV = r->hE.data();
+  } else {
+    pbft_votes_staging st{};
+    rc = pbft_verify_votes_stage(r->ctx, N, E, &st);
+    if (rc) { r->segs.clear(); return rc; }
+    SIG = st.sig; K = st.key_idx; IDX = st.env_idx; ENV = st.envelopes;
+  }
+  const size_t G = r->segs.size();
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t T = N >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, 8), G) : 1;
+  if (T <= 1) {
+    fill_segs(r, 0, G, SIG, K, IDX, ENV);
+  } else {
+    std::vector<std::thread> th;
+    size_t s0 = 0;
+    for (size_t t = 0; t < T; ++t) {  // balanced by rows
+      const uint64_t hi_row = N * (t + 1) / T;
+      size_t s1 = s0;
+      while (s1 < G && (t + 1 == T || r->segs[s1].row0 < hi_row)) ++s1;
+      if (s1 > s0) th.emplace_back(fill_segs, r, s0, s1, SIG, K, IDX, ENV);
+      s0 = s1;
+    }
+    for (auto& x : th) x.join();
+  }
+  // 3. launch
+  if (r->verify_fn) {  // synchronous per-signature override: R, S columns and one envelope per signature
+    r->hR.resize(32 * N); r->hS.resize(32 * N);
+    r->hM.assign(PBFT_ENVELOPE_BYTES * N + 16, 0);  // + read slack
+    for (uint64_t i = 0; i < N; ++i) {
+      memcpy(&r->hR[32 * i], SIG + 64 * i, 32);
+      memcpy(&r->hS[32 * i], SIG + 64 * i + 32, 32);
+      memcpy(&r->hM[PBFT_ENVELOPE_BYTES * i], ENV + PBFT_ENVELOPE_BYTES * (size_t)IDX[i], PBFT_ENVELOPE_BYTES);
+    }
+    rc = r->verify_fn(r->verify_user, r->hR.data(), r->hS.data(), K, r->hM.data(), PBFT_ENVELOPE_BYTES,
+                      PBFT_ENVELOPE_BYTES, N, r->bitmap.data());
+    r->in_flight_via = 2;
+  } else if (r->vsub) {
+    rc = r->vsub(r->vuser, SIG, K, IDX, ENV, E, N, r->bitmap.data());
+    r->in_flight_via = 1;
+  } else {
+    rc = pbft_verify_votes_submit(r->ctx, N, E, r->bitmap.data());
+    r->in_flight_via = 0;
+  }
+  if (rc) { revert_segs(r); return rc; }  // nothing applied: the candidates stay pending
+  r->in_flight = true;
+  return PBFT_OK;
+}
+
+// 1 = no batch in flight any more (the finished one applied; events of every dirty window queued and delivered
+// up to max_events -- the rest wait for the next call); 0 = still running; < 0 = the batch failed (its
+// candidates are pending again).
+int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t max_events, uint32_t* n_events) {
+  if (!r) return PBFT_EINVAL;
+  if (n_events) *n_events = 0;
+  if (r->in_flight) {
+    int st = 1;
+    if (r->in_flight_via == 0) st = pbft_verify_poll(r->ctx);
+    else if (r->in_flight_via == 1) st = r->vpoll(r->vuser);
+    if (st == 0) return 0;
+    if (st < 0) { revert_segs(r); return st; }
+    apply_segs(r);
+  }
+  evaluate(r);
+  gc(r);
+  drain(r, events, max_events, n_events);
   return 1;
 }
 
@@ -251,108 +656,30 @@ int pbft_replica_flush(pbft_replica* r, int force, pbft_round_event* events, uin
                        uint32_t* n_events) {
   if (!r) return PBFT_EINVAL;
   if (n_events) *n_events = 0;
-  // 1. every ready sub-window of every round window -> one SoA batch.  A signer's
-  //    candidates travel together, so after the batch none of them is pending.
-  struct Row {
-    Window* w;
-    Key key;
-    int kind;  // 0 PrePrepare, 1 Prepare, 2 Commit
-    uint32_t signer;
-    const Cand* c;
-  };
-  std::vector<Row> rows;
-  for (auto& kv : r->windows) {
-    Window& w = kv.second;
-    const uint64_t view = kv.first.first;
-    for (const Cand& c : w.pp_pending) rows.push_back({&w, kv.first, 0, primary_of(r, view), &c});
-    const bool rd[2] = {force || prepare_ready(r, view, w), force || commit_ready(r, w)};
-    for (int k = 0; k < 2; ++k) {
-      if (!rd[k]) continue;
-      for (auto& sc : w.ph[k].pending)
-        for (const Cand& c : sc.second) rows.push_back({&w, kv.first, k + 1, sc.first, &c});
+  // a batch submitted earlier completes first (its events are queued, not lost)
+  while (r->in_flight) {
+    if (r->in_flight_via == 0) {
+      const int w = pbft_verify_wait(r->ctx);
+      if (w < 0) { revert_segs(r); return w; }
     }
+    const int p = pbft_replica_flush_poll(r, nullptr, 0, nullptr);
+    if (p < 0) return p;
+    if (p == 0) std::this_thread::yield();
   }
-  const uint64_t N = rows.size();
-  if (N) {
-    std::vector<uint8_t> R(32 * N), S(32 * N), M(PBFT_ENVELOPE_BYTES * N + 16, 0);  // + read slack
-    std::vector<uint16_t> K(N);
-    for (uint64_t i = 0; i < N; ++i) {
-      const Row& x = rows[i];
-      memcpy(&R[32 * i], x.c->sig, 32);
-      memcpy(&S[32 * i], x.c->sig + 32, 32);
-      K[i] = (uint16_t)x.signer;
-      pbft_envelope(&M[PBFT_ENVELOPE_BYTES * i], (uint8_t)x.kind, x.key.first, x.key.second, x.c->digest.data());
+  int rc = pbft_replica_flush_submit(r, force, nullptr);
+  if (rc) return rc;
+  for (;;) {
+    if (r->in_flight && r->in_flight_via == 0) {
+      const int w = pbft_verify_wait(r->ctx);
+      if (w < 0) { revert_segs(r); return w; }
     }
-    std::vector<uint64_t> bitmap((N + 63) / 64, 0);
-    int rc;
-    if (r->verify_fn) {
-      rc = r->verify_fn(r->verify_user, R.data(), S.data(), K.data(), M.data(), PBFT_ENVELOPE_BYTES,
-                        PBFT_ENVELOPE_BYTES, N, bitmap.data());
-    } else {
-      if (!r->ctx) return PBFT_ENODEV;
-      rc = pbft_verify_batch(r->ctx, R.data(), S.data(), K.data(), M.data(), PBFT_ENVELOPE_BYTES,
-                             PBFT_ENVELOPE_BYTES, N, bitmap.data());
-    }
-    if (rc) return rc;  // nothing applied: the candidates stay pending
-    ++r->stats.batches;
-    r->stats.verified += N;
-    // 2. apply in push order: State::insert_* for accepted votes only (last accepted wins per signer);
-    //    the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151)
-    for (uint64_t i = 0; i < N; ++i) {
-      const Row& x = rows[i];
-      const bool ok = (bitmap[i >> 6] >> (i & 63)) & 1;
-      if (!ok) { ++r->stats.rejected_sig; continue; }
-      ++r->stats.accepted;
-      r->dirty.insert(x.key);
-      if (x.kind == 0) {
-        if (!x.w->have_pre_prepare) {
-          x.w->have_pre_prepare = true;
-          x.w->digest = x.c->digest;
-        } else if (x.w->digest != x.c->digest) {
-          ++r->stats.rejected_digest;
-        }
-        continue;
-      }
-      x.w->ph[x.kind - 1].accepted[x.signer] = x.c->digest;
-      if (x.w->have_pre_prepare && x.c->digest != x.w->digest) ++r->stats.rejected_digest;
-    }
-    // 3. drop the verified candidates (the rows point into these vectors: cleared only now)
-    for (const Row& x : rows) {
-      if (x.kind == 0) x.w->pp_pending.clear();
-      else x.w->ph[x.kind - 1].pending.erase(x.signer);
-    }
+    const int p = pbft_replica_flush_poll(r, events, max_events, n_events);
+    if (p != 0) return p < 0 ? p : PBFT_OK;
+    std::this_thread::yield();
   }
-  // 4. events (pre-prepared, prepared :177-182, committed_local :214-223) for every dirty window,
-  //    in (view, seq) order; a window stays dirty while an event did not fit into `events`
-  uint32_t ne = 0;
-  for (auto it = r->dirty.begin(); it != r->dirty.end();) {
-    auto wi = r->windows.find(*it);
-    if (wi == r->windows.end()) { it = r->dirty.erase(it); continue; }
-    Window& w = wi->second;
-    const uint64_t view = it->first, seq = it->second;
-    bool full = false;
-    auto emit = [&](uint32_t kind, bool& reported) {
-      if (full) return;
-      if (ne >= max_events || !events) { full = true; return; }
-      events[ne++] = {view, seq, kind};
-      reported = true;
-    };
-    if (!w.pre_prepared_reported && w.have_pre_prepare) emit(PBFT_EVENT_PRE_PREPARED, w.pre_prepared_reported);
-    if (!w.prepared_reported && is_prepared(r, view, w)) emit(PBFT_EVENT_PREPARED, w.prepared_reported);
-    if (!w.committed_reported && is_committed_local(r, view, w)) {
-      emit(PBFT_EVENT_COMMITTED_LOCAL, w.committed_reported);
-      if (w.committed_reported) {  // decided: stragglers are never needed
-        w.pp_pending.clear();
-        w.ph[0].pending.clear();
-        w.ph[1].pending.clear();
-      }
-    }
-    if (full) ++it; else it = r->dirty.erase(it);
-  }
-  if (n_events) *n_events = ne;
-  gc(r);
-  return PBFT_OK;
 }
+
+int pbft_replica_in_flight(pbft_replica* r) { return r ? (r->in_flight ? 1 : 0) : PBFT_EINVAL; }
 
 // One connection's byte stream of UviBytes/JSON frames (src/protocol_config.rs:50-76 ->
 // src/handler.rs:533-548 -> inject_node_event).  peer_idx = the authenticated peer.
@@ -382,8 +709,10 @@ int pbft_replica_push_frames(pbft_replica* r, uint32_t peer_idx, const uint8_t* 
       if (m.replica != peer_idx) ++r->stats.rejected_signer;
       else got = pbft_replica_push(r, (uint8_t)m.kind, m.view, m.seq, m.digest, peer_idx, m.sig);
     } else if (m.kind == PBFT_MSG_PREPREPARE) {
-      // signed by the view's primary (the signature proves it; any peer may relay)
-      if (r->n == 0 || m.replica != primary_of(r, m.view)) ++r->stats.rejected_signer;
+      // only on the primary's own connection (the reference receives it from the primary, src/behavior.rs:89-95):
+      // a relayed PrePrepare could otherwise fill the window's candidate slots ahead of the real one
+      const uint32_t p = r->n ? primary_of(r, m.view) : 0;
+      if (r->n == 0 || m.replica != p || peer_idx != p) ++r->stats.rejected_signer;
       else
         got = pbft_replica_on_pre_prepare(r, m.view, m.seq, (const uint8_t*)m.operation, m.operation_len, m.digest,
                                           m.sig, nullptr);
@@ -404,18 +733,20 @@ int pbft_replica_stable_checkpoint(pbft_replica* r, uint64_t seq) {
   return PBFT_OK;
 }
 
+// A GC'd seq reports prepared / committed only if THIS replica committed it locally (a stable checkpoint
+// moves h without deciding anything here).
 int pbft_replica_prepared(pbft_replica* r, uint64_t view, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
-  if (view == r->current_view && seq <= r->h_commit && seq > 0) return 1;  // GC'd committed prefix
   auto it = r->windows.find({view, seq});
-  return it != r->windows.end() && is_prepared(r, view, it->second) ? 1 : 0;
+  if (it != r->windows.end()) return is_prepared(r, view, it->second) ? 1 : 0;
+  return is_done(r, view, seq) ? 1 : 0;
 }
 
 int pbft_replica_committed_local(pbft_replica* r, uint64_t view, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
-  if (view == r->current_view && seq <= r->h_commit && seq > 0) return 1;
   auto it = r->windows.find({view, seq});
-  return it != r->windows.end() && is_committed_local(r, view, it->second) ? 1 : 0;
+  if (it != r->windows.end()) return is_committed_local(r, view, it->second) ? 1 : 0;
+  return is_done(r, view, seq) ? 1 : 0;
 }
 
 int pbft_replica_get_stats(pbft_replica* r, pbft_replica_stats* out) {

@@ -8,7 +8,9 @@
 //   keys   raw 32-byte key encodings (hashed as given) + key_ok bytes
 //   batch  SoA: R[N][32], S[N][32], key_idx[N] u16, msg[N][stride]
 //   bitmap ceil(N/64) u64 words, one per wavefront (ballot)
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>  // types only: librccl.so.1 is dlopen'ed by pbft_multi_create
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -139,11 +141,66 @@ struct pbft_ctx {
   uint64_t* h_bitmap = nullptr;  // pinned
   uint64_t async_words = 0;
   float last_ms = 0.f;
+  // pinned host staging of the non-blocking host-buffer forms (pageable caller buffers are copied here,
+  // then DMA'd asynchronously; pbft_verify_votes_stage hands it out for in-place filling)
+  uint8_t* h_stage = nullptr;
+  size_t h_stage_cap = 0;
+  uint64_t staged_n = 0;   // pbft_verify_votes_stage: the batch the staging is laid out for
+  uint32_t staged_env = 0;
+  bool staged = false;
 };
 
 #ifndef PBFT_ENV_SCHED
 #define PBFT_ENV_SCHED 1  // A/B: 0 = every signature expands its own block-2 schedule
 #endif
+
+// Pinned host staging (grow-only: hipHostMalloc costs milliseconds).  Never while a batch is in flight.
+static int ensure_host_stage(pbft_ctx* c, size_t bytes) {
+  if (bytes <= c->h_stage_cap) return PBFT_OK;
+  if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
+  c->h_stage = nullptr;
+  c->h_stage_cap = 0;
+  const size_t cap = bytes + (bytes >> 2) + 4096;
+  if (hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(PBFT_ENOMEM, "pinned host staging alloc");
+  }
+  c->h_stage_cap = cap;
+  return PBFT_OK;
+}
+
+// True if p is host memory the DMA engines can read in place (hipHostMalloc / hipHostRegister).  A pageable
+// pointer makes the query fail; the error is cleared so that the next launch's hipGetLastError is clean.
+static bool host_pinned(const void* p) {
+  if (!p) return true;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// Columnar pinned layout of a votes batch (pbft_verify_votes_stage) / a per-signature batch.
+struct host_votes_layout {
+  size_t offS, offK, offI, offE, bytes;
+  host_votes_layout(uint64_t n, uint32_t n_env) {
+    offS = 32 * n;
+    offK = 64 * n;
+    offI = (offK + 2 * n + 15) & ~(size_t)15;
+    offE = (offI + 4 * n + 255) & ~(size_t)255;
+    bytes = offE + (size_t)PBFT_ENVELOPE_LEN * n_env + 64;  // + read slack of the envelope loads
+  }
+};
+struct host_batch_layout {
+  size_t offS, offK, offM, bytes;
+  host_batch_layout(uint64_t n, uint32_t msg_stride) {
+    offS = 32 * n;
+    offK = 64 * n;
+    offM = (offK + 2 * n + 255) & ~(size_t)255;
+    bytes = offM + (size_t)msg_stride * n + 64;
+  }
+};
 
 static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
   if (bytes > c->stage_cap) {
@@ -375,6 +432,8 @@ static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, h
 
 // Votes form (include/pbft_verify.h pbft_verify_votes): R, S, key_idx and a 4-byte envelope index per
 // signature (70 B instead of 151 B over PCIe) + the batch's table of distinct 85-byte envelopes.
+// Device chunk layout: R | S (rs_stride 32), or the signatures as 64-byte R || S rows (rs_stride 64, the
+// staging of pbft_verify_votes_stage), then key_idx and env_idx.
 struct votes_layout {
   size_t offS, offK, offI, bytes;
   explicit votes_layout(uint64_t n) {
@@ -385,8 +444,10 @@ struct votes_layout {
   }
 };
 
+// rs_stride 32: R and S are separate [N][32] host columns; 64: R = the [N][64] signature rows, S = R + 32.
 static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K,
-                                  const uint32_t* IDX, const uint8_t* ENV, uint32_t n_env, uint64_t N) {
+                                  const uint32_t* IDX, const uint8_t* ENV, uint32_t n_env, uint64_t N,
+                                  uint32_t rs_stride = 32) {
   const uint64_t words = (N + 63) / 64;
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
   const uint64_t ch = N < PIPE_CHUNK ? N : PIPE_CHUNK;
@@ -409,15 +470,19 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
     const int b = (int)(chunk & 1);
     uint8_t* base = c->d_stage + env_bytes + (size_t)b * L.bytes;
     if (chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
-    HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
-    HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    if (rs_stride == 64) {
+      HIP_TRY(hipMemcpyAsync(base, R + 64 * lo, 64 * n, hipMemcpyHostToDevice, c->cstream));
+    } else {
+      HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+      HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    }
     HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream));
     HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream));
     HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
-    rc = launch_verify(c, base, base + L.offS, (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN,
-                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, 32, 2, nullptr,
-                       (const uint32_t*)(base + L.offI), n_env, dWK);
+    rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS, (const uint16_t*)(base + L.offK),
+                       c->d_stage, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream,
+                       rs_stride, 2, nullptr, (const uint32_t*)(base + L.offI), n_env, dWK);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
   }
@@ -530,6 +595,7 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   c->adopt(nullptr);
   (void)hipFree(c->d_stage); (void)hipFree(c->d_bitmap); (void)hipFree(c->d_work); (void)hipFree(c->d_wk);
   if (c->h_bitmap) (void)hipHostFree(c->h_bitmap);
+  if (c->h_stage) (void)hipHostFree(c->h_stage);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
@@ -642,6 +708,19 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
   if (N == 0) return PBFT_OK;
   HIP_TRY(hipSetDevice(c->device));
+  if (!(host_pinned(R) && host_pinned(S) && host_pinned(K) && host_pinned(M))) {
+    // pageable: copy into the pinned staging first, so the DMA below is asynchronous (a pageable
+    // hipMemcpyAsync stages through the runtime's buffers and returns only when the copy is done)
+    const host_batch_layout L(N, msg_stride);
+    int rc = ensure_host_stage(c, L.bytes);
+    if (rc) return rc;
+    uint8_t* h = c->h_stage;
+    memcpy(h, R, 32 * N);
+    memcpy(h + L.offS, S, 32 * N);
+    memcpy(h + L.offK, K, 2 * N);
+    if (M && msg_stride) memcpy(h + L.offM, M, (size_t)msg_stride * N);
+    R = h; S = h + L.offS; K = (const uint16_t*)(h + L.offK); M = M ? h + L.offM : M;
+  }
   int rc = stage_and_launch(c, R, S, K, M, msg_len, msg_stride, N);
   if (rc) return rc;
   const uint64_t words = (N + 63) / 64;
@@ -667,7 +746,10 @@ int pbft_verify_poll(pbft_ctx* c) {
   if (!c->in_flight) return 1;
   hipError_t e = hipEventQuery(c->ev_done);
   if (e == hipErrorNotReady) return 0;
-  HIP_TRY(e);
+  if (e != hipSuccess) {
+    c->in_flight = false;  // the batch is lost; the context stays usable for the next submit
+    HIP_TRY(e);
+  }
   finish_async(c);
   return 1;
 }
@@ -675,8 +757,84 @@ int pbft_verify_poll(pbft_ctx* c) {
 int pbft_verify_wait(pbft_ctx* c) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight) return PBFT_OK;
-  HIP_TRY(hipEventSynchronize(c->ev_done));
+  const hipError_t e = hipEventSynchronize(c->ev_done);
+  if (e != hipSuccess) {
+    c->in_flight = false;
+    HIP_TRY(e);
+  }
   return finish_async(c);
+}
+
+// ---- votes form, non-blocking (include/pbft_verify.h) ----
+static int votes_submit_from(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* I,
+                             const uint8_t* E, uint32_t n_env, uint64_t N, uint64_t* out, uint32_t rs_stride = 32) {
+  int rc = stage_votes_and_launch(c, R, S, K, I, E, n_env, N, rs_stride);
+  if (rc) return rc;
+  const uint64_t words = (N + 63) / 64;
+  HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->ev_done, c->stream));
+  c->in_flight = true;
+  c->async_out = out;
+  c->async_words = words;
+  return PBFT_OK;
+}
+
+int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_staging* out) {
+  if (!c || !out) return set_err(PBFT_EINVAL, "null argument");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (N && n_env == 0) return set_err(PBFT_EINVAL, "votes batch without envelopes");
+  HIP_TRY(hipSetDevice(c->device));
+  const host_votes_layout L(N, n_env);
+  int rc = ensure_host_stage(c, L.bytes);
+  if (rc) return rc;
+  uint8_t* h = c->h_stage;
+  out->sig = h;  // [N][64]: R || S rows over the R and S columns of the layout
+  out->key_idx = (uint16_t*)(h + L.offK);
+  out->env_idx = (uint32_t*)(h + L.offI);
+  out->envelopes = h + L.offE;
+  c->staged = true;
+  c->staged_n = N;
+  c->staged_env = n_env;
+  return PBFT_OK;
+}
+
+int pbft_verify_votes_submit(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (!c->staged || N != c->staged_n || n_env != c->staged_env)
+    return set_err(PBFT_EINVAL, "pbft_verify_votes_stage was not called for this batch");
+  if (N && !out) return set_err(PBFT_EINVAL, "null bitmap");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  c->staged = false;
+  if (N == 0) return PBFT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  const host_votes_layout L(N, n_env);
+  uint8_t* h = c->h_stage;
+  return votes_submit_from(c, h, h + 32, (const uint16_t*)(h + L.offK), (const uint32_t*)(h + L.offI), h + L.offE,
+                           n_env, N, out, 64);
+}
+
+int pbft_verify_votes_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* I,
+                            const uint8_t* E, uint32_t n_env, uint64_t N, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (N && (!R || !S || !K || !I || !out || !E || n_env == 0)) return set_err(PBFT_EINVAL, "bad votes arguments");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  if (N == 0) return PBFT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  if (host_pinned(R) && host_pinned(S) && host_pinned(K) && host_pinned(I) && host_pinned(E))
+    return votes_submit_from(c, R, S, K, I, E, n_env, N, out);
+  pbft_votes_staging st;
+  int rc = pbft_verify_votes_stage(c, N, n_env, &st);
+  if (rc) return rc;
+  for (uint64_t i = 0; i < N; ++i) {
+    memcpy(st.sig + 64 * i, R + 32 * i, 32);
+    memcpy(st.sig + 64 * i + 32, S + 32 * i, 32);
+  }
+  memcpy(st.key_idx, K, 2 * N);
+  memcpy(st.env_idx, I, 4 * N);
+  memcpy(st.envelopes, E, (size_t)PBFT_ENVELOPE_LEN * n_env);
+  return pbft_verify_votes_submit(c, N, n_env, out);
 }
 
 // One host batch over several contexts (GPUs of this process, or cloned contexts
@@ -708,6 +866,130 @@ int pbft_verify_batch_multi(pbft_ctx* const* ctxs, uint32_t n_ctx, const uint8_t
     if (!rc) rc = w;
   }
   return rc;
+}
+
+}  // extern "C"
+
+// ---- single-process multi-GPU round, bitmap all-gather on RCCL (include/pbft_verify.h) ----
+// RCCL is resolved at run time (dlopen), so the verifier loads on hosts and in processes without it; in a
+// process that already loaded torch's bundled librccl.so.1 the same object is reused (SONAME match).
+namespace {
+struct rccl_api {
+  bool ok = false;
+  decltype(&ncclCommInitAll) CommInitAll = nullptr;
+  decltype(&ncclCommDestroy) CommDestroy = nullptr;
+  decltype(&ncclAllGather) AllGather = nullptr;
+  decltype(&ncclGroupStart) GroupStart = nullptr;
+  decltype(&ncclGroupEnd) GroupEnd = nullptr;
+  decltype(&ncclGetErrorString) GetErrorString = nullptr;
+};
+rccl_api* rccl() {
+  static rccl_api api;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    api.CommInitAll = (decltype(api.CommInitAll))dlsym(h, "ncclCommInitAll");
+    api.CommDestroy = (decltype(api.CommDestroy))dlsym(h, "ncclCommDestroy");
+    api.AllGather = (decltype(api.AllGather))dlsym(h, "ncclAllGather");
+    api.GroupStart = (decltype(api.GroupStart))dlsym(h, "ncclGroupStart");
+    api.GroupEnd = (decltype(api.GroupEnd))dlsym(h, "ncclGroupEnd");
+    api.GetErrorString = (decltype(api.GetErrorString))dlsym(h, "ncclGetErrorString");
+    api.ok = api.CommInitAll && api.CommDestroy && api.AllGather && api.GroupStart && api.GroupEnd &&
+             api.GetErrorString;
+  });
+  return api.ok ? &api : nullptr;
+}
+int rccl_err(ncclResult_t r, const char* what) {
+  char b[256];
+  snprintf(b, sizeof b, "%s: %s", what, rccl() ? rccl()->GetErrorString(r) : "RCCL unavailable");
+  return set_err(PBFT_EHIP, b);
+}
+}  // namespace
+
+struct pbft_multi {
+  std::vector<pbft_ctx*> ctx;
+  std::vector<ncclComm_t> comm;
+};
+
+extern "C" {
+
+int pbft_multi_create(pbft_ctx* const* ctxs, uint32_t n_ctx, pbft_multi** out) {
+  if (!ctxs || !out || n_ctx == 0) return set_err(PBFT_EINVAL, "no contexts");
+  *out = nullptr;
+  std::vector<int> devs(n_ctx);
+  for (uint32_t i = 0; i < n_ctx; ++i) {
+    if (!ctxs[i]) return set_err(PBFT_EINVAL, "null context");
+    devs[i] = ctxs[i]->device;
+    for (uint32_t j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) return set_err(PBFT_EINVAL, "one context per device (distinct devices)");
+  }
+  rccl_api* api = rccl();
+  if (!api) return set_err(PBFT_ENODEV, "librccl.so.1 not loadable");
+  pbft_multi* m = new pbft_multi();
+  m->ctx.assign(ctxs, ctxs + n_ctx);
+  m->comm.assign(n_ctx, nullptr);
+  const ncclResult_t r = api->CommInitAll(m->comm.data(), (int)n_ctx, devs.data());
+  if (r != ncclSuccess) {
+    delete m;
+    return rccl_err(r, "ncclCommInitAll");
+  }
+  *out = m;
+  return PBFT_OK;
+}
+
+int pbft_multi_destroy(pbft_multi* m) {
+  if (!m) return PBFT_OK;
+  (void)pbft_multi_sync(m);
+  if (rccl_api* api = rccl())
+    for (ncclComm_t c : m->comm)
+      if (c) (void)api->CommDestroy(c);
+  delete m;
+  return PBFT_OK;
+}
+
+int pbft_multi_sync(pbft_multi* m) {
+  if (!m) return set_err(PBFT_EINVAL, "null multi");
+  for (pbft_ctx* c : m->ctx) {
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  return PBFT_OK;
+}
+
+int pbft_verify_batch_device_multi(pbft_multi* m, const uint8_t* const* dR, const uint8_t* const* dS,
+                                   const uint16_t* const* dK, const uint8_t* const* dM, uint32_t msg_len,
+                                   uint32_t msg_stride, const uint64_t* n, uint64_t wpr, uint64_t* const* dB) {
+  if (!m || !dR || !dS || !dK || !dM || !n || !dB) return set_err(PBFT_EINVAL, "null argument");
+  const uint32_t G = (uint32_t)m->ctx.size();
+  for (uint32_t r = 0; r < G; ++r) {
+    if ((n[r] + 63) / 64 > wpr) return set_err(PBFT_EINVAL, "words_per_rank < ceil(n[r] / 64)");
+    if (!dB[r] || !check_batch_args(dR[r], dS[r], dK[r], dM[r], msg_len, msg_stride, n[r], dB[r]))
+      return set_err(PBFT_EINVAL, "bad shard arguments");
+    if (m->ctx[r]->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  }
+  for (uint32_t r = 0; r < G; ++r) {
+    pbft_ctx* c = m->ctx[r];
+    HIP_TRY(hipSetDevice(c->device));
+    uint64_t* mine = dB[r] + (size_t)r * wpr;
+    const uint64_t words = (n[r] + 63) / 64;
+    if (wpr > words) HIP_TRY(hipMemsetAsync(mine + words, 0, (wpr - words) * 8, c->stream));
+    int rc = launch_verify(c, dR[r], dS[r], dK[r], dM[r], msg_len, msg_stride, n[r], mine, c->stream);
+    if (rc) return rc;
+  }
+  rccl_api* api = rccl();
+  ncclResult_t e = api->GroupStart();
+  if (e != ncclSuccess) return rccl_err(e, "ncclGroupStart");
+  for (uint32_t r = 0; r < G; ++r) {
+    pbft_ctx* c = m->ctx[r];
+    e = api->AllGather(dB[r] + (size_t)r * wpr, dB[r], wpr, ncclUint64, m->comm[r], c->stream);
+    if (e != ncclSuccess) break;
+  }
+  const ncclResult_t e2 = api->GroupEnd();
+  if (e != ncclSuccess) return rccl_err(e, "ncclAllGather");
+  if (e2 != ncclSuccess) return rccl_err(e2, "ncclGroupEnd");
+  return PBFT_OK;
 }
 
 int pbft_verify_batch_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK,
@@ -742,13 +1024,9 @@ int pbft_verify_votes(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uin
     return set_err(PBFT_EINVAL, "bad votes arguments");
   if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
   if (N == 0) return PBFT_OK;
-  HIP_TRY(hipSetDevice(c->device));
-  int rc = stage_votes_and_launch(c, R, S, K, env_idx, envelopes, n_env, N);
+  int rc = pbft_verify_votes_async(c, R, S, K, env_idx, envelopes, n_env, N, out);
   if (rc) return rc;
-  HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, (N + 63) / 64 * 8, hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
-  memcpy(out, c->h_bitmap, (N + 63) / 64 * 8);
-  return PBFT_OK;
+  return pbft_verify_wait(c);
 }
 
 int pbft_verify_votes_device(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK,

@@ -43,6 +43,10 @@ int pbft_verify_batch(pbft_ctx*, const uint8_t*, const uint8_t*, const uint16_t*
 int pbft_digest_blake2b512(pbft_ctx*, const uint8_t*, const uint64_t*, const uint32_t*, uint64_t, uint8_t*) {
   return PBFT_ENODEV;
 }
+int pbft_verify_votes_stage(pbft_ctx*, uint64_t, uint32_t, pbft_votes_staging*) { return PBFT_ENODEV; }
+int pbft_verify_votes_submit(pbft_ctx*, uint64_t, uint32_t, uint64_t*) { return PBFT_ENODEV; }
+int pbft_verify_poll(pbft_ctx*) { return PBFT_ENODEV; }
+int pbft_verify_wait(pbft_ctx*) { return PBFT_ENODEV; }
 }
 
 using PL = plan<40, 6, 14>;  // balanced 7/6-bit windows, incl. take_last (as the GPU plans)
@@ -385,12 +389,115 @@ static void test_replica(const Keys& k, std::mt19937_64& rng) {
   printf("replica: %d commits, %llu verify batches\n", committed, (unsigned long long)vu.calls);
 }
 
+// ---- 4. non-blocking flush: an asynchronous votes verifier that completes on the third poll; pushes,
+// duplicates of in-flight votes and a stable checkpoint land while a batch is in flight ----------------------
+struct AsyncUser {
+  const Keys* k;
+  const uint8_t *SIG = nullptr, *E = nullptr;
+  const uint16_t* K = nullptr;
+  const uint32_t* I = nullptr;
+  uint32_t n_env = 0;
+  uint64_t N = 0;
+  uint64_t* out = nullptr;
+  int polls = 0;
+  uint64_t batches = 0;
+};
+
+static int async_submit(void* user, const uint8_t* SIG, const uint16_t* K, const uint32_t* I, const uint8_t* E,
+                        uint32_t n_env, uint64_t N, uint64_t* out) {
+  AsyncUser* u = (AsyncUser*)user;
+  CHECK(u->out == nullptr);  // one batch in flight
+  u->SIG = SIG; u->K = K; u->I = I; u->E = E; u->n_env = n_env; u->N = N; u->out = out; u->polls = 0;
+  ++u->batches;
+  return 0;
+}
+
+static int async_poll(void* user) {
+  AsyncUser* u = (AsyncUser*)user;
+  if (!u->out) return 1;
+  if (++u->polls < 3) return 0;
+  for (uint64_t i = 0; i < (u->N + 63) / 64; ++i) u->out[i] = 0;
+  for (uint64_t i = 0; i < u->N; ++i) {
+    uint8_t sig[64], env[PBFT_ENVELOPE_BYTES + 16] = {0};
+    memcpy(sig, u->SIG + 64 * i, 64);
+    CHECK(u->I[i] < u->n_env);
+    memcpy(env, u->E + (size_t)PBFT_ENVELOPE_BYTES * u->I[i], PBFT_ENVELOPE_BYTES);
+    if (u->K[i] < u->k->n && verify(*u->k, u->K[i], env, PBFT_ENVELOPE_BYTES, sig)) u->out[i / 64] |= 1ull << (i % 64);
+  }
+  u->out = nullptr;
+  return 1;
+}
+
+static void test_replica_async(const Keys& k) {
+  const int n = k.n;
+  std::vector<uint8_t> keys(32 * (size_t)n);
+  for (int i = 0; i < n; ++i) memcpy(&keys[32 * (size_t)i], k.pub[i].data(), 32);
+  pbft_replica* r = nullptr;
+  CHECK(pbft_replica_create(nullptr, (uint32_t)n, 0, keys.data(), &r) == 0);
+  AsyncUser u{&k};
+  CHECK(pbft_replica_set_votes_verifier(r, async_submit, async_poll, &u) == 0);
+  pbft_replica_set_digest_fn(r, host_digest, nullptr);
+  const char op[] = "testOperation";
+  uint8_t d[64];
+  digest_padded(d, (const uint8_t*)op, strlen(op));
+  const int primary = 1;
+  const int S = 6;
+  std::vector<std::array<uint8_t, 64>> prep(n * (S + 1)), com(n * (S + 1));
+  for (int q = 1; q <= S; ++q) {
+    uint8_t ps[64];
+    env_sign(k, primary, PBFT_KIND_PREPREPARE, 1, (uint64_t)q, d, ps);
+    CHECK(pbft_replica_on_pre_prepare(r, 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d, ps, nullptr) == 1);
+    for (int i = 0; i < n; ++i) {
+      env_sign(k, i, PBFT_KIND_PREPARE, 1, (uint64_t)q, d, prep[q * n + i].data());
+      env_sign(k, i, PBFT_KIND_COMMIT, 1, (uint64_t)q, d, com[q * n + i].data());
+    }
+  }
+  for (int q = 1; q <= S; ++q)
+    for (int i = 0; i < n; ++i) CHECK(pbft_replica_push(r, PBFT_KIND_PREPARE, 1, (uint64_t)q, d, (uint32_t)i, prep[q * n + i].data()) == 1);
+  uint64_t rows = 0;
+  CHECK(pbft_replica_flush_submit(r, 1, &rows) == 0 && rows == (uint64_t)(S + S * n));
+  CHECK(pbft_replica_in_flight(r) == 1);
+  CHECK(pbft_replica_flush_submit(r, 1, &rows) == PBFT_EBUSY);
+  // during the flight: a duplicate of an in-flight vote, new Commits, and a checkpoint past seq 1
+  CHECK(pbft_replica_push(r, PBFT_KIND_PREPARE, 1, 2, d, 2, prep[2 * n + 2].data()) == 0);
+  for (int q = 1; q <= S; ++q)
+    for (int i = 0; i < n; ++i) CHECK(pbft_replica_push(r, PBFT_KIND_COMMIT, 1, (uint64_t)q, d, (uint32_t)i, com[q * n + i].data()) == 1);
+  CHECK(pbft_replica_stable_checkpoint(r, 1) == 0);
+  pbft_round_event ev[256];
+  uint32_t ne = 0;
+  int polls = 0, st;
+  while ((st = pbft_replica_flush_poll(r, ev, 2, &ne)) == 0) { CHECK(ne == 0); ++polls; }
+  CHECK(st == 1 && polls == 2 && ne == 2);  // only 2 delivered now: the rest stay queued
+  std::vector<pbft_round_event> all(ev, ev + 2);
+  CHECK(pbft_replica_flush_poll(r, ev, 256, &ne) == 1);  // nothing in flight: drains the queue
+  all.insert(all.end(), ev, ev + ne);
+  int pre = 0, prepared = 0, committed = 0;
+  for (const auto& e : all) {
+    CHECK(e.seq >= 2);  // seq 1 was checkpointed away while its rows were in flight
+    pre += e.kind == PBFT_EVENT_PRE_PREPARED;
+    prepared += e.kind == PBFT_EVENT_PREPARED;
+  }
+  CHECK(pre == S - 1 && prepared == S - 1 && all.size() == 2 * (size_t)(S - 1));
+  CHECK(pbft_replica_flush_submit(r, 0, &rows) == 0 && rows == (uint64_t)((S - 1) * n));
+  while ((st = pbft_replica_flush_poll(r, ev, 256, &ne)) == 0) {}
+  for (uint32_t e = 0; e < ne; ++e) committed += ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL;
+  CHECK(committed == S - 1);
+  // a locally committed, GC'd seq reports committed; the checkpointed seq 1 never was decided here
+  CHECK(pbft_replica_committed_local(r, 1, 2) == 1 && pbft_replica_committed_local(r, 1, 1) == 0);
+  pbft_replica_stats s;
+  pbft_replica_get_stats(r, &s);
+  CHECK(s.low_watermark == (uint64_t)S && s.live_windows == 0 && s.duplicates >= 1);
+  pbft_replica_destroy(r);
+  printf("replica async: %llu batches, %d commits\n", (unsigned long long)u.batches, committed);
+}
+
 int main() {
   std::mt19937_64 rng(0x5EED);
   Keys k = make_keys(4, rng);
   test_arithmetic(k, rng);
   test_wire(rng);
   test_replica(k, rng);
+  test_replica_async(k);
   printf("sanitized host run ok\n");
   return 0;
 }

@@ -30,6 +30,10 @@ class Stats(ctypes.Structure):
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p)
 DIGEST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p)
+# (user, sig[N][64] = R || S, key_idx[N], env_idx[N], envelopes[n_env][85], n_env, N, bitmap_out)
+VOTES_SUBMIT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                   ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p)
+VOTES_POLL_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
 
 
 def lib():
@@ -57,6 +61,11 @@ def lib():
     L.pbft_replica_prepared.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
     L.pbft_replica_committed_local.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64]
     L.pbft_replica_get_stats.argtypes = [vp, ctypes.POINTER(Stats)]
+    L.pbft_replica_set_votes_verifier.argtypes = [vp, VOTES_SUBMIT_FN, VOTES_POLL_FN, vp]
+    L.pbft_replica_push_many.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp]
+    L.pbft_replica_flush_submit.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]
+    L.pbft_replica_flush_poll.argtypes = [vp, ctypes.POINTER(Event), ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+    L.pbft_replica_in_flight.argtypes = [vp]
     L.pbft_envelope.argtypes = [ctypes.c_char_p, ctypes.c_uint8, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p]
     return L
 
@@ -74,6 +83,56 @@ def oracle():
 def seeds(n, tag=1):
     return [hashlib.sha512(b"pbft-key" + tag.to_bytes(8, "little") + i.to_bytes(8, "little")).digest()[:32]
             for i in range(n)]
+
+
+class AsyncOracleVerifier:
+    """Asynchronous votes-form verifier (pbft_replica_set_votes_verifier) backed by the C oracle on a worker thread:
+    submit expands envelopes[env_idx[i]] per signature and starts the thread, poll reports it done.  What a
+    replica's flush_submit / flush_poll see from the GPU, without a GPU."""
+
+    def __init__(self, cluster, threads=4):
+        import threading
+        self.c, self.threads, self._t, self._lock = cluster, threads, None, threading.Lock()
+        self.submit_cb = VOTES_SUBMIT_FN(self._submit)
+        self.poll_cb = VOTES_POLL_FN(self._poll)
+        self.batches = 0
+
+    def install(self, rep):
+        assert self.c.L.pbft_replica_set_votes_verifier(rep, self.submit_cb, self.poll_cb, None) == 0
+
+    def _submit(self, user, SIG, K, I, E, n_env, N, out):
+        import threading
+        assert self._t is None
+        n = int(N)
+        sig = np.ctypeslib.as_array(ctypes.cast(SIG, ctypes.POINTER(ctypes.c_uint8)), (n * 64,)).reshape(n, 64)
+        Rn = np.ascontiguousarray(sig[:, :32])
+        Sn = np.ascontiguousarray(sig[:, 32:])
+        Kn = np.ctypeslib.as_array(ctypes.cast(K, ctypes.POINTER(ctypes.c_uint16)), (n,)).copy()
+        In = np.ctypeslib.as_array(ctypes.cast(I, ctypes.POINTER(ctypes.c_uint32)), (n,)).copy()
+        En = np.ctypeslib.as_array(ctypes.cast(E, ctypes.POINTER(ctypes.c_uint8)), (int(n_env) * 85,)).copy()
+        M = np.zeros((n + 1, 85), np.uint8)
+        M[:n] = En.reshape(-1, 85)[In]
+        acc = np.zeros(n, np.uint8)
+        self.batches += 1
+
+        def work():
+            self.c.o.oracle_verify_batch(self.c.keys_np.ctypes.data, self.c.n, Rn.ctypes.data, Sn.ctypes.data,
+                                         Kn.ctypes.data, M.ctypes.data, 85, 85, n, acc.ctypes.data, self.threads)
+        self._t = (threading.Thread(target=work), acc, out, n)
+        self._t[0].start()
+        return 0
+
+    def _poll(self, user):
+        if self._t is None:
+            return 1
+        th, acc, out, n = self._t
+        if th.is_alive():
+            return 0
+        th.join()
+        bits = np.packbits(np.concatenate([acc, np.zeros((-n) % 64, np.uint8)]), bitorder="little")
+        ctypes.memmove(out, bits.ctypes.data, len(bits))
+        self._t = None
+        return 1
 
 
 class Cluster:
@@ -130,6 +189,30 @@ class Cluster:
         assert self.L.pbft_replica_flush(self.reps[i], force, ev, max_events, ctypes.byref(ne)) == 0
         return [(e.view, e.seq, e.kind) for e in ev[: ne.value]]
 
+    def flush_submit(self, i, force=0):
+        n = ctypes.c_uint64()
+        rc = self.L.pbft_replica_flush_submit(self.reps[i], force, ctypes.byref(n))
+        assert rc == 0, rc
+        return n.value
+
+    def flush_poll(self, i, max_events=4096):
+        """None while the batch is in flight, else the delivered events."""
+        ev = (Event * max_events)()
+        ne = ctypes.c_uint32()
+        rc = self.L.pbft_replica_flush_poll(self.reps[i], ev, max_events, ctypes.byref(ne))
+        assert rc >= 0, rc
+        return None if rc == 0 else [(e.view, e.seq, e.kind) for e in ev[: ne.value]]
+
+    def flush_async(self, i, force=0, max_events=4096):
+        """flush_submit, then poll until done (yielding, as an event loop would)."""
+        import time
+        self.flush_submit(i, force)
+        while True:
+            evs = self.flush_poll(i, max_events)
+            if evs is not None:
+                return evs
+            time.sleep(0.0005)
+
     def primary(self, view=1):
         return view % self.n
 
@@ -181,8 +264,9 @@ class PhaseSim:
             for i in range(self.c.n):
                 assert self.c.pre_prepare(i, view, q, self.op) == 1
 
-    def run(self, max_rounds=20):
-        """Deliver, flush (never forced), react to events; until quiescent.  Returns rounds used."""
+    def run(self, max_rounds=20, async_flush=False):
+        """Deliver, flush (never forced), react to events; until quiescent.  Returns rounds used.
+        async_flush: every replica's flush is flush_submit + flush_poll (non-blocking form)."""
         L = self.c.L
         for rnd in range(max_rounds):
             progressed = False
@@ -194,7 +278,7 @@ class PhaseSim:
             for i in range(self.c.n):
                 if i in self.silent:
                     continue
-                for v, q, k in self.c.flush(i):
+                for v, q, k in (self.c.flush_async(i) if async_flush else self.c.flush(i)):
                     progressed = True
                     self.events[i].append((v, q, k))
                     if k == EV_PRE_PREPARED:

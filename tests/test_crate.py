@@ -46,13 +46,26 @@ def test_build_rs_matches_graft_build():
     g = open(os.path.join(ROOT, "__graft_entry__.py")).read()
     for flag in ("--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared"):
         assert flag in b and flag in g, flag
-    for src in ("pbft_amd/csrc/pbft_verify.hip", "replica", "wire"):
-        assert src in b
+    # the same translation units as pbft_amd/native_build.py (the product build), in the same roles
+    import sys
+    sys.path.insert(0, ROOT)
+    from pbft_amd import native_build
+    m = re.search(r"let hip_sources = \[([^\]]*)\]", b)
+    assert m, "build.rs: hip_sources list not found"
+    assert re.findall(r'"([^"]+)"', m.group(1)) == native_build.HIP_SOURCES
+    m = re.search(r'for name in \[([^\]]*)\]\.iter\(\)', b)
+    assert m, "build.rs: host source list not found"
+    assert [x + ".cpp" for x in re.findall(r'"([^"]+)"', m.group(1))] == native_build.HOST_SOURCES
+    for flag in native_build.HIP_FLAGS:
+        assert flag in b, flag
+    for flag in native_build.HOST_FLAGS:
+        assert flag in b, flag
     assert 'links = "pbft_verify"' in open(os.path.join(CRATE, "Cargo.toml")).read()
 
 
 def test_trait_surface():
     lib = open(os.path.join(CRATE, "src", "lib.rs")).read()
     for item in ("pub trait BatchVerifier", "fn submit(", "fn poll(", "fn verify(", "impl BatchVerifier for GpuVerifier",
-                 "impl BatchVerifier for CpuVerifier", "verify_strict", "pub struct Replica", "fn key_from_peer_id"):
+                 "impl BatchVerifier for CpuVerifier", "verify_strict", "pub struct Replica", "fn key_from_peer_id",
+                 "fn flush_submit(", "fn flush_poll(", "fn submit_votes(", "pub struct MultiGpu"):
         assert item in lib, item
