@@ -159,13 +159,20 @@ def pmc_traffic(pb: int, pa: int, n: int) -> dict:
 
 
 def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int = 4096, n_ctx: int = 4,
-                   duration_s: float = 1.0):
+                   duration_s: float = 1.0, pinned: bool = True):
     """BASELINE config #5 on this GPU: 4096-signature batches arriving at a fixed offered rate, each submitted
     through the host-buffer API (H2D copies + kernels + bitmap D2H) on one of n_ctx contexts (own HIP streams,
     shared tables: pbft_verify_ctx_clone).  Latency = bitmap ready (host poll) - scheduled arrival.
-    offered_sigs_per_s = inf measures back-to-back pipelined throughput instead."""
+    offered_sigs_per_s = inf measures back-to-back pipelined throughput instead.  pinned: the batches live in
+    pinned host memory (DMA'd in place); else pageable numpy arrays (the library copies them into its pinned
+    staging inside the submit)."""
     from pbft_amd import SigBatch
     ctxs = [v.clone() for _ in range(n_ctx)]
+    if pinned:
+        import torch
+        pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()  # noqa: E731
+        m = min(len(R), 64 * batch)
+        R, S, key_idx, msg = pin(R[:m]), pin(S[:m]), pin(key_idx[:m]), pin(msg[:m])
     nb = max(1, len(R) // batch)
     batches = [SigBatch(R[i * batch:(i + 1) * batch], S[i * batch:(i + 1) * batch],
                         key_idx[i * batch:(i + 1) * batch], msg[i * batch:(i + 1) * batch], ENVELOPE)
@@ -206,6 +213,8 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
             "offered_sigs_per_s": offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else None,
             "achieved_sigs_per_s": done * batch / wall, "batches": int(done),
             "p50_ms": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)),
+            "p999_ms": float(np.percentile(lat, 99.9)), "max_ms": float(lat.max()),
+            "inputs": "pinned host memory" if pinned else "pageable host memory (copied into the pinned staging)",
             "path": "host buffers: H2D + verify kernels + D2H per batch"}
 
 
@@ -311,6 +320,119 @@ def votes_device_round(v, d, msg, expect, stream, torch, dev, iters: int = 50):
             "path": "device-resident votes form: envelope-schedule kernel + comb + finish per call"}
 
 
+def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 5):
+    """the 2^20 round through the replica state machine (include/pbft_replica.h) on this GPU,
+    the way a reference replica runs it: one pbft_replica (n = 256) receives the round's 2048 signed PrePrepares and
+    2^20 Prepare / Commit votes (pbft_replica_push_many, not timed: ingress), then ONE pbft_replica_flush_submit
+    (rows written in the votes form straight into the context's pinned staging, 64 + 2 + 4 B per signature + 4096
+    envelopes, launched without waiting) and pbft_replica_flush_poll from the loop until the bitmap is applied and
+    the events are out.  Timed: submit -> last poll.  A fresh replica per round (same seqs)."""
+    import ctypes
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from replica_sim import Event, Stats, lib
+    L = lib()
+    n_rep = len(pub)
+    n = len(R)
+    n_seq = n // (2 * n_rep)
+    # bench round order: for seq, for kind (Prepare, Commit), for replica
+    seq = np.repeat(np.arange(1, n_seq + 1, dtype=np.uint64), 2 * n_rep)
+    kind = np.tile(np.repeat(np.array([1, 2], np.uint8), n_rep), n_seq)
+    signer = key_idx.astype(np.uint32)
+    view = np.ones(n, np.uint64)
+    digs = np.ascontiguousarray(msg[:, 21:85])
+    sigs = np.ascontiguousarray(np.concatenate([R, S], axis=1))
+    primary = 1 % n_rep
+    pp_env = msg[::2 * n_rep].copy()
+    pp_env[:, 4] = 0  # kind 0: the PrePrepare envelope of each seq
+    pR, pS, _ = v.sign(seeds, np.full(n_seq, primary, np.uint16), pp_env, ENVELOPE)
+    ops = [b"op-" + str(q).encode() for q in range(1, n_seq + 1)]
+    res = {"submit_ms": [], "e2e_ms": [], "polls": [], "push_ms": []}
+    ev = (Event * 16384)()
+    for r in range(rounds + 1):
+        rep = ctypes.c_void_p()
+        assert L.pbft_replica_create(v._ctx, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+        for q in range(n_seq):
+            assert L.pbft_replica_on_pre_prepare(rep, 1, q + 1, ops[q], len(ops[q]), digs[2 * n_rep * q].tobytes(),
+                                                 pR[q].tobytes() + pS[q].tobytes(), None) == 1
+        qd = ctypes.c_uint64()
+        t = time.perf_counter()
+        assert L.pbft_replica_push_many(rep, n, kind.ctypes.data, view.ctypes.data, seq.ctypes.data, digs.ctypes.data,
+                                        signer.ctypes.data, sigs.ctypes.data, ctypes.byref(qd)) == 0 and qd.value == n
+        t_push = time.perf_counter() - t
+        rows, ne = ctypes.c_uint64(), ctypes.c_uint32()
+        t0 = time.perf_counter()
+        assert L.pbft_replica_flush_submit(rep, 0, ctypes.byref(rows)) == 0
+        t1 = time.perf_counter()
+        polls = 0
+        while True:
+            rc = L.pbft_replica_flush_poll(rep, ev, len(ev), ctypes.byref(ne))
+            assert rc >= 0
+            if rc == 1:
+                break
+            polls += 1
+        t2 = time.perf_counter()
+        assert rows.value == n + n_seq
+        st = Stats()
+        L.pbft_replica_get_stats(rep, ctypes.byref(st))
+        assert st.rejected_sig == int((~expect).sum()) and st.batches == 1
+        committed = sum(1 for e in ev[: ne.value] if e.kind == 2)
+        assert committed == n_seq, committed
+        L.pbft_replica_destroy(rep)
+        if r:  # round 0 warms the staging
+            res["submit_ms"].append((t1 - t0) * 1e3)
+            res["e2e_ms"].append((t2 - t0) * 1e3)
+            res["polls"].append(polls)
+            res["push_ms"].append(t_push * 1e3)
+    e2e = float(np.median(res["e2e_ms"]))
+    return {"value": n / (e2e * 1e-3), "unit": "verifies/s", "ms_per_round": e2e,
+            "flush_submit_ms": float(np.median(res["submit_ms"])), "polls_while_running": int(np.median(res["polls"])),
+            "push_many_ms": float(np.median(res["push_ms"])), "sigs": n + n_seq, "rounds": rounds,
+            "path": "pbft_replica: push_many (2^20 votes + 2048 PrePrepares, untimed) -> flush_submit (votes form "
+                    "into pinned staging, async H2D + kernels + D2H) -> flush_poll loop until the bitmap is applied "
+                    "and 2048 COMMITTED_LOCAL events are out; H2D 70 B/sig + 4096 envelopes"}
+
+
+def plan_legs(v, pub, d, n, stream, torch):
+    """what a re-keying costs (set_keys of the n = 256 replica keys: decompress, small-order
+    check, comb tables) and the 2^20 device-resident rate of every key plan a shared or smaller GPU falls back to
+    (forced with PBFT_OPT_KEY_TABLE_BUDGET_MB).  Restores the default plan at the end."""
+    import re
+    info = v._lib.pbft_build_info().decode()
+    pas = [int(x) for x in re.search(r"PA=([\d|]+)", info).group(1).split("|")]
+    sizes = [int(x) for x in re.search(r"tabA/key=([\dB|]+)", info).group(1).replace("B", "").split("|")]
+    per_key = dict(zip(pas, sizes))
+    out = {}
+    torch.cuda.synchronize()
+    for name, budget in (("PLA_BIG_14", 100_000), ("PLA_MID_16", 20_000), ("PLA_SMALL_32", 1_000),
+                         ("default", 0)):
+        v.set_option(v.OPT_KEY_TABLE_BUDGET_MB, budget)
+        t = time.perf_counter()
+        assert v.set_keys(pub).all()
+        ms_keys = (time.perf_counter() - t) * 1e3
+        pb, pa = v.positions()
+        time_device(v, stream, d, n, 3, torch)
+        k, w = time_device(v, stream, d, n, 20, torch)
+        out[name] = {"positions": [pb, pa], "steps": pb + pa, "set_keys_ms": ms_keys, "kernel_ms": k,
+                     "verifies_per_s": n / (k * 1e-3), "key_tables_gb": per_key.get(pa, 0) * len(pub) / 1e9}
+    return out
+
+
+def shuffled_leg(v, d, n, stream, torch, dev, expect):
+    """The headline round with its rows in a random order (every wave mixes envelopes and keys: block 2's SHA-512
+    schedule per lane instead of the scalar unit's per-wave copy); VERDICT r02 item 9."""
+    from pbft_amd import bitmap_to_bool
+    perm = torch.from_numpy(np.random.default_rng(7).permutation(n)).to(dev)
+    M = d["M"][: n * ENVELOPE].view(n, ENVELOPE)[perm].reshape(-1)
+    ds = {"R": d["R"][perm].contiguous(), "S": d["S"][perm].contiguous(), "K": d["K"][perm].contiguous(),
+          "M": torch.cat([M, torch.zeros(64, dtype=M.dtype, device=dev)]), "B": torch.zeros_like(d["B"])}
+    time_device(v, stream, ds, n, 2, torch)
+    got = bitmap_to_bool(ds["B"].cpu().numpy().view(np.uint64), n)
+    assert (got == expect[perm.cpu().numpy()]).all(), "shuffled round bitmap differs"
+    k, w = time_device(v, stream, ds, n, 20, torch)
+    return {"kernel_ms": k, "verifies_per_s": n / (k * 1e-3),
+            "note": "same 2^20 round, rows randomly permuted (device-resident)"}
+
+
 def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 signatures per window batch, one GPU
     (device-resident p50 and host-buffer p50) vs the CPU baselines on the same batch."""
@@ -402,7 +524,9 @@ def main():
     S, bad = corrupt(S_good, ADV_FRAC, SEED)
     expect = np.ones(n_total, bool)
     expect[bad] = False
+    t_keys = time.perf_counter()
     key_ok = v.set_keys(pub)
+    set_keys_ms = (time.perf_counter() - t_keys) * 1e3  # n = 256: decompression, small-order check, comb tables
     assert key_ok.all()
     pb, pa = v.positions()  # the key plan set_keys chose for this key set
 
@@ -564,11 +688,18 @@ def main():
         # (>= 10k batches for the p50 / p99, as SURVEY §8d asks: 20 s at 512 batches/s)
         extras["stream_4k"] = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21),
                                                                       duration_s=args.stream_s),
+                               "offered_2^21_per_gpu_pageable": stream_latency(v, R, S, key_idx, msg, float(1 << 21),
+                                                                               duration_s=args.stream_s / 2,
+                                                                               pinned=False),
                                "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
         extras["e2e_2^20"] = e2e_host_round(v, R, S, key_idx, msg, expect, torch)
         extras["e2e_votes_2^20"] = e2e_votes_round(v, R, S, key_idx, msg, expect, torch)
         extras["votes_device_2^20"] = votes_device_round(v, d, msg, expect, stream, torch, dev)
         extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
+        extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect)
+        extras["shuffled_2^20"] = shuffled_leg(v, d, n, stream, torch, dev, expect)
+        extras["set_keys_ms"] = set_keys_ms
+        extras["key_plans_2^20"] = plan_legs(v, pub, d, n, stream, torch)
 
     if rank == 0:
         total = n_total * args.steps

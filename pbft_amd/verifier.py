@@ -56,6 +56,12 @@ class SigBatch:
         return len(self.R)
 
 
+class VotesStaging(ctypes.Structure):
+    """pbft_votes_staging (include/pbft_verify.h)."""
+    _fields_ = [("sig", ctypes.c_void_p), ("key_idx", ctypes.c_void_p), ("env_idx", ctypes.c_void_p),
+                ("envelopes", ctypes.c_void_p)]
+
+
 def bitmap_to_bool(bitmap: np.ndarray, n: int) -> np.ndarray:
     """LSB-first u64 words -> bool[n]."""
     bits = np.unpackbits(bitmap.view(np.uint8), bitorder="little")
@@ -71,6 +77,33 @@ def verify_multi(verifiers, b: "SigBatch") -> np.ndarray:
     check(lib.pbft_verify_batch_multi(arr, len(verifiers), _ptr(b.R), _ptr(b.S), _ptr(b.key_idx), _ptr(b.msg),
                                       b.msg_len, b.msg.shape[1], n, _ptr(out)))
     return out
+
+
+class MultiGpu:
+    """pbft_multi_create / pbft_verify_batch_device_multi: one context per device of this process, the round's
+    bitmap words all-gathered on RCCL (include/pbft_verify.h)."""
+
+    def __init__(self, verifiers):
+        self._lib = load()
+        self._m = ctypes.c_void_p()
+        arr = (ctypes.c_void_p * len(verifiers))(*[v._ctx.value for v in verifiers])
+        check(self._lib.pbft_multi_create(arr, len(verifiers), ctypes.byref(self._m)))
+        self.n = len(verifiers)
+
+    def verify_device(self, d_R, d_S, d_K, d_M, n, words_per_rank, d_bitmaps, msg_len=85, msg_stride=85):
+        """Per-rank lists of device pointers / counts; enqueue only (sync() to wait)."""
+        P = ctypes.c_void_p * self.n
+        check(self._lib.pbft_verify_batch_device_multi(self._m, P(*d_R), P(*d_S), P(*d_K), P(*d_M), msg_len,
+                                                       msg_stride, (ctypes.c_uint64 * self.n)(*n), words_per_rank,
+                                                       P(*d_bitmaps)))
+
+    def sync(self):
+        check(self._lib.pbft_multi_sync(self._m))
+
+    def close(self):
+        if self._m:
+            self._lib.pbft_multi_destroy(self._m)
+            self._m = ctypes.c_void_p()
 
 
 class GpuBatchVerifier:
@@ -163,6 +196,44 @@ class GpuBatchVerifier:
         out = np.zeros((n + 63) // 64, dtype=np.uint64)
         check(self._lib.pbft_verify_votes(self._ctx, _ptr(R), _ptr(S), _ptr(K), _ptr(I), _ptr(E), len(E), n, _ptr(out)))
         return out
+
+    def submit_votes(self, R, S, key_idx, env_idx, envelopes) -> int:
+        """pbft_verify_votes_async: non-blocking votes form; complete with poll / wait (the library copies
+        pageable buffers into its pinned staging, so the arrays may be reused once this returns)."""
+        R = np.ascontiguousarray(R, np.uint8).reshape(-1, 32)
+        S = np.ascontiguousarray(S, np.uint8).reshape(-1, 32)
+        K = np.ascontiguousarray(key_idx, np.uint16).reshape(-1)
+        I = np.ascontiguousarray(env_idx, np.uint32).reshape(-1)
+        E = np.ascontiguousarray(envelopes, np.uint8).reshape(-1, 85)
+        n = len(R)
+        if not (len(S) == len(K) == len(I) == n):
+            raise ValueError("R, S, key_idx, env_idx must have the same length")
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_votes_async(self._ctx, _ptr(R), _ptr(S), _ptr(K), _ptr(I), _ptr(E), len(E), n,
+                                                _ptr(out)))
+        self._pending = ((R, S, K, I, E), out)  # (pinned inputs are DMA'd in place: keep them alive)
+        return id(out)
+
+    def stage_votes(self, n: int, n_env: int) -> dict:
+        """pbft_verify_votes_stage: numpy views of the context's pinned staging for an (n, n_env) votes batch
+        (sig rows R || S, key_idx, env_idx, envelopes), to be filled in place and launched by submit_staged."""
+        st = VotesStaging()
+        check(self._lib.pbft_verify_votes_stage(self._ctx, n, n_env, ctypes.byref(st)))
+
+        def view(ptr, dtype, shape):
+            count = int(np.prod(shape))
+            if count == 0:
+                return np.zeros(shape, dtype)
+            buf = (ctypes.c_uint8 * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dtype).reshape(shape)
+        return {"sig": view(st.sig, np.uint8, (n, 64)), "key_idx": view(st.key_idx, np.uint16, (n,)),
+                "env_idx": view(st.env_idx, np.uint32, (n,)), "envelopes": view(st.envelopes, np.uint8, (n_env, 85))}
+
+    def submit_staged(self, n: int, n_env: int) -> int:
+        out = np.zeros((n + 63) // 64, dtype=np.uint64)
+        check(self._lib.pbft_verify_votes_submit(self._ctx, n, n_env, _ptr(out)))
+        self._pending = (None, out)
+        return id(out)
 
     def verify_votes_device(self, d_R: int, d_S: int, d_key_idx: int, d_env_idx: int, d_envelopes: int,
                             n_env: int, n: int, d_bitmap: int, stream: int = 0) -> None:

@@ -546,3 +546,88 @@ def test_votes_form_matches_oracle_and_soa(gv, coracle):
     g4 = bitmap_to_bool(gv.verify_votes(RR, SS, KK, II, env), len(RR))
     g5 = bitmap_to_bool(gv.verify(SigBatch(RR, SS, KK, MM, 85)), len(RR))
     assert (g4 == g5).all() and (g4[:n] == exp).all()
+
+
+def test_async_host_forms_pinned_staging(gv, coracle):
+    """The non-blocking host-buffer forms: pbft_verify_batch_async and pbft_verify_votes_async
+    copy pageable buffers into the context's pinned staging before returning (the caller may reuse them at once:
+    they are overwritten here while the batch runs), DMA pinned buffers in place, and the zero-copy
+    pbft_verify_votes_stage / _submit pair fills the staging directly.  All equal the oracle."""
+    import torch
+    from pbft_amd import SigBatch, bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=41)   # 65,536 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(41)
+    R, S, K, M, _ = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R, S, K, M, 85)
+    n = len(R)
+    env, inv = np.unique(M, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    # pageable, overwritten right after submit
+    for form in ("batch", "votes"):
+        Rc, Sc, Kc, Mc, Ic, Ec = R.copy(), S.copy(), K.copy(), M.copy(), ei.copy(), env.copy()
+        t = gv.submit(SigBatch(Rc, Sc, Kc, Mc, 85)) if form == "batch" else gv.submit_votes(Rc, Sc, Kc, Ic, Ec)
+        for a in (Rc, Sc, Mc, Ec):
+            a[:] = 0x5A
+        Kc[:] = 1
+        Ic[:] = 0
+        out = gv.wait(t)
+        assert (bitmap_to_bool(out, n) == exp).all(), form
+    # pinned caller buffers: DMA'd in place (kept alive until completion)
+    pin = lambda a: torch.from_numpy(np.ascontiguousarray(a)).pin_memory().numpy()  # noqa: E731
+    t = gv.submit_votes(pin(R), pin(S), pin(K), pin(ei), pin(env))
+    out = None
+    while out is None:
+        out = gv.poll(t)
+    assert (bitmap_to_bool(out, n) == exp).all()
+    # zero-copy staging
+    st = gv.stage_votes(n, len(env))
+    st["sig"][:, :32] = R
+    st["sig"][:, 32:] = S
+    st["key_idx"][:] = K
+    st["env_idx"][:] = ei
+    st["envelopes"][:] = env
+    t = gv.submit_staged(n, len(env))
+    assert (bitmap_to_bool(gv.wait(t), n) == exp).all()
+    # a submit without a matching stage is refused; one batch in flight per context
+    from pbft_amd import PbftError
+    with pytest.raises(PbftError):
+        gv.submit_staged(n, len(env))
+    t = gv.submit_votes(R, S, K, ei, env)
+    with pytest.raises(PbftError):
+        gv.submit_votes(R, S, K, ei, env)
+    gv.wait(t)
+
+
+def test_multi_gpu_rccl_allgather_one_rank(gv, coracle):
+    """pbft_multi_create / pbft_verify_batch_device_multi on the one GPU of this box: a
+    1-rank RCCL communicator, the shard verified into its slice of the padded rank-major bitmap, then
+    ncclAllGather.  (Unmeasured on 8 GPUs: the multi-rank layout is the same as bench.py's, gloo-tested.)"""
+    import torch
+    from pbft_amd import MultiGpu, bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 8, 160, tag=43)     # 2,560 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(43)
+    R, S, K, M, _ = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R, S, K, M, 85)
+    n = len(R) - 5                                                        # ragged: not a multiple of 64
+    dev = torch.device("cuda", 0)
+    dR, dS = torch.from_numpy(R[:n].copy()).to(dev), torch.from_numpy(S[:n].copy()).to(dev)
+    dK = torch.from_numpy(K[:n].view(np.int16).copy()).to(dev)
+    mp = np.zeros(n * 85 + 64, np.uint8)
+    mp[: n * 85] = M[:n].reshape(-1)
+    dM = torch.from_numpy(mp).to(dev)
+    wpr = (n + 63) // 64 + 3                                              # padded slice: 3 extra words
+    dB = torch.full((wpr,), -1, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    m = MultiGpu([gv])
+    try:
+        m.verify_device([dR.data_ptr()], [dS.data_ptr()], [dK.data_ptr()], [dM.data_ptr()], [n], wpr,
+                        [dB.data_ptr()])
+        m.sync()
+    finally:
+        m.close()
+    words = dB.cpu().numpy().view(np.uint64)
+    assert (bitmap_to_bool(words, n) == exp[:n]).all()
+    assert (words[(n + 63) // 64:] == 0).all()                            # padding words zeroed
+    assert int(words[n // 64]) >> (n % 64) == 0                          # bits past n
