@@ -16,6 +16,10 @@
 // launch, return) and pbft_replica_flush_poll (apply the bitmap, emit events) so
 // that the loop never blocks on the GPU.
 #include <algorithm>
+#ifdef PBFT_REPLICA_TIMING
+#include <chrono>
+#include <cstdio>
+#endif
 #include <array>
 #include <cstring>
 #include <deque>
@@ -102,6 +106,15 @@ struct Phase {
     sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
     n_pending = 0;
   }
+  // back to a fresh phase, keeping every allocation (recycled windows)
+  void reset() {
+    clear_candidates();
+    std::fill(cnt.begin(), cnt.end(), 0);
+    std::fill(acc.begin(), acc.end(), 0);
+    acc_digs.clear();
+    acc_cnt.clear();
+    distinct = 0;
+  }
   uint32_t acc_index(const Digest& d) {  // index into acc_digs (appended if new)
     for (size_t j = 0; j < acc_digs.size(); ++j)
       if (acc_digs[j] == d) return (uint32_t)j;
@@ -116,10 +129,16 @@ struct Window {
   bool have_pre_prepare = false;
   Digest digest{};
   bool pre_prepared_reported = false, prepared_reported = false, committed_reported = false;
+  void reset() {
+    for (Phase& p : ph) p.reset();
+    have_pre_prepare = pre_prepared_reported = prepared_reported = committed_reported = false;
+  }
 };
+using WindowMap = std::map<std::pair<uint64_t, uint64_t>, Window>;
 
 // One phase of the in-flight batch: rows [row0, row0 + count) are its first `count` candidates.
 struct Seg {
+  Window* w;  // valid unless a window was erased while the batch was in flight (then looked up by key)
   Key key;
   uint64_t row0;
   uint32_t count;
@@ -137,7 +156,8 @@ struct pbft_replica {
   uint64_t log_window = PBFT_DEFAULT_LOG_WINDOW;
   std::vector<uint8_t> keys;
   std::unordered_map<std::string, uint32_t> key_index;
-  std::map<Key, Window> windows;
+  WindowMap windows;
+  std::vector<WindowMap::node_type> spare;  // GC'd windows kept for reuse (no allocation per round)
   std::set<Key> dirty;                    // windows whose events must be (re-)evaluated
   std::deque<pbft_round_event> evq;       // decided, not yet delivered
   std::map<uint64_t, uint64_t> done;      // seqs of current_view committed locally and GC'd: [lo, hi]
@@ -156,6 +176,7 @@ struct pbft_replica {
   int in_flight_via = 0;  // 0 GPU context, 1 votes override, 2 SoA override (already complete)
   std::vector<Seg> segs;
   uint64_t rows = 0;
+  bool erased_in_flight = false;  // a stable checkpoint erased windows while the batch was in flight
   std::vector<uint64_t> bitmap;
   // host buffers of the verifier overrides (the GPU path fills the context's pinned staging instead)
   std::vector<uint8_t> hSig, hR, hS, hM, hE;
@@ -207,10 +228,30 @@ static std::string key_str(const uint8_t* A) { return std::string((const char*)A
 
 static Window& window_at(pbft_replica* r, const Key& k) {
   if (r->last_w && r->last_key == k) return *r->last_w;
-  Window& w = r->windows[k];
+  auto it = r->windows.find(k);
+  if (it == r->windows.end()) {
+    if (!r->spare.empty()) {
+      auto nh = std::move(r->spare.back());
+      r->spare.pop_back();
+      nh.key() = k;
+      nh.mapped().reset();
+      it = r->windows.insert(std::move(nh)).position;
+    } else {
+      it = r->windows.emplace(k, Window()).first;
+    }
+  }
   r->last_key = k;
-  r->last_w = &w;
-  return w;
+  r->last_w = &it->second;
+  return it->second;
+}
+
+// erase a window, keeping its node (and every vector in it) for the next window
+static WindowMap::iterator drop_window(pbft_replica* r, WindowMap::iterator it) {
+  auto next = std::next(it);
+  if (r->in_flight) r->erased_in_flight = true;
+  if (r->spare.size() < 4096) r->spare.push_back(r->windows.extract(it));
+  else r->windows.erase(it);
+  return next;
 }
 
 // seqs of the current view committed locally whose windows are gone (interval set)
@@ -251,7 +292,7 @@ static void gc(pbft_replica* r) {
     if (it == r->windows.end() || !it->second.committed_reported) break;
     record_done(r, r->h + 1);
     r->dirty.erase(it->first);
-    r->windows.erase(it);
+    drop_window(r, it);
     ++r->h;
     ++r->stats.windows_gc;
   }
@@ -261,7 +302,7 @@ static void gc(pbft_replica* r) {
     if (it->first.second <= r->h) {
       if (it->second.committed_reported && it->first.first == r->current_view) record_done(r, it->first.second);
       r->dirty.erase(it->first);
-      it = r->windows.erase(it);
+      it = drop_window(r, it);
       ++r->stats.windows_gc;
     } else {
       ++it;
@@ -315,68 +356,115 @@ static void revert_segs(pbft_replica* r) {
   }
   r->segs.clear();
   r->in_flight = false;
+  r->erased_in_flight = false;
 }
 
 // The finished batch: State::insert_* for accepted candidates (in push order: the last accepted vote of a signer
 // wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
-// candidates leave the windows.
+// candidates leave the windows.  Segments [s0, s1) (whole windows: a window's segments stay on one thread, in
+// order); counts into st[3] = accepted, rejected_sig, rejected_digest; touched[g] = some candidate accepted.
+static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st[3], uint8_t* touched) {
+  std::vector<int64_t> amap;
+  std::vector<uint8_t> mism;
+  for (size_t gi = s0; gi < s1; ++gi) {
+    const Seg& g = r->segs[gi];
+    Window* wp = g.w;
+    if (r->erased_in_flight) {
+      auto wi = r->windows.find(g.key);
+      if (wi == r->windows.end()) continue;  // window erased (stable checkpoint) while the batch was in flight
+      wp = &wi->second;
+    }
+    Window& w = *wp;
+    Phase& p = w.ph[g.kind];
+    const uint64_t* bm = r->bitmap.data();
+    uint32_t acc_n = 0;
+    if (g.kind == 0) {
+      for (uint32_t i = 0; i < g.count; ++i) {
+        const uint64_t row = g.row0 + i;
+        if (!((bm[row >> 6] >> (row & 63)) & 1)) continue;
+        ++acc_n;
+        const Digest& d = p.digs[p.dix[i]];
+        if (!w.have_pre_prepare) {
+          w.have_pre_prepare = true;
+          w.digest = d;
+        } else if (w.digest != d) {
+          ++st[2];
+        }
+      }
+    } else {
+      amap.assign(p.digs.size(), -1);
+      mism.resize(p.digs.size());
+      for (size_t j = 0; j < p.digs.size(); ++j) mism[j] = w.have_pre_prepare && p.digs[j] != w.digest;
+      const uint16_t* who = p.who.data();
+      const uint32_t* dix = p.dix.data();
+      uint32_t* acc = p.acc.data();
+      uint8_t* cnt = p.cnt.data();
+      const bool one = p.digs.size() == 1;
+      if (one) amap[0] = p.acc_index(p.digs[0]);
+      for (uint32_t i = 0; i < g.count; ++i) {
+        const uint64_t row = g.row0 + i;
+        const uint32_t s = who[i];
+        if ((bm[row >> 6] >> (row & 63)) & 1) {
+          ++acc_n;
+          const uint32_t d = one ? 0 : dix[i];
+          if (amap[d] < 0) amap[d] = p.acc_index(p.digs[d]);
+          const uint32_t a = (uint32_t)amap[d] + 1;
+          if (acc[s] != a) {
+            if (acc[s]) --p.acc_cnt[acc[s] - 1];
+            acc[s] = a;
+            ++p.acc_cnt[a - 1];
+          }
+          st[2] += mism[d];
+        }
+        if (--cnt[s] == 0 && !acc[s]) --p.distinct;
+      }
+    }
+    st[0] += acc_n;
+    st[1] += g.count - acc_n;
+    p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
+    touched[gi] = acc_n > 0;
+  }
+}
+
 static void apply_segs(pbft_replica* r) {
   ++r->stats.batches;
   r->stats.verified += r->rows;
-  std::vector<int64_t> amap;
-  std::vector<uint8_t> mism;
-  for (const Seg& g : r->segs) {
-    auto wi = r->windows.find(g.key);
-    if (wi == r->windows.end()) continue;  // window erased (stable checkpoint) while the batch was in flight
-    Window& w = wi->second;
-    Phase& p = w.ph[g.kind];
-    amap.assign(p.digs.size(), -1);
-    bool any = false;
-    for (uint32_t i = 0; i < g.count; ++i) {
-      const uint64_t row = g.row0 + i;
-      const bool ok = (r->bitmap[row >> 6] >> (row & 63)) & 1;
-      const uint32_t d = p.dix[i];
-      if (!ok) {
-        ++r->stats.rejected_sig;
-      } else {
-        ++r->stats.accepted;
-        any = true;
-      }
-      if (g.kind == 0) {
-        if (!ok) continue;
-        if (!w.have_pre_prepare) {
-          w.have_pre_prepare = true;
-          w.digest = p.digs[d];
-        } else if (w.digest != p.digs[d]) {
-          ++r->stats.rejected_digest;
-        }
-        continue;
-      }
-      const uint32_t s = p.who[i];
-      if (ok) {
-        if (amap[d] < 0) amap[d] = p.acc_index(p.digs[d]);
-        const uint32_t a = (uint32_t)amap[d];
-        if (p.acc[s] != a + 1) {
-          if (p.acc[s]) --p.acc_cnt[p.acc[s] - 1];
-          p.acc[s] = a + 1;
-          ++p.acc_cnt[a];
-        }
-        if (w.have_pre_prepare && p.digs[d] != w.digest) ++r->stats.rejected_digest;
-      }
-      if (--p.cnt[s] == 0 && !p.acc[s]) --p.distinct;
+  const size_t G = r->segs.size();
+  std::vector<uint8_t> touched(G, 0);
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t T = r->rows >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, 8), G) : 1;
+  std::vector<std::array<uint64_t, 3>> st(T, {0, 0, 0});
+  if (T <= 1) {
+    apply_range(r, 0, G, st[0].data(), touched.data());
+  } else {
+    std::vector<std::thread> th;
+    size_t s0 = 0;
+    for (size_t t = 0; t < T && s0 < G; ++t) {  // balanced by rows, cut at window boundaries
+      const uint64_t hi_row = r->rows * (t + 1) / T;
+      size_t s1 = s0 + 1;
+      while (s1 < G && (t + 1 == T || r->segs[s1].row0 < hi_row || r->segs[s1].key == r->segs[s1 - 1].key)) ++s1;
+      th.emplace_back(apply_range, r, s0, s1, st[t].data(), touched.data());
+      s0 = s1;
     }
-    p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
-    if (any) r->dirty.insert(g.key);
+    for (auto& x : th) x.join();
   }
+  for (const auto& c : st) {
+    r->stats.accepted += c[0];
+    r->stats.rejected_sig += c[1];
+    r->stats.rejected_digest += c[2];
+  }
+  for (size_t gi = 0; gi < G; ++gi)
+    if (touched[gi]) r->dirty.insert(r->segs[gi].key);
   r->segs.clear();
   r->in_flight = false;
+  r->erased_in_flight = false;
 }
 
 // Copy the candidates of segments [s0, s1) into the batch (pinned staging or the overrides' buffers).
 static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
-    Phase& p = r->windows.find(g.key)->second.ph[g.kind];
+    Phase& p = g.w->ph[g.kind];
     memcpy(SIG + 64 * g.row0, p.sig.data(), 64 * (size_t)g.count);
     memcpy(K + g.row0, p.who.data(), 2 * (size_t)g.count);
     if (p.digs.size() == 1) {
@@ -566,7 +654,7 @@ int pbft_replica_flush_submit(pbft_replica* r, int force, uint64_t* n_rows) {
     for (int kind = 0; kind < 3; ++kind) {
       if (!rd[kind]) continue;
       Phase& p = w.ph[kind];
-      r->segs.push_back({kv.first, N, (uint32_t)p.size(), E, (uint8_t)kind});
+      r->segs.push_back({&w, kv.first, N, (uint32_t)p.size(), E, (uint8_t)kind});
       N += p.size();
       E += (uint32_t)p.digs.size();
     }
@@ -644,7 +732,21 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
     else if (r->in_flight_via == 1) st = r->vpoll(r->vuser);
     if (st == 0) return 0;
     if (st < 0) { revert_segs(r); return st; }
+#ifdef PBFT_REPLICA_TIMING
+    auto t0 = std::chrono::steady_clock::now();
+#endif
     apply_segs(r);
+#ifdef PBFT_REPLICA_TIMING
+    auto t1 = std::chrono::steady_clock::now();
+    evaluate(r);
+    auto t2 = std::chrono::steady_clock::now();
+    gc(r);
+    auto t3 = std::chrono::steady_clock::now();
+    fprintf(stderr, "apply %.2f ms evaluate %.2f ms gc %.2f ms\n",
+            std::chrono::duration<double, std::milli>(t1 - t0).count(),
+            std::chrono::duration<double, std::milli>(t2 - t1).count(),
+            std::chrono::duration<double, std::milli>(t3 - t2).count());
+#endif
   }
   evaluate(r);
   gc(r);
