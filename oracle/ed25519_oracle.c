@@ -25,6 +25,7 @@
 #include <stddef.h>
 #include <string.h>
 #include <pthread.h>
+#include <stdlib.h>
 
 typedef unsigned __int128 u128;
 typedef struct { uint64_t v[5]; } fe;
@@ -392,21 +393,39 @@ int oracle_key_ok(const uint8_t pk[32]) {
   return !ge_is_small_order(&A);
 }
 
-/* ed25519-dalek 1.0.1 verify_strict: 1 = accept, 0 = reject */
-int oracle_verify_strict(const uint8_t pk[32], const uint8_t sig[64], const uint8_t *msg, size_t len) {
-  pthread_once(&init_once, init_consts);
+/* verify_strict given the key already decoded the way a dalek PublicKey holds it: negA = -A (a_ok = 0: the
+ * encoding did not decompress or A has small order -- every signature under it is rejected) */
+static int verify_strict_negA(const ge *negA, int a_ok, const uint8_t pk[32], const uint8_t sig[64],
+                              const uint8_t *msg, size_t len) {
   const uint8_t *s = sig + 32;
   if (!sc_lt_L(s)) return 0;                       /* check_scalar */
-  ge A, R, negA, Rp;
-  if (!ge_decompress(&A, pk)) return 0;            /* PublicKey::from_bytes */
+  if (!a_ok) return 0;
+  ge R, Rp;
   if (!ge_decompress(&R, sig)) return 0;           /* signature.R.decompress() */
-  if (ge_is_small_order(&R) || ge_is_small_order(&A)) return 0;
+  if (ge_is_small_order(&R)) return 0;
   uint8_t h[64], k[32];
   sha512_3(h, sig, 32, pk, 32, msg, len);          /* R || A || M, raw bytes */
   sc_reduce(k, h, 64);                             /* Scalar::from_hash */
-  ge_neg(&negA, &A);
-  ge_double_scalarmult(&Rp, k, &negA, s, &GE_B);  /* [k](-A) + [s]B */
+  ge_double_scalarmult(&Rp, k, negA, s, &GE_B);   /* [k](-A) + [s]B */
   return ge_eq(&Rp, &R);                           /* EdwardsPoint == */
+}
+
+/* PublicKey::from_bytes (decompression) + the small-order rejection verify_strict applies to A */
+static int decode_key(ge *negA, const uint8_t pk[32]) {
+  ge A;
+  if (!ge_decompress(&A, pk)) return 0;
+  if (ge_is_small_order(&A)) return 0;
+  ge_neg(negA, &A);
+  return 1;
+}
+
+/* ed25519-dalek 1.0.1 verify_strict: 1 = accept, 0 = reject */
+int oracle_verify_strict(const uint8_t pk[32], const uint8_t sig[64], const uint8_t *msg, size_t len) {
+  pthread_once(&init_once, init_consts);
+  if (!sc_lt_L(sig + 32)) return 0;                /* check_scalar first, as dalek */
+  ge negA;
+  const int a_ok = decode_key(&negA, pk);
+  return verify_strict_negA(&negA, a_ok, pk, sig, msg, len);
 }
 
 void oracle_public_key(uint8_t pk[32], const uint8_t seed[32]) {
@@ -447,6 +466,7 @@ void oracle_sign(uint8_t sig[64], const uint8_t seed[32], const uint8_t *msg, si
 typedef struct {
   const uint8_t *R, *S, *msg, *keys; const uint16_t *key_idx;
   uint32_t msg_len, msg_stride, n_keys; uint64_t lo, hi; uint8_t *acc;
+  const ge *negA; const uint8_t *a_ok;
 } job_t;
 static void *batch_worker(void *arg) {
   job_t *j = (job_t *)arg;
@@ -456,30 +476,39 @@ static void *batch_worker(void *arg) {
     if (ki >= j->n_keys) { j->acc[i] = 0; continue; }
     memcpy(sig, j->R + 32 * i, 32);
     memcpy(sig + 32, j->S + 32 * i, 32);
-    j->acc[i] = (uint8_t)oracle_verify_strict(j->keys + 32 * (size_t)ki, sig,
-                                              j->msg + (size_t)j->msg_stride * i, j->msg_len);
+    j->acc[i] = (uint8_t)verify_strict_negA(&j->negA[ki], j->a_ok[ki], j->keys + 32 * (size_t)ki, sig,
+                                            j->msg + (size_t)j->msg_stride * i, j->msg_len);
   }
   return NULL;
 }
+/* Like a libp2p replica, which decodes each peer's key once (PublicKey::from_bytes) and verifies many
+ * signatures under it, the batch decodes the n_keys keys first (-A and the small-order check), then
+ * verifies every signature against the decoded key. */
 int oracle_verify_batch(const uint8_t *keys, uint32_t n_keys, const uint8_t *R, const uint8_t *S,
                         const uint16_t *key_idx, const uint8_t *msg, uint32_t msg_len, uint32_t msg_stride,
                         uint64_t N, uint8_t *accept_bytes, int nthreads) {
   pthread_once(&init_once, init_consts);
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
+  ge *negA = (ge *)malloc(sizeof(ge) * (n_keys ? n_keys : 1));
+  uint8_t *a_ok = (uint8_t *)malloc(n_keys ? n_keys : 1);
+  if (!negA || !a_ok) { free(negA); free(a_ok); return -1; }
+  for (uint32_t k = 0; k < n_keys; ++k) a_ok[k] = (uint8_t)decode_key(&negA[k], keys + 32 * (size_t)k);
   pthread_t th[256];
   job_t jobs[256];
   uint64_t per = (N + nthreads - 1) / nthreads;
-  int started = 0;
+  int started = 0, rc = 0;
   for (int t = 0; t < nthreads; ++t) {
     uint64_t lo = per * t, hi = lo + per > N ? N : lo + per;
     if (lo >= hi) break;
-    jobs[t] = (job_t){R, S, msg, keys, key_idx, msg_len, msg_stride, n_keys, lo, hi, accept_bytes};
-    if (pthread_create(&th[t], NULL, batch_worker, &jobs[t]) != 0) return -1;
+    jobs[t] = (job_t){R, S, msg, keys, key_idx, msg_len, msg_stride, n_keys, lo, hi, accept_bytes, negA, a_ok};
+    if (pthread_create(&th[t], NULL, batch_worker, &jobs[t]) != 0) { rc = -1; break; }
     ++started;
   }
   for (int t = 0; t < started; ++t) pthread_join(th[t], NULL);
-  return 0;
+  free(negA);
+  free(a_ok);
+  return rc;
 }
 
 typedef struct {
