@@ -508,8 +508,8 @@ def main():
 
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
     from pbft_amd.dist import allgather_bitmap, round_bitmap, shard_bounds, shard_words
-    from pbft_amd.roofline import (INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, products_comb,
-                                   products_per_verify)
+    from pbft_amd.roofline import (INPUT_BYTES, VALU_MAD_PEAK_PER_S, gather_bytes_per_verify, mad_peak_at,
+                                   products_comb, products_per_verify)
 
     n_rep, n_seq = args.replicas, args.seqs
     seeds = key_seeds(n_rep)
@@ -730,6 +730,9 @@ def main():
                        "parallelism": f"shard-by-index x{ws}" + (" + RCCL all-gather of bitmaps" if ws > 1 else "")},
             "roofline": {"bound": "valu", "achieved": products / 1e12, "peak": VALU_MAD_PEAK_PER_S / 1e12,
                          "unit": "T products/s (v_mad_u64_u32)", "frac": products / VALU_MAD_PEAK_PER_S,
+                         "peak_source": "profiles/r03/valu_clock.txt: v_mad_u64_u32 issue, 4.53 cycles per "
+                                        "wave-instruction per SIMD at the in-kernel clock 2.157 GHz",
+                         "peak_at_2.4GHz": mad_peak_at(2.4e9) / 1e12,
                          "traffic": pmc.get("traffic_bytes_per_launch"),
                          "traffic_source": pmc.get("source"),
                          "valu_busy_pct": pmc.get("valu_busy_pct"),

@@ -20,12 +20,30 @@ per lane):
 as products; the VALU-issue view is in profiles/*/summary*.txt.)
 
 VALU_MAD_PEAK_PER_S is the measured chip-wide v_mad_u64_u32 issue rate on
-MI355X (tools/microbench/valu_rates.hip, profiles/r01_valu_rates.txt).
+MI355X at the clock the chip holds under that load (tools/microbench/valu_clock.hip,
+profiles/r03/valu_clock.txt: 8 independent chains per lane, 8 waves per SIMD, >= 2 s
+of back-to-back launches first; the clock is stamped in-kernel as
+d(s_memtime) / d(s_memrealtime) x 100 MHz).  It issues one wave-instruction per
+4.53 cycles per SIMD at 2.157 GHz: 1024 SIMDs x 64 lanes / 4.53 x 2.157e9 = 31.2e12.
+(r01's 30.25e12 came from the same loop without a clock stamp; its "@2.4GHz"
+columns assumed the spec clock.  v_fma_f32 runs 2.29 cycles per wave-instruction
+with three distinct source VGPRs -- the guide's 2 -- but 3.79 with src1 == src2,
+the form r01 timed: that, not the VALU, was the gap to MI355X_MICROARCH.md's rate.)
 """
 import re
 
 FIN_M = 16
-VALU_MAD_PEAK_PER_S = 30.25e12
+VALU_MAD_PEAK_PER_S = 31.19e12   # measured, profiles/r03/valu_clock.txt
+MAD_CYCLES_PER_WAVE_INSTR = 4.53  # per SIMD, at the measured clock
+MAD_CLOCK_HZ = 2.157e9            # in-kernel clock during that measurement
+SIMDS = 256 * 4
+
+
+def mad_peak_at(clock_hz: float) -> float:
+    """v_mad_u64_u32 products/s the chip can issue at clock_hz (1024 SIMDs x 64 lanes / 4.53 cycles)."""
+    return SIMDS * 64 / MAD_CYCLES_PER_WAVE_INSTR * clock_hz
+
+
 VALU_OP_PEAK_PER_S = 37.2e12  # 32-bit VOP3 integer ops (v_add3_u32 / v_alignbit_b32), measured
 ENTRY_BYTES = 128
 INPUT_BYTES = 32 + 32 + 2 + 85  # R, S, key index, envelope

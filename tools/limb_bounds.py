@@ -17,7 +17,7 @@ def sub(a, b, off):
     for x, o in zip(b, off): assert x <= o, "sub underflow"
     return [x + o for x, o in zip(a, off)]
 def mulmax(f, g):
-    worst = 0
+    worst, cols = 0, []
     for k in range(10):
         s = 0
         for i in range(10):
@@ -27,6 +27,7 @@ def mulmax(f, g):
                 if i + j >= 10: c *= 19
                 s += c * f[i] * g[j]
         worst = max(worst, s)
+        cols.append(s)
     for x in f + g: assert x < 2**32
     for i, x in enumerate(g): assert 19 * x < 2**32, "19*g overflows u32"
     for i, x in enumerate(f):
@@ -34,7 +35,28 @@ def mulmax(f, g):
     if f is g:  # fe_sq precomputes 38*f_odd and 19*f_even
         for i, x in enumerate(f): assert (38 if i % 2 else 19) * x < 2**32, "fe_sq premult overflow"
     assert worst < 2**64, math.log2(worst)
+    chain1(cols)
     return math.log2(worst)
+
+
+def chain1(cols):
+    """fe_reduce_wide with PBFT_REDUCE_1CHAIN (0 -> 1 -> ... -> 9 -> 0 x19 -> 1) on columns <= cols: the
+    result must stay within CARRIED (h1 is the only limb above its width) and no step may overflow u64."""
+    h = list(cols)
+    for i in range(10):
+        w = 26 if i % 2 == 0 else 25
+        c = h[i] >> w
+        h[i] = (1 << w) - 1
+        if i < 9:
+            h[i + 1] += c
+        else:
+            h[0] += 19 * c
+        assert max(h) < 2**64
+    c = h[0] >> 26
+    h[0] = (1 << 26) - 1
+    h[1] += c
+    for x, b in zip(h, CARRIED):
+        assert x <= b, "chain1 overshoot"
 
 C = CARRIED
 # mixed add (comb step): P3 + halved affine Niels ((y+x)/2, (y-x)/2, dxy) with canonical table limbs
