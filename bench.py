@@ -142,8 +142,8 @@ def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_pmc_cur.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
-    for rnd in ("r02", "r01"):
-        p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_comb", "derived.json")
+    for rel in ("r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
+        p = os.path.join(ROOT, "profiles", rel, "derived.json")
         try:
             d = json.load(open(p))
         except (OSError, ValueError):
@@ -154,7 +154,7 @@ def pmc_traffic(pb: int, pa: int, n: int) -> dict:
                 "valu_busy_pct": d["comb_kernel"]["valu_busy_pct"],
                 "valu_insts_per_sig": d.get("valu_insts_per_sig_total"),
                 "valu_insts_per_sig_comb": d["comb_kernel"].get("valu_insts_per_sig"),
-                "source": f"profiles/{rnd}_pmc_comb/derived.json (PMC passes, not this run)"}
+                "source": f"profiles/{rel}/derived.json (PMC passes, not this run)"}
     return {}
 
 

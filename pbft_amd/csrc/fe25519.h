@@ -187,6 +187,67 @@ FE_FN void fe_mul(fe& h, const fe& f, const fe& g) {
   fe_reduce_wide(h, acc[0], acc[1], acc[2], acc[3], acc[4], acc[5], acc[6], acc[7], acc[8], acc[9]);
 }
 
+// acc' = a * b + acc with the accumulator pinned as the mad's addend, so that LLVM cannot re-associate a carry
+// that starts the chain into a separate 64-bit add.
+// acc' = a * b + acc, laundered: the opaque result keeps LLVM from re-associating a chain that starts with a
+// carry (it would add the carry last, as a separate 64-bit add); the add still folds into the v_mad_u64_u32.
+// (Writing the mad itself as inline asm was slower: its SGPR carry-out makes the hazard recognizer pad every
+// asm boundary with an s_nop.)
+FE_FN uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc) {
+  acc += MUL64(a, b);
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm("" : "+v"(acc));
+#endif
+  return acc;
+}
+
+// N independent products h[m] = f[m] g[m], each computed as ONE dependent chain over the columns: column k's
+// mads accumulate on top of column k-1's carry, so a carry costs one 64-bit shift and one mask and no 64-bit
+// add (fe_reduce_wide's single-chain arithmetic, PBFT_REDUCE_1CHAIN: identical outputs and bounds).  The N
+// chains are interleaved product by product, so a wave has N independent mads in flight.  For the comb step
+// of large batches (comb_kernel<..., CHAIN>); latency-bound code (one wave per SIMD) keeps fe_mul.
+template <int N>
+FE_FN void fe_mul_chain(fe* const h[], const fe* const f[], const fe* const g[]) {
+  uint32_t g19[N][10], fx[N][10], l[N][10];
+  uint64_t acc[N];
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      g19[m][i] = 19u * g[m]->v[i];
+      fx[m][i] = (i & 1) ? dbl32(f[m]->v[i]) : f[m]->v[i];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 10; ++k) {
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int j = k - i;  // g index; j < 0 wraps with x19
+      uint32_t fi[N], gj[N];
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        fi[m] = ((i & 1) && (j & 1)) ? fx[m][i] : f[m]->v[i];
+        gj[m] = j >= 0 ? g[m]->v[j] : g19[m][j + 10];
+      }
+#pragma unroll
+      for (int m = 0; m < N; ++m) acc[m] = (k == 0 && i == 0) ? MUL64(fi[m], gj[m]) : mad_acc(fi[m], gj[m], acc[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < N; ++m) {
+      l[m][k] = (uint32_t)acc[m] & ((k & 1) ? M25 : M26);
+      acc[m] >>= (k & 1) ? 25 : 26;
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < N; ++m) {
+    const uint64_t h0 = (uint64_t)l[m][0] + acc[m] * 19u;  // acc = the carry out of column 9
+    l[m][1] += (uint32_t)(h0 >> 26);
+    l[m][0] = (uint32_t)h0 & M26;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) h[m]->v[i] = l[m][i];
+  }
+}
+
 FE_FN void fe_sq_cols(uint64_t c[10], const fe& f) {
   const uint32_t f0 = f.v[0], f1 = f.v[1], f2 = f.v[2], f3 = f.v[3], f4 = f.v[4];
   const uint32_t f5 = f.v[5], f6 = f.v[6], f7 = f.v[7], f8 = f.v[8], f9 = f.v[9];

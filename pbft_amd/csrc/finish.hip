@@ -41,8 +41,31 @@ struct fin_unroll<0> {
 // multiplications and 1 / (2^LV FM) of an inversion, instead of 3 (FM - 1) + 2
 // and 1 / FM.  The down-sweep peels the partners off again:
 // 1 / t_k = (1 / t_{k+1}) q_k, since t_{k+1} = t_k q_k.
+#ifndef PBFT_FIN_LV_WAVES
+#define PBFT_FIN_LV_WAVES 1  // waves per SIMD the product-tree finish is compiled for (1: no scratch spills)
+#endif
+#ifndef PBFT_FIN_PREFETCH
+#define PBFT_FIN_PREFETCH 1
+#endif
+#ifndef PBFT_FIN_STAMPS
+#define PBFT_FIN_STAMPS 0  // 1: timing build -- every wave stamps s_memtime at its phase boundaries
+#endif
+#if PBFT_FIN_STAMPS
+#define FIN_STAMP_WAVES 4096
+__device__ uint64_t g_fin_stamp[FIN_STAMP_WAVES][12];
+#define FIN_STAMP(k) \
+  if (lane == 0 && wave < FIN_STAMP_WAVES) g_fin_stamp[wave][k] = __builtin_amdgcn_s_memtime()
+extern "C" int pbft_debug_fin_stamps(uint64_t* out, uint32_t waves) {
+  if (waves > FIN_STAMP_WAVES) waves = FIN_STAMP_WAVES;
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fin_stamp), sizeof(uint64_t) * 12 * waves, 0,
+                                  hipMemcpyDeviceToHost);
+}
+#else
+#define FIN_STAMP(k)
+#endif
+
 template <int FM, int LV>
-__global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU : 2) finish_kernel(const uint8_t* __restrict__ R,
+__global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU : PBFT_FIN_LV_WAVES) finish_kernel(const uint8_t* __restrict__ R,
                                                        uint32_t rs_stride,
                                                        const uint32_t* __restrict__ xyz,
                                                        const uint8_t* __restrict__ flags, uint64_t N,
@@ -51,19 +74,34 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const uint64_t base = wave * FM * 64 + lane;
   if (wave * FM * 64 >= N) return;
+  FIN_STAMP(0);
+#if PBFT_FIN_STAMPS
+  if (lane == 0 && wave < FIN_STAMP_WAVES) g_fin_stamp[wave][6] = __builtin_amdgcn_s_memrealtime();
+#endif
   const uint32_t* Xb = xyz;
   const uint32_t* Yb = xyz + 10 * N;
   const uint32_t* Zb = xyz + 20 * N;
   // prefix products of Z (lanes past N contribute 1)
   fe pre[FM];
+  // PRE: small FM keeps every Z and issues the X, Y loads before the inversion, so the back-substitution
+  // does not wait on memory (FM <= 4: ~100 more VGPRs, within the 2-waves-per-SIMD budget)
+  constexpr bool PRE = PBFT_FIN_PREFETCH && FM <= 4;
+  fe zs[PRE ? FM : 1], xs[PRE ? FM : 1], ys[PRE ? FM : 1];
   fin_unroll<FM>::up([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
     fe z;
     if (i < N) load_fe(z, Zb, N, i); else fe_one(z);
+    if constexpr (PRE) {
+      zs[m] = z;
+      const uint64_t ii = i < N ? i : 0;
+      load_fe(xs[m], Xb, N, ii);
+      load_fe(ys[m], Yb, N, ii);
+    }
     if constexpr (m == 0) pre[0] = z;
     else fe_mul(pre[m], pre[m - 1], z);
   });
+  FIN_STAMP(1);
   fe inv;
   fe tq[LV > 0 ? LV : 1];  // partner products of the butterfly levels
   fe t = pre[FM - 1];
@@ -73,6 +111,7 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
     for (int u = 0; u < 10; ++u) tq[k].v[u] = (uint32_t)__shfl_xor((int)t.v[u], 1 << k);
     fe_mul(t, t, tq[k]);
   });
+  FIN_STAMP(2);
 #if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
   inv = t;
 #elif PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
@@ -80,15 +119,25 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
 #else
   if constexpr (LV == 6) {
     // every lane holds the wave's product: the variable-time divsteps never diverge (inv25519.h)
+#if PBFT_FIN_STAMPS
+    uint64_t prof[3];
+    fe_invert_var(inv, t, prof);
+    if (lane == 0 && wave < FIN_STAMP_WAVES) {
+      g_fin_stamp[wave][8] = prof[0]; g_fin_stamp[wave][9] = prof[1]; g_fin_stamp[wave][10] = prof[2];
+    }
+#else
     fe_invert_var(inv, t);
+#endif
   } else {
     fe_invert_gcd(inv, t);  // divsteps: ~19k instructions instead of ~44k on the serial chain
   }
 #endif
+  FIN_STAMP(3);
   static_for<LV>([&](auto kc) {
     constexpr int k = LV - 1 - decltype(kc)::value;
     fe_mul(inv, inv, tq[k]);  // 1 / (product of this lane's 2^k group)
   });
+  FIN_STAMP(4);
   fin_unroll<FM>::down([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
@@ -98,14 +147,20 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
     if constexpr (m > 0) {
       fe_mul(zi, inv, pre[m - 1]);   // 1 / Z_m
       fe z;
-      if (live) load_fe(z, Zb, N, ii); else fe_one(z);
+      if constexpr (PRE) z = zs[m];
+      else if (live) load_fe(z, Zb, N, ii); else fe_one(z);
       fe_mul(inv, inv, z);           // 1 / (Z_0 ... Z_{m-1})
     } else {
       zi = inv;
     }
     fe X, Y, x, y;
-    load_fe(X, Xb, N, ii);
-    load_fe(Y, Yb, N, ii);
+    if constexpr (PRE) {
+      X = xs[m];
+      Y = ys[m];
+    } else {
+      load_fe(X, Xb, N, ii);
+      load_fe(Y, Yb, N, ii);
+    }
     fe_mul(x, X, zi);
     fe_mul(y, Y, zi);
     uint32_t xw[8], yw[8], r[8], ry[8];
@@ -120,6 +175,10 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
     const uint64_t vote = __ballot(ok);
     if (lane == 0 && live) bitmap[(wave * FM + m)] = vote;
   });
+  FIN_STAMP(5);
+#if PBFT_FIN_STAMPS
+  if (lane == 0 && wave < FIN_STAMP_WAVES) g_fin_stamp[wave][7] = __builtin_amdgcn_s_memrealtime();
+#endif
 }
 
 

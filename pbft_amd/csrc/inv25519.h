@@ -213,7 +213,10 @@ __host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t
 }
 
 // out = z^-1 (0 -> 0) for a wave-uniform z (see above); z as for fe_invert_gcd
-__host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z) {
+// (The scalar unit does not help here, measured r03 with PBFT_FIN_STAMPS: run on the SALU, the divsteps take
+// half their VALU time but the 30-bit-limb updates, which need 64-bit products, take as long as the divsteps
+// saved -- whole-inversion or hybrid alike, ~78k shader cycles either way; profiles/r03/finish_stamps.txt.)
+__host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z, uint64_t* prof = nullptr) {
   uint32_t w[8];
   fe_to_words(w, z);
   s30 f, g, d, e;
@@ -228,16 +231,36 @@ __host__ __device__ __forceinline__ void fe_invert_var(fe& out, const fe& z) {
     e.v[i] = i == 0 ? 1 : 0;
   }
   int32_t eta = -1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint64_t t_ds = 0, t_up = 0, n_it = 0;
+#endif
   for (int it = 0; it < 25; ++it) {
     int32_t nz = 0;
 #pragma unroll
     for (int i = 0; i < 9; ++i) nz |= g.v[i];
     if (nz == 0) break;
     int32_t t[4];
+#if defined(__HIP_DEVICE_COMPILE__)
+    uint64_t c0 = 0, c1 = 0;
+    if (prof) c0 = __builtin_amdgcn_s_memtime();
+#endif
     eta = divsteps30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (prof) { asm volatile("" :: "v"(t[0]), "v"(t[3])); c1 = __builtin_amdgcn_s_memtime(); t_ds += c1 - c0; }
+#endif
     inv_update_de(d, e, t);
     inv_update_fg(f, g, t);
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (prof) {
+      asm volatile("" :: "v"(f.v[0]), "v"(g.v[0]), "v"(d.v[8]), "v"(e.v[8]));
+      t_up += __builtin_amdgcn_s_memtime() - c1;
+      ++n_it;
+    }
+#endif
   }
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (prof) { prof[0] = t_ds; prof[1] = t_up; prof[2] = n_it; }
+#endif
   inv_normalize(d, f.v[8] >> 31);  // f = +-1
 #pragma unroll
   for (int j = 0; j < 8; ++j) {

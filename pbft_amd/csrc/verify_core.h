@@ -122,6 +122,9 @@ FE_FN uint32_t lane_mask(bool c) {
 #ifndef PBFT_MADD_V2
 #define PBFT_MADD_V2 1
 #endif
+#ifndef PBFT_CHAIN_MIN_N
+#define PBFT_CHAIN_MIN_N (1u << 19)  // comb_kernel uses the single-chain multiplies (CHAIN) from this batch size
+#endif
 // 2p - k per limb for canonical k (the conditional negation of the entry's d*x*y)
 FE_FN void fe_cneg_canon(fe& out, const fe& k, uint32_t m) {
   fe nk;
@@ -129,7 +132,7 @@ FE_FN void fe_cneg_canon(fe& out, const fe& k, uint32_t m) {
 #pragma unroll
   for (int i = 0; i < 10; ++i) out.v[i] = (k.v[i] & ~m) | (nk.v[i] & m);  // one v_bitop3 per limb
 }
-template <bool WITH_T = true>
+template <bool WITH_T = true, bool CHAIN = false>
 FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& k, bool neg) {
 #if PBFT_MADD_V2
   // r02 form below, re-ordered for fewer VALU instructions per step (profiles/r03_step_hist.txt):
@@ -142,19 +145,46 @@ FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& 
   fe a, b, c, t, kk;
   fe_cneg_canon(kk, k, lane_mask(neg));
   fe_sub(t, p.Y, p.X);
-  fe_mul(a, t, qa);
-  fe_add(t, p.Y, p.X);
-  fe_mul(b, t, qb);
-  fe_mul(c, p.T, kk);
+  if constexpr (CHAIN) {
+    // The 3 + 4 products as interleaved single-chain multiplies (fe_mul_chain: no 64-bit carry adds).  Fewer
+    // VALU instructions (-55 per step) but longer dependency chains: faster when many blocks per CU overlap
+    // (2^20: -1.8 %), slower on a single wave of blocks (131k: +6 %), so launch_comb_plan picks it by size
+    // (profiles/r03/ab_chain_mul.txt).
+    fe t2;
+    fe_add(t2, p.Y, p.X);
+    {
+      fe* const ho[3] = {&a, &b, &c};
+      const fe* const fo[3] = {&t, &t2, &p.T};
+      const fe* const go[3] = {&qa, &qb, &kk};
+      fe_mul_chain<3>(ho, fo, go);
+    }
+  } else {
+    fe_mul(a, t, qa);
+    fe_add(t, p.Y, p.X);
+    fe_mul(b, t, qb);
+    fe_mul(c, p.T, kk);
+  }
   fe e, f, g, h;
   fe_sub(e, b, a);
   fe_sub(f, p.Z, c);
   fe_add(g, p.Z, c);
   fe_add(h, b, a);
-  fe_mul(r.X, f, e);
-  fe_mul(r.Y, h, g);
-  fe_mul(r.Z, f, g);
-  if constexpr (WITH_T) fe_mul(r.T, h, e);
+  if constexpr (CHAIN && WITH_T) {
+    fe* const ho[4] = {&r.X, &r.Y, &r.Z, &r.T};
+    const fe* const fo[4] = {&f, &h, &f, &h};
+    const fe* const go[4] = {&e, &g, &g, &e};
+    fe_mul_chain<4>(ho, fo, go);
+  } else if constexpr (CHAIN) {
+    fe* const ho[3] = {&r.X, &r.Y, &r.Z};
+    const fe* const fo[3] = {&f, &h, &f};
+    const fe* const go[3] = {&e, &g, &g};
+    fe_mul_chain<3>(ho, fo, go);
+  } else {
+    fe_mul(r.X, f, e);
+    fe_mul(r.Y, h, g);
+    fe_mul(r.Z, f, g);
+    if constexpr (WITH_T) fe_mul(r.T, h, e);
+  }
 #else
   fe a, b, c, t;
   const uint32_t m = lane_mask(neg);

@@ -221,7 +221,7 @@ __device__ __forceinline__ void sha512_k(uint32_t h[16], const uint32_t r[8], co
   }
 }
 
-template <int LEN, class PLA>
+template <int LEN, class PLA, bool CHAIN = false>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
@@ -322,7 +322,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #pragma unroll
     for (int t = 0; t < 10; ++t) { P.X.v[t] ^= qa.v[t]; P.Y.v[t] ^= qb.v[t]; P.Z.v[t] += k.v[t] + neg; }
 #else
-    ge_madd_ab<true>(P, P, qa, qb, k, neg);
+    ge_madd_ab<true, CHAIN>(P, P, qa, qb, k, neg);
 #endif
 #if PBFT_LAUNDER
     // Keep the loop-carried limbs opaque 32-bit values: otherwise LLVM carries
@@ -339,7 +339,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     fe qa, qb, k;
     const bool neg = (uint32_t)(sgn >> (ST::N - 1)) & 1u;
     lds_entry_signed(rd0, neg, qa, qb, k);
-    ge_madd_ab<false>(P, P, qa, qb, k, neg);
+    ge_madd_ab<false, CHAIN>(P, P, qa, qb, k, neg);
   }
   if (live) {
 #pragma unroll
@@ -679,7 +679,11 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
   } else {
     const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
     const size_t lds = (BLOCK / 64) * COMB_LDS_PER_WAVE;
-    if (a.msg_len == PBFT_ENVELOPE_LEN)
+    if (a.msg_len == PBFT_ENVELOPE_LEN && N >= PBFT_CHAIN_MIN_N)
+      hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st,
+                         a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
+    else if (a.msg_len == PBFT_ENVELOPE_LEN)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
                          a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
                          a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);

@@ -110,6 +110,23 @@ def main():
         t = np.array(res[p])
         print(f"N={n:8d} {os.path.basename(p):32s} median {np.median(t):.4f} ms  min {t.min():.4f}  "
               f"-> {n / np.median(t) * 1e3 / 1e6:.1f} M verifies/s   [{lib.pbft_build_info().decode()}]", flush=True)
+        if hasattr(lib, "pbft_debug_fin_stamps"):
+            # finish-kernel phase stamps of the last launch (PBFT_FIN_STAMPS build): per wave, shader cycles
+            waves = 4096
+            buf = np.zeros((waves, 12), np.uint64)
+            lib.pbft_debug_fin_stamps(ctypes.c_void_p(buf.ctypes.data), ctypes.c_uint32(waves))
+            live = buf[(buf[:, 5] > buf[:, 0]) & (buf[:, 0] > 0)]
+            if len(live):
+                d = np.diff(live[:, :6].astype(np.int64), axis=1)
+                names = ["prefix", "tree-up", "inversion", "tree-down", "back+compare"]
+                med = ", ".join(f"{nm} {int(np.median(d[:, k]))}" for k, nm in enumerate(names))
+                span = (live[:, 7].max() - live[:, 6].min()) / 100.0  # s_memrealtime: 100 MHz
+                first = (live[:, 6].max() - live[:, 6].min()) / 100.0
+                print(f"    finish stamps ({len(live)} waves, median shader cycles): {med}; "
+                      f"total {int(np.median(live[:, 5].astype(np.int64) - live[:, 0].astype(np.int64)))}; "
+                      f"wall span {span:.1f} us, wave starts spread {first:.1f} us; inversion: divsteps "
+                      f"{int(np.median(live[:, 8]))}, updates {int(np.median(live[:, 9]))} cycles over "
+                      f"{int(np.median(live[:, 10]))} batches", flush=True)
 
 
 if __name__ == "__main__":

@@ -79,6 +79,11 @@ def main():
             print(f"  class {kk:10s} {v}")
         for o, v in c.most_common(60):
             print(f"  {o:28s} {v}")
+        nvalu = lambda a, b: sum(1 for o in ops(body[a:b]) if o.startswith("v_"))
+        print(f"VALU before the largest loop: {nvalu(0, lo)}, after it: {nvalu(hi + 1, len(body))}")
+        print("all loops (start line, end line, VALU in body):")
+        for a, b in sorted(set(loops)):
+            print(f"  {a:6d} {b:6d} {nvalu(a, b + 1):6d}")
 
 
 if __name__ == "__main__":

@@ -138,6 +138,58 @@ __global__ void k_bitop3(uint64_t* out, stamp* st, uint32_t seed) {
   BODY_END(s)
 }
 
+
+// generic 32-bit three-operand forms: acc = op(acc, a, b) with distinct VGPRs
+#define K32(NAME, ASM)                                                                               \
+  __global__ void NAME(uint64_t* out, stamp* st, uint32_t seed) {                                    \
+    uint32_t a = threadIdx.x * 2654435761u + seed, b = a * 3u + 7u, acc[CH];                         \
+    for (int c = 0; c < CH; ++c) acc[c] = a + c;                                                     \
+    BODY_BEGIN                                                                                       \
+    for (int i = 0; i < ITERS; ++i)                                                                  \
+      _Pragma("unroll") for (int c = 0; c < CH; ++c) asm volatile(ASM : "+v"(acc[c]) : "v"(a), "v"(b) : "vcc", "s0", "s1"); \
+    uint32_t s = 0;                                                                                  \
+    for (int c = 0; c < CH; ++c) s ^= acc[c];                                                        \
+    BODY_END(s)                                                                                      \
+  }
+K32(k_alignbit, "v_alignbit_b32 %0, %1, %0, 26")
+K32(k_bfi, "v_bfi_b32 %0, %1, %0, %2")
+K32(k_and, "v_and_b32_e32 %0, %1, %0")
+K32(k_sub, "v_sub_u32_e32 %0, %1, %0")
+K32(k_add3, "v_add3_u32 %0, %1, %0, %2")
+K32(k_mul24, "v_mul_u32_u24_e32 %0, %1, %0")
+K32(k_mad24, "v_mad_u32_u24 %0, %1, %0, %2")
+K32(k_lshl_or, "v_lshl_or_b32 %0, %1, 6, %0")
+K32(k_and_or, "v_and_or_b32 %0, %1, %2, %0")
+K32(k_cndmask64, "v_cmp_lt_u32_e64 s[0:1], %1, %2\n v_cndmask_b32_e64 %0, %0, %1, s[0:1]")
+
+// 64-bit shift: acc = acc >> 26 | a (kept live), the carry step's shift
+__global__ void k_lshr64(uint64_t* out, stamp* st, uint32_t seed) {
+  uint64_t a = threadIdx.x * 2654435761ull + seed, acc[CH];
+  for (int c = 0; c < CH; ++c) acc[c] = a + c;
+  BODY_BEGIN
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) asm volatile("v_lshrrev_b64 %0, 1, %0" : "+v"(acc[c]));
+  uint64_t s = a;
+  for (int c = 0; c < CH; ++c) s ^= acc[c];
+  BODY_END(s)
+}
+
+// 64-bit add as a VOP2 pair through VCC (v_add_co_u32 + v_addc_co_u32): counts 2 instructions per op
+__global__ void k_addc_pair(uint64_t* out, stamp* st, uint32_t seed) {
+  uint32_t a = threadIdx.x * 2654435761u + seed, lo[CH], hi[CH];
+  for (int c = 0; c < CH; ++c) { lo[c] = a + c; hi[c] = c; }
+  BODY_BEGIN
+  for (int i = 0; i < ITERS; ++i)
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      asm volatile("v_add_co_u32_e32 %0, vcc, %2, %0\n v_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+                   : "+v"(lo[c]), "+v"(hi[c]) : "v"(a) : "vcc");
+  uint32_t s = 0;
+  for (int c = 0; c < CH; ++c) s ^= lo[c] ^ hi[c];
+  BODY_END(s)
+}
+
 typedef void (*kfn)(uint64_t*, stamp*, uint32_t);
 
 int main() {
@@ -154,7 +206,12 @@ int main() {
     int lanes_per_op;  // results per lane per instruction
   } ks[] = {{"v_fma_f32 same-src", k_fma_same, 1}, {"v_fma_f32", k_fma, 1}, {"v_pk_fma_f32", k_pk_fma, 2},
             {"v_mad_u64_u32", k_mad64, 1},     {"v_add_u32_e32", k_add, 1}, {"v_lshl_add_u64", k_lshl_add64, 1},
-            {"v_mul_lo_u32", k_mullo, 1},      {"v_bitop3_b32", k_bitop3, 1}};
+            {"v_mul_lo_u32", k_mullo, 1},      {"v_bitop3_b32", k_bitop3, 1},
+            {"v_alignbit_b32", k_alignbit, 1}, {"v_bfi_b32", k_bfi, 1},   {"v_and_b32_e32", k_and, 1},
+            {"v_sub_u32_e32", k_sub, 1},       {"v_add3_u32", k_add3, 1}, {"v_mul_u32_u24_e32", k_mul24, 1},
+            {"v_mad_u32_u24", k_mad24, 1},     {"v_lshl_or_b32", k_lshl_or, 1}, {"v_and_or_b32", k_and_or, 1},
+            {"v_cmp+v_cndmask_e64 (2)", k_cndmask64, 1}, {"v_lshrrev_b64", k_lshr64, 1},
+            {"v_add_co+v_addc_co (2)", k_addc_pair, 1}};
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """profiles/<run>/derived.json from rocprofv3 --pmc pass CSVs of the verify launch pair (read by bench.py).
 
-usage: python tools/pmc_derive.py PMC_DIR PB PA [n_sigs]   (comb positions of the base-point / key plans)
+usage: python tools/pmc_derive.py PMC_DIR PB PA [n_sigs [KERNEL_STATS_CSV]]   (comb positions of the plans)
+
+With the rocprofv3 --kernel-trace --stats CSV of the same command, each kernel also gets its average duration and
+the shader clock it ran at: GRBM_GUI_ACTIVE (GPU-busy cycles of the dispatch) / the average duration.
 """
 import collections
 import csv
@@ -12,6 +15,15 @@ import sys
 
 d, pb, pa = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 n = int(sys.argv[4]) if len(sys.argv) > 4 else 1 << 20
+stats = {}
+if len(sys.argv) > 5:
+    for r in csv.DictReader(open(sys.argv[5])):
+        stats[r["Name"]] = float(r["AverageNs"])
+
+
+def avg_ns(name):
+    hits = [v for k, v in stats.items() if name in k and "entry" not in k and "base" not in k]
+    return max(hits) if hits else None
 
 
 def agg(name):
@@ -33,6 +45,13 @@ for k in ("comb_kernel", "finish_kernel"):
               "valu_insts_per_lane": m["SQ_INSTS_VALU"] / m["SQ_WAVES"], "waves": m["SQ_WAVES"],
               # wave-instructions x 64 lanes / signatures: the VALU instructions one signature costs
               "valu_insts_per_sig": m["SQ_INSTS_VALU"] * 64 / n}
+    ns = avg_ns(k)
+    if ns and "GRBM_GUI_ACTIVE" in m:
+        out[k]["avg_ns"] = ns
+        out[k]["grbm_gui_active"] = m["GRBM_GUI_ACTIVE"]
+        out[k]["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / ns
+        # VALU wave-instructions per SIMD per cycle (1024 SIMDs) at that clock
+        out[k]["valu_issue_per_simd_cycle"] = m["SQ_INSTS_VALU"] / 1024 / m["GRBM_GUI_ACTIVE"]
     tot += fb + wbytes
 out["traffic_bytes_per_launch"] = tot
 out["valu_insts_per_sig_total"] = sum(out[k]["valu_insts_per_sig"] for k in ("comb_kernel", "finish_kernel"))
