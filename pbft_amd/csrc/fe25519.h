@@ -201,6 +201,9 @@ FE_FN uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc) {
   return acc;
 }
 
+#ifndef PBFT_CHAIN_FORM
+#define PBFT_CHAIN_FORM 0
+#endif
 // N independent products h[m] = f[m] g[m], each computed as ONE dependent chain over the columns: column k's
 // mads accumulate on top of column k-1's carry, so a carry costs one 64-bit shift and one mask and no 64-bit
 // add (fe_reduce_wide's single-chain arithmetic, PBFT_REDUCE_1CHAIN: identical outputs and bounds).  The N
@@ -229,8 +232,24 @@ FE_FN void fe_mul_chain(fe* const h[], const fe* const f[], const fe* const g[])
         fi[m] = ((i & 1) && (j & 1)) ? fx[m][i] : f[m]->v[i];
         gj[m] = j >= 0 ? g[m]->v[j] : g19[m][j + 10];
       }
+#if PBFT_CHAIN_FORM == 0
 #pragma unroll
       for (int m = 0; m < N; ++m) acc[m] = (k == 0 && i == 0) ? MUL64(fi[m], gj[m]) : mad_acc(fi[m], gj[m], acc[m]);
+#else
+      // launder only the carry that starts a column (its first mad takes it as the addend); the column's other
+      // mads chain on that one
+#pragma unroll
+      for (int m = 0; m < N; ++m) {
+        if (k == 0 && i == 0) acc[m] = MUL64(fi[m], gj[m]);
+        else if (i == 0) acc[m] = mad_acc(fi[m], gj[m], acc[m]);
+        else acc[m] += MUL64(fi[m], gj[m]);
+      }
+#if PBFT_CHAIN_FORM == 2 && defined(__HIP_DEVICE_COMPILE__)
+      // one mad of each chain in turn: no two dependent mads back to back
+#pragma unroll
+      for (int m = 0; m < N; ++m) __builtin_amdgcn_sched_group_barrier(0x2, 1, 0);
+#endif
+#endif
     }
 #pragma unroll
     for (int m = 0; m < N; ++m) {

@@ -49,14 +49,16 @@ for k in ("comb_kernel", "finish_kernel"):
     if ns and "GRBM_GUI_ACTIVE" in m:
         out[k]["avg_ns"] = ns
         out[k]["grbm_gui_active"] = m["GRBM_GUI_ACTIVE"]
-        out[k]["clock_ghz"] = m["GRBM_GUI_ACTIVE"] / ns
+        # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
+        cyc = m["GRBM_GUI_ACTIVE"] / 8
+        out[k]["clock_ghz"] = cyc / ns
         # VALU wave-instructions per SIMD per cycle (1024 SIMDs) at that clock
-        out[k]["valu_issue_per_simd_cycle"] = m["SQ_INSTS_VALU"] / 1024 / m["GRBM_GUI_ACTIVE"]
+        out[k]["valu_issue_per_simd_cycle"] = m["SQ_INSTS_VALU"] / 1024 / cyc
     tot += fb + wbytes
 out["traffic_bytes_per_launch"] = tot
 out["valu_insts_per_sig_total"] = sum(out[k]["valu_insts_per_sig"] for k in ("comb_kernel", "finish_kernel"))
 out["note"] = ("rocprofv3 --pmc passes (one counter group per run, no tracing) of `python3 bench.py --steps 5 "
-               "--warmup 1 --no-cpu --no-extras` (tools/gpu_pmc_cur.sh); FETCH_SIZE (KB) doubled per the "
+               "--warmup 1 --no-cpu --no-extras` (tools/gpu_prof_r03.sh); FETCH_SIZE (KB) doubled per the "
                "gfx950 correction of MI355X_MICROARCH.md's HBM section; WRITE_SIZE taken as is")
 json.dump(out, open(os.path.join(d, "derived.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
