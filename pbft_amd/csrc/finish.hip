@@ -41,12 +41,13 @@ struct fin_unroll<0> {
 // multiplications and 1 / (2^LV FM) of an inversion, instead of 3 (FM - 1) + 2
 // and 1 / FM.  The down-sweep peels the partners off again:
 // 1 / t_k = (1 / t_{k+1}) q_k, since t_{k+1} = t_k q_k.
-#ifndef PBFT_FIN_LV_WAVES
-#define PBFT_FIN_LV_WAVES 1  // waves per SIMD the product-tree finish is compiled for (1: no scratch spills)
-#endif
 #ifndef PBFT_FIN_PREFETCH
 #define PBFT_FIN_PREFETCH 1
 #endif
+#ifndef PBFT_FIN_TAB
+#define PBFT_FIN_TAB 1  // LV = 6: table-driven divsteps (inv25519.h fe_invert_tab) instead of divsteps30_var
+#endif
+#define FIN_USE_TAB (PBFT_FIN_TAB && !PBFT_ABL_NOINV && !PBFT_FIN_EXP)
 #ifndef PBFT_FIN_STAMPS
 #define PBFT_FIN_STAMPS 0  // 1: timing build -- every wave stamps s_memtime at its phase boundaries
 #endif
@@ -64,8 +65,9 @@ extern "C" int pbft_debug_fin_stamps(uint64_t* out, uint32_t waves) {
 #define FIN_STAMP(k)
 #endif
 
-template <int FM, int LV>
-__global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU : PBFT_FIN_LV_WAVES) finish_kernel(const uint8_t* __restrict__ R,
+// W: waves per SIMD the kernel is compiled for (register budget 512 / W); the prefetch of X, Y, Z needs W = 1
+template <int FM, int LV, int W>
+__global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restrict__ R,
                                                        uint32_t rs_stride,
                                                        const uint32_t* __restrict__ xyz,
                                                        const uint8_t* __restrict__ flags, uint64_t N,
@@ -73,6 +75,18 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
   const int lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const uint64_t base = wave * FM * 64 + lane;
+#if FIN_USE_TAB
+  // LV = 6: the divstep table (inv25519.h) goes to LDS; every wave of the block copies its share and meets the
+  // one barrier before the inversion (waves past N included, so the barrier count always matches)
+  __shared__ uint64_t ds_tab[LV == 6 ? DS_TAB_ENTRIES : 1];
+  if constexpr (LV == 6) {
+    const uint4* src = (const uint4*)g_ds_tab.e;
+    uint4* dst = (uint4*)ds_tab;
+#pragma unroll
+    for (int k = 0; k < DS_TAB_ENTRIES / 2 / BLOCK; ++k) dst[k * BLOCK + threadIdx.x] = src[k * BLOCK + threadIdx.x];
+    if (wave * FM * 64 >= N) { __syncthreads(); return; }
+  }
+#endif
   if (wave * FM * 64 >= N) return;
   FIN_STAMP(0);
 #if PBFT_FIN_STAMPS
@@ -85,7 +99,7 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
   fe pre[FM];
   // PRE: small FM keeps every Z and issues the X, Y loads before the inversion, so the back-substitution
   // does not wait on memory (FM <= 4: ~100 more VGPRs, within the 2-waves-per-SIMD budget)
-  constexpr bool PRE = PBFT_FIN_PREFETCH && FM <= 4;
+  constexpr bool PRE = PBFT_FIN_PREFETCH && FM <= 4 && W == 1;
   fe zs[PRE ? FM : 1], xs[PRE ? FM : 1], ys[PRE ? FM : 1];
   fin_unroll<FM>::up([&](auto mc) {
     constexpr int m = decltype(mc)::value;
@@ -119,7 +133,14 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
 #else
   if constexpr (LV == 6) {
     // every lane holds the wave's product: the variable-time divsteps never diverge (inv25519.h)
-#if PBFT_FIN_STAMPS
+#if FIN_USE_TAB
+    __syncthreads();  // the block's divstep table is in LDS
+    #if PBFT_INV_WAVE
+    fe_invert_wave(inv, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
+#else
+    fe_invert_tab(inv, t, ds_tab);
+#endif
+#elif PBFT_FIN_STAMPS
     uint64_t prof[3];
     fe_invert_var(inv, t, prof);
     if (lane == 0 && wave < FIN_STAMP_WAVES) {
@@ -182,24 +203,28 @@ __global__ void __launch_bounds__(BLOCK, (FM >= 8 || LV == 0) ? FIN_WAVES_PER_EU
 }
 
 
-hipError_t launch_finish(int fm, int lv, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
+hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
                          const uint8_t* flags, uint64_t N, uint64_t* bitmap, hipStream_t st) {
-#define PBFT_LAUNCH_FIN(M_, LV_)                                                                               \
-  hipLaunchKernelGGL((finish_kernel<M_, LV_>),                                                              \
+#define PBFT_LAUNCH_FIN(M_, LV_, W_)                                                                           \
+  hipLaunchKernelGGL((finish_kernel<M_, LV_, W_>),                                                          \
                      dim3((unsigned)((((N + 64 * M_ - 1) / (64 * M_)) * 64 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, \
                      st, R, rs_stride, xyz, flags, N, bitmap)
   if (lv == 0) {
-    if (fm == 16) PBFT_LAUNCH_FIN(16, 0);
-    else if (fm == 8) PBFT_LAUNCH_FIN(8, 0);
-    else if (fm == 4) PBFT_LAUNCH_FIN(4, 0);
-    else if (fm == 2) PBFT_LAUNCH_FIN(2, 0);
-    else PBFT_LAUNCH_FIN(1, 0);
+    if (fm == 16) PBFT_LAUNCH_FIN(16, 0, FIN_WAVES_PER_EU);
+    else if (fm == 8) PBFT_LAUNCH_FIN(8, 0, FIN_WAVES_PER_EU);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4, 0, FIN_WAVES_PER_EU);
+    else if (fm == 2) PBFT_LAUNCH_FIN(2, 0, FIN_WAVES_PER_EU);
+    else PBFT_LAUNCH_FIN(1, 0, FIN_WAVES_PER_EU);
+  } else if (w >= 2) {  // product tree at two waves per SIMD (no prefetch): large rounds
+    if (fm >= 8) PBFT_LAUNCH_FIN(8, 6, 2);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4, 6, 2);
+    else PBFT_LAUNCH_FIN(2, 6, 2);
   } else {
-    if (fm == 16) PBFT_LAUNCH_FIN(16, 6);
-    else if (fm == 8) PBFT_LAUNCH_FIN(8, 6);
-    else if (fm == 4) PBFT_LAUNCH_FIN(4, 6);
-    else if (fm == 2) PBFT_LAUNCH_FIN(2, 6);
-    else PBFT_LAUNCH_FIN(1, 6);
+    if (fm == 16) PBFT_LAUNCH_FIN(16, 6, 1);
+    else if (fm == 8) PBFT_LAUNCH_FIN(8, 6, 1);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4, 6, 1);
+    else if (fm == 2) PBFT_LAUNCH_FIN(2, 6, 1);
+    else PBFT_LAUNCH_FIN(1, 6, 1);
   }
 #undef PBFT_LAUNCH_FIN
   return hipGetLastError();

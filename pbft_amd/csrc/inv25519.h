@@ -212,6 +212,234 @@ __host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t
   return eta;
 }
 
+// ---- table-driven divsteps, for a wave-uniform input ------------------------------
+// The half-delta divsteps of divsteps30, DS_TN = 5 at a time: the 5 steps' decisions depend only on zeta's
+// class (clamp(zeta, -5, 4): from zeta >= 4 no swap can occur within 5 steps, and every zeta <= -5 takes the
+// same decisions), f mod 32 (odd) and g mod 32, so one lookup gives their 2x2 transition matrix S
+// (2^5 [f'; g'] = S [f; g], entries in [-32, 32]) and the affine map zeta' = +-zeta + c.  A batch of 30 is six
+// lookups, T <- S T each, and ends with the same t and zeta as divsteps30 (host-tested step for step), so
+// inv_update_de / inv_update_fg apply unchanged.  With the 5,120-entry table in LDS (40 KB) a lookup is one
+// ds_read_b64 plus ~8 dependent VALU operations on the critical path instead of ~5 x 18 (constant-time) or
+// the ctz / Newton-inverse chain of divsteps30_var.
+#define DS_TN 5
+#ifndef PBFT_INV_WAVE
+#define PBFT_INV_WAVE 1  // wave-uniform inversions: fe_invert_wave (limbs across lanes) instead of fe_invert_tab
+#endif
+#define DS_TZ (2 * DS_TN)
+#define DS_TAB_ENTRIES (DS_TZ * 16 * 32)
+
+// entry idx = ((zc + 5) * 16 + (f >> 1) % 16) * 32 + g % 32: u, v, q, r as int8 in bits 0..31, c (int8) in
+// bits 32..39, bit 40 = the map negates zeta
+__host__ __device__ constexpr uint64_t ds_tab_entry(uint32_t idx) {
+  int32_t zeta = (int32_t)(idx / 512) - DS_TN;
+  int32_t f = (int32_t)((((idx / 32) % 16) << 1) | 1), g = (int32_t)(idx % 32);
+  int32_t u = 1, v = 0, q = 0, r = 1, s = 1, c = 0;
+  for (int i = 0; i < DS_TN; ++i) {
+    const bool c1 = zeta < 0, c2 = (g & 1) != 0, c3 = c1 && c2;
+    if (c2) {
+      g += c1 ? -f : f;
+      q += c1 ? -u : u;
+      r += c1 ? -v : v;
+    }
+    if (c3) { zeta = -zeta - 2; s = -s; c = -c - 2; f += g; u += q; v += r; }
+    else { zeta -= 1; c -= 1; }
+    u *= 2; v *= 2;
+    g /= 2;  // exact: g is even here
+  }
+  return (uint64_t)(uint8_t)(int8_t)u | (uint64_t)(uint8_t)(int8_t)v << 8 | (uint64_t)(uint8_t)(int8_t)q << 16 |
+         (uint64_t)(uint8_t)(int8_t)r << 24 | (uint64_t)(uint8_t)(int8_t)c << 32 | (uint64_t)(s < 0 ? 1 : 0) << 40;
+}
+struct ds_table {
+  uint64_t e[DS_TAB_ENTRIES];
+  constexpr ds_table() : e() {
+    for (uint32_t i = 0; i < DS_TAB_ENTRIES; ++i) e[i] = ds_tab_entry(i);
+  }
+};
+
+// 30 half-delta divsteps by 6 lookups; same return value and t as divsteps30(zeta, f, g, t)
+__host__ __device__ __forceinline__ int32_t divsteps30_tab(int32_t zeta, uint32_t f, uint32_t g, int32_t t[4],
+                                                           const uint64_t* tab) {
+  int32_t u = 1, v = 0, q = 0, r = 1;
+#pragma unroll
+  for (int k = 0; k < 30 / DS_TN; ++k) {
+    const int32_t zc = zeta < -DS_TN ? -DS_TN : (zeta > DS_TN - 1 ? DS_TN - 1 : zeta);
+    const uint32_t idx = (uint32_t)(zc + DS_TN) * 512u + ((f >> 1) & 15u) * 32u + (g & 31u);
+    const uint64_t e = tab[idx];
+    const int32_t su = (int8_t)e, sv = (int8_t)(e >> 8), sq = (int8_t)(e >> 16), sr = (int8_t)(e >> 24);
+    const int32_t c = (int8_t)(e >> 32);
+    zeta = ((e >> 40) & 1u ? -zeta : zeta) + c;
+    const uint32_t f2 = (uint32_t)su * f + (uint32_t)sv * g;  // low 32 bits of 2^5 f' (exactly divisible)
+    const uint32_t g2 = (uint32_t)sq * f + (uint32_t)sr * g;
+    f = f2 >> DS_TN;  // low 27, 22, ... bits exact: enough for the remaining lookups
+    g = g2 >> DS_TN;
+    const int32_t nu = su * u + sv * q, nv = su * v + sv * r;
+    const int32_t nq = sq * u + sr * q, nr = sq * v + sr * r;
+    u = nu; v = nv; q = nq; r = nr;
+  }
+  t[0] = u; t[1] = v; t[2] = q; t[3] = r;
+  return zeta;
+}
+
+// out = z^-1 (0 -> 0) for a wave-uniform z, table in `tab` (LDS on the device); z as for fe_invert_gcd.
+// Half-delta divsteps as fe_invert_gcd, batches of 30 until g = 0 (at most 20: the 590-divstep bound).
+__host__ __device__ __forceinline__ void fe_invert_tab(fe& out, const fe& z, const uint64_t* tab) {
+  uint32_t w[8];
+  fe_to_words(w, z);
+  s30 f, g, d, e;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int b = 30 * i, wi = b >> 5, sh = b & 31;
+    uint64_t x = w[wi] >> sh;
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << (32 - sh);
+    g.v[i] = (int32_t)((uint32_t)x & INV_M30);
+    f.v[i] = p30_limb(i);
+    d.v[i] = 0;
+    e.v[i] = i == 0 ? 1 : 0;
+  }
+  int32_t zeta = -1;
+  for (int it = 0; it < 20; ++it) {
+    int32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < 9; ++i) nz |= g.v[i];
+    if (nz == 0) break;
+    int32_t t[4];
+    zeta = divsteps30_tab(zeta, (uint32_t)f.v[0], (uint32_t)g.v[0], t, tab);
+    inv_update_de(d, e, t);
+    inv_update_fg(f, g, t);
+  }
+  inv_normalize(d, f.v[8] >> 31);  // f = +-1
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int b = 32 * j, li = b / 30, sh = b % 30;
+    uint64_t x = (uint64_t)(uint32_t)d.v[li] >> sh;
+    x |= (uint64_t)(uint32_t)d.v[li + 1] << (30 - sh);
+    if (li + 2 < 9 && 60 - sh < 32) x |= (uint64_t)(uint32_t)d.v[li + 2] << (60 - sh);
+    w[j] = (uint32_t)x;
+  }
+  fe_from_words(out, w);
+}
+
+// ---- wave-uniform inversion with the limb updates spread over lanes --------------------------------
+// With table lookups the divsteps are short, and the serial 9-limb updates of f, g, d, e (~200 VALU per batch
+// on one wave) become the chain (profiles/r03/finish_stamps_tab.txt).  fe_invert_wave keeps the same
+// divsteps (divsteps30_tab on limb 0 of f and g) but holds limb j of every vector in lane j of each 16-lane
+// row (the four rows compute the same), so an update is a few lane-parallel instructions plus DPP carries:
+//  * f, g (30-bit limbs, exact integers): n_j = (u f + v g)_j >> 30 + lo30((u f + v g)_{j+1}) is the exact
+//    division by 2^30 (the limb-0 remainder is 0); a second carry round keeps limbs in [-1, 2^30] (the top
+//    limb signed).  Limb 0 stays exact mod 2^30 -- all the divsteps read.
+//  * d, e are replaced by the second column (D, E) of the accumulated transition matrix, mod p, in radix
+//    2^25.5 with signed limbs: (D, E) <- t (D, E) per batch, two carry rounds (the top carry folds back x19).
+//    After k batches f = (A00 p + D x) / 2^30k = +-1, so x^-1 = +-D 2^-30k mod p (DS_INV2K: the constants).
+//    No Montgomery correction per batch, no sign tests.
+// The same divstep sequence as fe_invert_tab, so the result is the same inverse (it is unique).
+static constexpr uint32_t DS_INV2K[21][10] = {  // 2^(-30 k) mod p, k = 0 .. 20, radix 2^25.5 limbs
+    {0x0000001u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u, 0x0000000u},
+    {0x3fffff4u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x35fffffu, 0x1435e50u},
+    {0x3fffff8u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x01affffu, 0x39435e5u, 0x0d79435u},
+    {0x3ffffeeu, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x0a1afffu, 0x0bca1afu, 0x10d7943u, 0x1e50d79u},
+    {0x3fffff4u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x3ffffffu, 0x1e50d7fu, 0x06bca1au, 0x1286bcau, 0x35e50d7u, 0x1435e50u},
+    {0x3fffff8u, 0x1ffffffu, 0x3ffffffu, 0x1ffffffu, 0x35e50d7u, 0x1435e50u, 0x2f286bcu, 0x01af286u, 0x39435e5u, 0x0d79435u},
+    {0x3ffffeeu, 0x1ffffffu, 0x2ffffffu, 0x01af286u, 0x39435e5u, 0x0d79435u, 0x0a1af28u, 0x0bca1afu, 0x10d7943u, 0x1e50d79u},
+    {0x3fffff4u, 0x0d7ffffu, 0x0a1af28u, 0x0bca1afu, 0x10d7943u, 0x1e50d79u, 0x06bca1au, 0x1286bcau, 0x35e50d7u, 0x1435e50u},
+    {0x10d7ff8u, 0x1e50d79u, 0x06bca1au, 0x1286bcau, 0x35e50d7u, 0x1435e50u, 0x2f286bcu, 0x01af286u, 0x39435e5u, 0x0d79435u},
+    {0x35e50d4u, 0x1435e50u, 0x2f286bcu, 0x01af286u, 0x39435e5u, 0x0d79435u, 0x0a1af28u, 0x0bca1afu, 0x10d7943u, 0x0607179u},
+    {0x39435d7u, 0x0d79435u, 0x0a1af28u, 0x0bca1afu, 0x10d7943u, 0x1e50d79u, 0x06bca1au, 0x1286bcau, 0x3860717u, 0x17aae72u},
+    {0x10d7941u, 0x1e50d79u, 0x06bca1au, 0x1286bcau, 0x35e50d7u, 0x1435e50u, 0x2f286bcu, 0x05c3038u, 0x1b7aae7u, 0x03fd29du},
+    {0x35e50ceu, 0x1435e50u, 0x2f286bcu, 0x01af286u, 0x39435e5u, 0x1179435u, 0x0e5c303u, 0x1adbd57u, 0x363fd29u, 0x102209eu},
+    {0x39435d3u, 0x0d79435u, 0x0a1af28u, 0x0bca1afu, 0x0717943u, 0x0e72e18u, 0x13adbd5u, 0x1db1fe9u, 0x3502209u, 0x1e6788du},
+    {0x10d7938u, 0x1e50d79u, 0x06bca1au, 0x1038bcau, 0x2ae72e1u, 0x129d6deu, 0x13db1feu, 0x1ba8110u, 0x03e6788u, 0x132595au},
+    {0x35e50c8u, 0x1435e50u, 0x03038bcu, 0x1d57397u, 0x3d29d6du, 0x009ed8fu, 0x11ba811u, 0x141f33cu, 0x1132595u, 0x1a3cfc7u},
+    {0x39435e2u, 0x0e181c5u, 0x1bd5739u, 0x1fe94ebu, 0x2209ed8u, 0x188dd40u, 0x2b41f33u, 0x0e8992cu, 0x31a3cfcu, 0x05242a8u},
+    {0x32e181bu, 0x16deab9u, 0x31fe94eu, 0x01104f6u, 0x2788dd4u, 0x195a0f9u, 0x38e8992u, 0x118d1e7u, 0x2c5242au, 0x024e016u},
+    {0x1d6dea8u, 0x0d8ff4au, 0x281104fu, 0x133c46eu, 0x2595a0fu, 0x0fc744cu, 0x1518d1eu, 0x0d62921u, 0x3224e01u, 0x06156c6u},
+    {0x1ed8ff3u, 0x1d40882u, 0x1f33c46u, 0x192cad0u, 0x3cfc744u, 0x02a8c68u, 0x02d6292u, 0x0d91270u, 0x306156cu, 0x02c905du},
+    {0x0dd407eu, 0x00f99e2u, 0x0992cadu, 0x11e7e3au, 0x242a8c6u, 0x0016b14u, 0x18d9127u, 0x1b830abu, 0x022c905u, 0x111a765u},
+};
+
+// Lane primitives of the row layout (device: DPP within 16-lane rows; the host harness emulates them).
+#if defined(__HIPCC__) && !defined(PBFT_HOST_ONLY)
+__device__ __forceinline__ int32_t row_from_below(int32_t x) {  // lane j <- lane j - 1 of its row, lane 0 <- 0
+  return __builtin_amdgcn_update_dpp(0, x, 0x111, 0xF, 0xF, true);  // row_shr:1, bound_ctrl
+}
+__device__ __forceinline__ int32_t row_from_above(int32_t x) {  // lane j <- lane j + 1 of its row, lane 15 <- 0
+  return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true);  // row_shl:1, bound_ctrl
+}
+
+// out = z^-1 (0 -> 0) for a wave-uniform z (z as for fe_invert_gcd), divstep table `tab` in LDS.  Every lane
+// of the wave must call it (the limbs live across lanes); `out` is the same in every lane, carried.
+__device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint64_t* tab) {
+  const int li = (int)(threadIdx.x & 15);  // limb held by this lane
+  uint32_t w[8];
+  fe_to_words(w, z);
+  // f = p, g = z in 30-bit limbs (lanes 0..8; lanes 9..15 hold 0)
+  int32_t g = 0;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int b = 30 * i, wi = b >> 5, sh = b & 31;
+    uint64_t x = w[wi] >> sh;
+    if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << (32 - sh);
+    if (li == i) g = (int32_t)((uint32_t)x & INV_M30);
+  }
+  int32_t f = li == 0 ? 0x3FFFFFED : li < 8 ? 0x3FFFFFFF : li == 8 ? 0x7FFF : 0;
+  // D, E: column (A01, A11) of the accumulated matrix mod p, radix 2^25.5 (lanes 0..9)
+  int32_t D = 0, E = li == 0 ? 1 : 0;
+  const uint32_t fmask = li < 8 ? INV_M30 : 0xFFFFFFFFu;  // f, g: the top limb (lane 8) keeps its sign
+  const int32_t fcarry = li < 8 ? -1 : 0;                  // f, g: carries leave lanes 0..7 only
+  const int dsh = (li & 1) ? 25 : 26;
+  const uint32_t dmask = (1u << dsh) - 1u;
+  const int32_t dlive = li < 10 ? -1 : 0;
+  const int32_t w19 = li == 0 ? 19 : 0;  // the carry out of limb 9 re-enters limb 0 times 19
+  // (D, E) <- tp (D, E) mod p, two carry rounds (|h| < 2^31, |k| < 2^10 by the limb bounds above; lane 10 picks
+  // up limb 9's carry too and the final mask drops it -- that carry re-enters at lane 0, times 19)
+  auto update_de = [&](const int32_t tp[4]) {
+    const int64_t u = tp[0], v = tp[1], q = tp[2], r = tp[3];
+    const int64_t ad = u * D + v * E, ae = q * D + r * E;
+    const int32_t hd = (int32_t)(ad >> dsh), he = (int32_t)(ae >> dsh);
+    const int32_t hd9 = __builtin_amdgcn_readlane(hd, 9), he9 = __builtin_amdgcn_readlane(he, 9);
+    const int64_t nd = (int64_t)(int32_t)(((uint32_t)ad & dmask) + (uint32_t)row_from_below(hd)) + (int64_t)w19 * hd9;
+    const int64_t ne = (int64_t)(int32_t)(((uint32_t)ae & dmask) + (uint32_t)row_from_below(he)) + (int64_t)w19 * he9;
+    const int32_t kd = (int32_t)(nd >> dsh), ke = (int32_t)(ne >> dsh);
+    const int32_t kd9 = __builtin_amdgcn_readlane(kd, 9), ke9 = __builtin_amdgcn_readlane(ke, 9);
+    D = ((int32_t)((uint32_t)nd & dmask) + row_from_below(kd) + w19 * kd9) & dlive;
+    E = ((int32_t)((uint32_t)ne & dmask) + row_from_below(ke) + w19 * ke9) & dlive;
+  };
+  int32_t zeta = -1;
+  int32_t tp[4] = {1, 0, 0, 1};  // the previous batch's matrix: (D, E) lag one batch behind f, g
+  int k = 0;
+  for (; k < 20; ++k) {
+    if (__ballot(g != 0) == 0) break;  // g = 0: f = +-1
+    int32_t t[4];
+    zeta = divsteps30_tab(zeta, (uint32_t)__builtin_amdgcn_readfirstlane(f),
+                          (uint32_t)__builtin_amdgcn_readfirstlane(g), t, tab);
+    // f, g <- (t [f, g]) / 2^30: the chain the next lookups wait for
+    {
+      const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+      const int64_t af = u * f + v * g, ag = q * f + r * g;
+      int32_t nf = (int32_t)(af >> 30) + row_from_above((int32_t)((uint32_t)af & INV_M30));
+      int32_t ng = (int32_t)(ag >> 30) + row_from_above((int32_t)((uint32_t)ag & INV_M30));
+      f = (int32_t)((uint32_t)nf & fmask) + row_from_below((nf >> 30) & fcarry);
+      g = (int32_t)((uint32_t)ng & fmask) + row_from_below((ng >> 30) & fcarry);
+    }
+    // the previous batch's (D, E) update: independent of this batch's lookups, so the scheduler overlaps them
+    update_de(tp);
+    tp[0] = t[0]; tp[1] = t[1]; tp[2] = t[2]; tp[3] = t[3];
+  }
+  update_de(tp);
+  // x^-1 = +-D 2^(-30 k): f = +1 iff its limb 0 is 1
+  const bool neg = ((uint32_t)__builtin_amdgcn_readfirstlane(f) & INV_M30) != 1u;
+  fe d, c, p2;
+#pragma unroll
+  for (int i = 0; i < 10; ++i) {
+    // limbs in [-2^12, 2^26 + 2^12]: + 2p makes them positive and within fe_mul's operand bounds
+    p2.v[i] = (uint32_t)__builtin_amdgcn_readlane(D, i);
+    d.v[i] = p2.v[i] + (i == 0 ? 0x7FFFFDAu : (i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu);
+    c.v[i] = DS_INV2K[k][i];
+  }
+  fe_mul(out, d, c);
+  if (neg) { fe_neg(p2, out); fe_carry(p2); out = p2; }
+}
+#endif
+
 // out = z^-1 (0 -> 0) for a wave-uniform z (see above); z as for fe_invert_gcd
 // (The scalar unit does not help here, measured r03 with PBFT_FIN_STAMPS: run on the SALU, the divsteps take
 // half their VALU time but the 30-bit-limb updates, which need 64-bit products, take as long as the divsteps

@@ -28,6 +28,27 @@
 
 using namespace pbft;
 #include "verify_kernels.h"
+// Finish configuration by batch size (signatures per lane, product tree, waves per SIMD), measured on MI355X
+// with the lane-parallel wave inversion (profiles/r03/ab_finish.txt): 131k 0.2115 -> 0.1906 ms (width 2),
+// 262k 0.3628 -> 0.3429 (width 4), 2^20 finish kernel 118.6 -> 91.4 us (width 8, tree, 2 waves per SIMD).
+#ifndef PBFT_FIN_SMALL_UPTO
+#define PBFT_FIN_SMALL_UPTO (1u << 17)
+#endif
+#ifndef PBFT_FIN_FM_SMALL
+#define PBFT_FIN_FM_SMALL 2  // finish signatures per lane for N <= PBFT_FIN_SMALL_UPTO
+#endif
+#ifndef PBFT_FIN_FM_MID
+#define PBFT_FIN_FM_MID 4  // ... for PBFT_FIN_SMALL_UPTO < N < 2^19
+#endif
+#ifndef PBFT_FIN_FM_BIG
+#define PBFT_FIN_FM_BIG 8  // ... for N >= 2^19
+#endif
+#ifndef PBFT_FIN_TREE_MAX_FM
+#define PBFT_FIN_TREE_MAX_FM 8  // finish widths up to this use the cross-lane product tree (one inversion per wave)
+#endif
+#ifndef PBFT_FIN_W_BIG
+#define PBFT_FIN_W_BIG 2  // waves per SIMD of the product-tree finish for N >= 2^19
+#endif
 
 
 // ------------------------------------------------------------------ errors
@@ -106,6 +127,7 @@ struct pbft_ctx {
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
   int fin_tree = -1;                   // finish cross-lane tree levels (0 / 6; -1 = by batch size)
+  int fin_waves = 0;                   // product-tree finish compiled for 1 or 2 waves per SIMD (0 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
@@ -312,16 +334,17 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     st = fst;
   }
   if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
-    // signatures per finish lane (one divsteps inversion per lane): measured on MI355X
-    // (tools/size_probe.py, profiles/r02_size_probe.md) -- 1 up to 2^16, 4 up to 2^18, then 16
-    int fm = N >= ((uint64_t)1 << 19) ? FIN_M : N > ((uint64_t)1 << 16) ? 4 : 1;
+    // signatures per finish lane, product tree and waves per SIMD by batch size (PBFT_FIN_* above)
+    const bool big = N >= ((uint64_t)1 << 19);
+    int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID : PBFT_FIN_FM_SMALL;
     // cross-lane product tree (one variable-time inversion per wave) where few signatures share a
     // lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
     // (profiles/r02_ab_log.md)
-    int lv = fm <= 4 ? 6 : 0;
+    int lv = fm <= PBFT_FIN_TREE_MAX_FM ? 6 : 0;
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
-    HIP_TRY(launch_finish(fm, lv, dR, rs_stride, xyz, flags, N, dB, st));
+    const int fw = c->fin_waves ? c->fin_waves : (big ? PBFT_FIN_W_BIG : 1);
+    HIP_TRY(launch_finish(fm, lv, fw, dR, rs_stride, xyz, flags, N, dB, st));
     HIP_TRY(hipGetLastError());
   }
   if (fst) {
@@ -686,6 +709,7 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->split_below = parent->split_below;
   c->fin_m = parent->fin_m;
   c->fin_tree = parent->fin_tree;
+  c->fin_waves = parent->fin_waves;
   c->lat_split = parent->lat_split;
   c->timing = parent->timing;
   c->key_budget_mb = parent->key_budget_mb;
@@ -1201,6 +1225,7 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
       c->fin_m = (int)value;
       return PBFT_OK;
     case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 6) ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_FINISH_WAVES: c->fin_waves = (value == 1 || value == 2) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;

@@ -385,6 +385,12 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #endif
 static constexpr uint64_t LAT_WIDE_UPTO = PBFT_LAT_WIDE_UPTO;
 static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
+#ifndef PBFT_LAT_TAB
+#define PBFT_LAT_TAB (PBFT_LAT_TREE && !PBFT_LAT_DECOMP)  // table-driven divsteps for the wave's inversion
+#endif
+// the divstep table of fe_invert_tab (inv25519.h), constant-initialised at compile time (40 KB); the kernels
+// that invert a wave-uniform value copy it to LDS per block
+__device__ const ds_table g_ds_tab;
 static constexpr int LAT_BLOCK = 4 * 64;                   // (PBFT_LAT_DECOMP: 3 comb waves + 1 decompression wave)
 #ifndef PBFT_SPLIT_BELOW
 #define PBFT_SPLIT_BELOW 12288  // measured crossover: 8,192 sigs 0.105 ms here vs 0.133 ms one-lane; 16,384: 0.195 vs 0.133
@@ -448,6 +454,18 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
+#if PBFT_LAT_TAB && !PBFT_ABL_NOINV
+  // divstep table for the wave's one inversion (inv25519.h fe_invert_tab): every thread copies its share now,
+  // the barrier before the inversion publishes it (every wave of the block reaches that barrier)
+  __shared__ uint64_t ds_tab[DS_TAB_ENTRIES];
+  {
+    const uint4* src = (const uint4*)g_ds_tab.e;
+    uint4* dst = (uint4*)ds_tab;
+#pragma unroll
+    for (int k = 0; k < DS_TAB_ENTRIES / 2 / LAT_BLOCK; ++k)
+      dst[k * LAT_BLOCK + threadIdx.x] = src[k * LAT_BLOCK + threadIdx.x];
+  }
+#endif
 #if PBFT_LAT_DECOMP
   uint32_t* rdec = (uint32_t*)(lds + LAT_COMB_WAVES * COMB_LDS_PER_WAVE);  // [21][64]: x_R, y_R limbs, ok
   if (wave == LAT_COMB_WAVES) {
@@ -596,6 +614,13 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     });
 #if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
     zi = t;
+#elif PBFT_LAT_TAB
+    __syncthreads();  // the block's divstep table is in LDS (copied at kernel start)
+    #if PBFT_INV_WAVE
+    fe_invert_wave(zi, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
+#else
+    fe_invert_tab(zi, t, ds_tab);
+#endif
 #else
     fe_invert_var(zi, t);
 #endif
@@ -706,8 +731,9 @@ hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int nega
                              uint8_t* d_key_ok, hipStream_t st);
 
 // finish.hip: batch-inversion finish of the one-lane comb: fm (1, 2, 4, 8, 16) signatures per lane, lv = 0
-// (one inversion per lane) or 6 (one per wave, cross-lane product tree)
-hipError_t launch_finish(int fm, int lv, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
+// (one inversion per lane) or 6 (one per wave, cross-lane product tree), w = waves per SIMD it is compiled for
+// (lv = 6: 1, or 2 for fm 2 / 4 / 8)
+hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
                          const uint8_t* flags, uint64_t N, uint64_t* bitmap, hipStream_t st);
 // sign.hip: RFC 8032 signing, len = 85 (envelope), 0 (public keys only) or -1 (any length)
 void launch_sign(int len, dim3 grid, dim3 block, size_t lds, hipStream_t st, const uint32_t* seeds,

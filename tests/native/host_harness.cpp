@@ -56,7 +56,113 @@ static void build_table(const ge& P0, uint32_t* out) {
     }
 }
 
+static const ds_table g_ds_tab;
+
+
+// Host emulation of fe_invert_wave (inv25519.h): the same per-lane arithmetic over one 16-lane row, the DPP
+// row shifts and readlanes spelled out -- checks the algorithm and its limb bounds off the GPU.
+static void fe_invert_wave_emu(fe& out, const fe& z, int* batches = nullptr) {
+  uint32_t w[8];
+  fe_to_words(w, z);
+  int32_t f[16], g[16], D[16], E[16];
+  for (int li = 0; li < 16; ++li) {
+    g[li] = 0;
+    if (li < 9) {
+      const int b = 30 * li, wi = b >> 5, sh = b & 31;
+      uint64_t x = w[wi] >> sh;
+      if (wi + 1 < 8) x |= (uint64_t)w[wi + 1] << (32 - sh);
+      g[li] = (int32_t)((uint32_t)x & INV_M30);
+    }
+    f[li] = li == 0 ? 0x3FFFFFED : li < 8 ? 0x3FFFFFFF : li == 8 ? 0x7FFF : 0;
+    D[li] = 0; E[li] = li == 0 ? 1 : 0;
+  }
+  auto below = [](const int32_t* x, int li) { return li == 0 ? 0 : x[li - 1]; };
+  auto above = [](const int32_t* x, int li) { return li == 15 ? 0 : x[li + 1]; };
+  int32_t zeta = -1;
+  int k = 0;
+  for (; k < 20; ++k) {
+    bool any = false;
+    for (int li = 0; li < 16; ++li) any |= g[li] != 0;
+    if (!any) break;
+    int32_t t[4];
+    zeta = divsteps30_tab(zeta, (uint32_t)f[0], (uint32_t)g[0], t, g_ds_tab.e);
+    const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
+    int32_t lf[16], lg[16], hf[16], hg[16], nf[16], ng[16], cf[16], cg[16];
+    for (int li = 0; li < 16; ++li) {
+      const int64_t af = u * f[li] + v * g[li], ag = q * f[li] + r * g[li];
+      if (af > ((int64_t)1 << 62) || af < -((int64_t)1 << 62)) throw 1;
+      lf[li] = (int32_t)((uint32_t)af & INV_M30); lg[li] = (int32_t)((uint32_t)ag & INV_M30);
+      hf[li] = (int32_t)(af >> 30); hg[li] = (int32_t)(ag >> 30);
+    }
+    for (int li = 0; li < 16; ++li) {
+      nf[li] = hf[li] + above(lf, li); ng[li] = hg[li] + above(lg, li);
+      const int32_t fc = li < 8 ? -1 : 0;
+      cf[li] = (nf[li] >> 30) & fc; cg[li] = (ng[li] >> 30) & fc;
+    }
+    for (int li = 0; li < 16; ++li) {
+      const uint32_t fm = li < 8 ? INV_M30 : 0xFFFFFFFFu;
+      f[li] = (int32_t)((uint32_t)nf[li] & fm) + below(cf, li);
+      g[li] = (int32_t)((uint32_t)ng[li] & fm) + below(cg, li);
+    }
+    int64_t ad[16], ae[16], nd[16], ne[16];
+    int32_t hd[16], he[16], kd[16], ke[16];
+    for (int li = 0; li < 16; ++li) {
+      const int dsh = (li & 1) ? 25 : 26;
+      ad[li] = u * D[li] + v * E[li]; ae[li] = q * D[li] + r * E[li];
+      const int64_t hd64 = ad[li] >> dsh, he64 = ae[li] >> dsh;
+      if (hd64 != (int32_t)hd64 || he64 != (int32_t)he64) throw 2;
+      hd[li] = (int32_t)hd64; he[li] = (int32_t)he64;
+    }
+    for (int li = 0; li < 16; ++li) {
+      const int dsh = (li & 1) ? 25 : 26;
+      const uint32_t dm = (1u << dsh) - 1u;
+      const int32_t w19 = li == 0 ? 19 : 0;
+      const int64_t sd = (int64_t)((uint32_t)ad[li] & dm) + below(hd, li), se = (int64_t)((uint32_t)ae[li] & dm) + below(he, li);
+      if (sd != (int32_t)sd || se != (int32_t)se) throw 3;
+      nd[li] = sd + (int64_t)w19 * hd[9]; ne[li] = se + (int64_t)w19 * he[9];
+      const int64_t kd64 = nd[li] >> dsh, ke64 = ne[li] >> dsh;
+      if (kd64 != (int32_t)kd64 || ke64 != (int32_t)ke64) throw 4;
+      kd[li] = (int32_t)kd64; ke[li] = (int32_t)ke64;
+    }
+    for (int li = 0; li < 16; ++li) {
+      const int dsh = (li & 1) ? 25 : 26;
+      const uint32_t dm = (1u << dsh) - 1u;
+      const int32_t w19 = li == 0 ? 19 : 0, dl = li < 10 ? -1 : 0;
+      D[li] = ((int32_t)((uint32_t)nd[li] & dm) + below(kd, li) + w19 * kd[9]) & dl;
+      E[li] = ((int32_t)((uint32_t)ne[li] & dm) + below(ke, li) + w19 * ke[9]) & dl;
+      if (D[li] > (1 << 26) + (1 << 12) || D[li] < -(1 << 12) || E[li] > (1 << 26) + (1 << 12) || E[li] < -(1 << 12))
+        throw 5;
+    }
+  }
+  if (batches) *batches = k;
+  const bool neg = ((uint32_t)f[0] & INV_M30) != 1u;
+  fe d, c, p2;
+  for (int i = 0; i < 10; ++i) {
+    d.v[i] = (uint32_t)D[i] + (i == 0 ? 0x7FFFFDAu : (i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu);
+    c.v[i] = DS_INV2K[k][i];
+  }
+  fe_mul(out, d, c);
+  if (neg) { fe_neg(p2, out); fe_carry(p2); out = p2; }
+}
+
 extern "C" {
+
+// divsteps30_tab against divsteps30 on n pseudo-random (zeta, f odd, g) triples: number of mismatches
+int hh_divsteps_tab_check(uint64_t seed, int n) {
+  int bad = 0;
+  uint64_t x = seed;
+  auto next = [&]() { x ^= x << 13; x ^= x >> 7; x ^= x << 17; return x; };
+  for (int i = 0; i < n; ++i) {
+    const uint64_t a = next(), b = next();
+    int32_t zeta = (int32_t)(a % 41) - 20;  // zeta classes well past the clamp on both sides
+    if (i % 7 == 0) zeta = (int32_t)(b % 1200) - 600;
+    const uint32_t f = (uint32_t)(a >> 32) | 1u, g = (uint32_t)b;
+    int32_t t1[4], t2[4];
+    const int32_t z1 = divsteps30(zeta, f, g, t1), z2 = divsteps30_tab(zeta, f, g, t2, g_ds_tab.e);
+    bad += (z1 != z2 || t1[0] != t2[0] || t1[1] != t2[1] || t1[2] != t2[2] || t1[3] != t2[3]);
+  }
+  return bad;
+}
 
 void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
   uint32_t wa[8], wb[8], wo[8];
@@ -83,6 +189,10 @@ void hh_fe_op(int op, const uint8_t* a, const uint8_t* b, uint8_t* out) {
     case 15: { fe t; fe_add(t, fa, fb); fe_invert_gcd(fo, t); break; } // of an uncarried sum
     case 16: fe_invert_var(fo, fa); break;                            // variable-time divsteps (uniform input)
     case 17: { fe t; fe_add(t, fa, fb); fe_invert_var(fo, t); break; }
+    case 18: fe_invert_tab(fo, fa, g_ds_tab.e); break;                // table-driven divsteps (uniform input)
+    case 19: { fe t; fe_add(t, fa, fb); fe_invert_tab(fo, t, g_ds_tab.e); break; }
+    case 20: try { fe_invert_wave_emu(fo, fa); } catch (int e) { fe_zero(fo); fo.v[0] = 1000u + (uint32_t)e; } break;
+    case 21: { fe t; fe_add(t, fa, fb); try { fe_invert_wave_emu(fo, t); } catch (int e) { fe_zero(fo); fo.v[0] = 1000u + (uint32_t)e; } break; }
     default: fo = fa;
   }
   fe_to_words(wo, fo);

@@ -84,6 +84,30 @@ def test_divsteps_inversion_extremes(hh):
         assert _fe(hh, 17, a % 2**255, b) == pow(a % 2**255 + b, P - 2, P)
 
 
+def test_table_divsteps_match_divsteps30(hh):
+    """divsteps30_tab (6 lookups of 5 half-delta divsteps in the 5,120-entry table, inv25519.h) returns the same
+    transition matrix and zeta as the step-by-step divsteps30, zeta classes on both sides of the clamp included."""
+    hh.hh_divsteps_tab_check.restype = ctypes.c_int
+    assert hh.hh_divsteps_tab_check(ctypes.c_uint64(0x9E3779B97F4A7C15), 300000) == 0
+
+
+def test_wave_inversion_emulation(hh):
+    """fe_invert_tab and the lane-parallel fe_invert_wave (its host emulation: 16-lane rows, DPP shifts and
+    readlanes spelled out, every limb bound asserted) equal z^(p-2) on the inversion extremes and random values."""
+    vals = [2**k for k in range(255)] + [P - 2**k for k in range(1, 255)] + [(2**k - 1) for k in range(1, 256)]
+    vals += [P - k for k in range(1, 40)] + [P + k for k in range(0, 19)] + [2**255 - 1 - k for k in range(20)] + [0]
+    rnd = random.Random(1234)
+    vals += [rnd.getrandbits(rnd.randrange(1, 256)) for _ in range(1500)]
+    for a in vals:
+        want = pow(a % 2**255, P - 2, P)
+        assert _fe(hh, 18, a % 2**255, 0) == want, a
+        assert _fe(hh, 20, a % 2**255, 0) == want, a   # (a bound violation would return 1000 + its site)
+    for i, a in enumerate(vals[:300]):
+        b = vals[(i * 7 + 3) % len(vals)] % 2**255
+        assert _fe(hh, 19, a % 2**255, b) == pow(a % 2**255 + b, P - 2, P)
+        assert _fe(hh, 21, a % 2**255, b) == pow(a % 2**255 + b, P - 2, P)
+
+
 @pytest.mark.parametrize("ln", [0, 1, 47, 48, 63, 64, 85, 111, 112, 175, 176, 239, 240, 300, 1023])
 def test_sha512_ram(hh, ln):
     rnd = random.Random(ln)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Interleaved A/B timing of verify_kernel builds in ONE process (cdna guide §5.4 rule 24).
 
-usage: python tools/ab.py lib1.so lib2.so ... [--rounds 8 --iters 10 --budget-mb X]
-Each lib gets its own context on the same synthetic 2^20-signature round.
+usage: python tools/ab.py lib1.so lib2.so[@opt=value,...] ... [--rounds 8 --iters 10 --budget-mb X]
+Each lib gets its own context on the same synthetic 2^20-signature round; `@2=4,4=6,8=2` sets
+pbft_verify_set_option(option, value) pairs on that context (the same library may appear with different options).
 """
 import argparse
 import ctypes
@@ -53,7 +54,8 @@ def main():
     st = torch.cuda.Stream(dev)
     ctxs = []
     for p in a.libs:
-        lib = ctypes.CDLL(os.path.abspath(p))
+        path, _, opts = p.partition("@")
+        lib = ctypes.CDLL(os.path.abspath(path))
         vp = ctypes.c_void_p
         lib.pbft_verify_ctx_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         lib.pbft_verify_set_keys.argtypes = [vp, vp, ctypes.c_uint32, vp]
@@ -63,6 +65,10 @@ def main():
         lib.pbft_build_info.restype = ctypes.c_char_p
         c = vp()
         assert lib.pbft_verify_ctx_create(0, ctypes.byref(c)) == 0
+        lib.pbft_verify_set_option.argtypes = [vp, ctypes.c_int, ctypes.c_uint64]
+        for kv in filter(None, opts.split(",")):
+            k, v = kv.split("=")
+            assert lib.pbft_verify_set_option(c, int(k), int(v)) == 0, kv
         ok = np.zeros(len(pub), np.uint8)
         assert lib.pbft_verify_set_keys(c, pub.ctypes.data, len(pub), ok.ctypes.data) == 0
         ctxs.append((p, lib, c))

@@ -32,6 +32,12 @@ __global__ void k(uint64_t* out, uint64_t* cyc, uint32_t seed) {
 #define R4 M1(0) M1(1) M1(2) M1(3)
       asm volatile(R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4 R4
                    : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3) : [x] "v"(x), [y] "v"(y) : "vcc");
+    } else if constexpr (CH == 101) {  // one chain, s_nop 0 after every mad (the asm-boundary pad)
+#define MN M1(0) "s_nop 0\n\t"
+      asm volatile(MN MN MN MN MN MN MN MN MN MN MN MN MN MN MN MN : "+v"(a0) : [x] "v"(x), [y] "v"(y) : "vcc");
+    } else if constexpr (CH == 102) {  // two chains, s_nop 0 after every second mad
+#define MN2 M1(0) M1(1) "s_nop 0\n\t"
+      asm volatile(MN2 MN2 MN2 MN2 MN2 MN2 MN2 MN2 : "+v"(a0), "+v"(a1) : [x] "v"(x), [y] "v"(y) : "vcc");
     } else {
 #define R8 M1(0) M1(1) M1(2) M1(3) M1(4) M1(5) M1(6) M1(7)
       asm volatile(R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8 R8
@@ -57,7 +63,7 @@ void run(uint64_t* d, uint64_t* dc, int wps) {
   std::vector<uint64_t> c(blocks);
   (void)hipMemcpy(c.data(), dc, blocks * 8, hipMemcpyDeviceToHost);
   std::sort(c.begin(), c.end());
-  const double mads_per_wave = (double)ITERS * 16 * CH;
+  const double mads_per_wave = (double)ITERS * 16 * (CH == 101 ? 1 : CH == 102 ? 1 : CH);
   const double med = (double)c[blocks / 2];
   const double wall_mads = (double)blocks * 64 * mads_per_wave;
   printf("chains=%d waves/SIMD=%d  cycles per mad in a wave %.2f  per SIMD %.2f  (%.3f ms, %.2f T mad/s)\n", CH, wps,
@@ -68,6 +74,6 @@ int main() {
   uint64_t *d, *dc;
   (void)hipMalloc(&d, sizeof(uint64_t) * 1024 * 8 * 64);
   (void)hipMalloc(&dc, sizeof(uint64_t) * 1024 * 8);
-  for (int w = 1; w <= 4; w *= 2) { run<1>(d, dc, w); run<2>(d, dc, w); run<3>(d, dc, w); run<4>(d, dc, w); run<8>(d, dc, w); }
+  for (int w = 1; w <= 4; w *= 2) { run<1>(d, dc, w); run<2>(d, dc, w); run<3>(d, dc, w); run<4>(d, dc, w); run<8>(d, dc, w); run<101>(d, dc, w); run<102>(d, dc, w); }
   return 0;
 }
