@@ -346,7 +346,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 5
     pp_env[:, 4] = 0  # kind 0: the PrePrepare envelope of each seq
     pR, pS, _ = v.sign(seeds, np.full(n_seq, primary, np.uint16), pp_env, ENVELOPE)
     ops = [b"op-" + str(q).encode() for q in range(1, n_seq + 1)]
-    res = {"submit_ms": [], "e2e_ms": [], "polls": [], "push_ms": []}
+    res = {"submit_ms": [], "e2e_ms": [], "polls": [], "push_ms": [], "apply_ms": []}
     ev = (Event * 16384)()
     for r in range(rounds + 1):
         rep = ctypes.c_void_p()
@@ -383,9 +383,12 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 5
             res["e2e_ms"].append((t2 - t0) * 1e3)
             res["polls"].append(polls)
             res["push_ms"].append(t_push * 1e3)
+            res["apply_ms"].append(st.apply_ns * 1e-6)
     e2e = float(np.median(res["e2e_ms"]))
     return {"value": n / (e2e * 1e-3), "unit": "verifies/s", "ms_per_round": e2e,
             "flush_submit_ms": float(np.median(res["submit_ms"])), "polls_while_running": int(np.median(res["polls"])),
+            "apply_ms": float(np.median(res["apply_ms"])),
+            "gpu_wait_ms": float(np.median(res["e2e_ms"]) - np.median(res["submit_ms"]) - np.median(res["apply_ms"])),
             "push_many_ms": float(np.median(res["push_ms"])), "sigs": n + n_seq, "rounds": rounds,
             "path": "pbft_replica: push_many (2^20 votes + 2048 PrePrepares, untimed) -> flush_submit (votes form "
                     "into pinned staging, async H2D + kernels + D2H) -> flush_poll loop until the bitmap is applied "

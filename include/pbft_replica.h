@@ -107,6 +107,8 @@ typedef struct {
   uint64_t windows_gc;         /* windows erased (committed prefix or checkpoint)       */
   uint64_t low_watermark;      /* h                                                     */
   uint64_t live_windows;       /* windows currently held                                */
+  uint64_t submit_ns;          /* host time inside pbft_replica_flush_submit (batch build + launch), summed */
+  uint64_t apply_ns;           /* host time applying finished batches (bitmap -> votes, quorums, GC), summed */
 } pbft_replica_stats;
 
 /* Optional verifier override (tests without a GPU): same SoA contract as

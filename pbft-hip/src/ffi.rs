@@ -80,6 +80,8 @@ pub struct pbft_replica_stats {
     pub windows_gc: u64,
     pub low_watermark: u64,
     pub live_windows: u64,
+    pub submit_ns: u64,
+    pub apply_ns: u64,
 }
 
 #[repr(C)]

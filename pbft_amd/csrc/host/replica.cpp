@@ -313,9 +313,14 @@ static void gc(pbft_replica* r) {
 // Events (pre-prepared, prepared :177-182, committed_local :214-223) of every dirty window, in (view, seq)
 // order, into the replica's queue: the decision is recorded whether or not the caller has room for it.
 static void evaluate(pbft_replica* r) {
+  auto wi = r->windows.begin();
   for (const Key& k : r->dirty) {
-    auto wi = r->windows.find(k);
-    if (wi == r->windows.end()) continue;
+    // both sorted by key: advance (a lookup when the next dirty key is far ahead)
+    if (wi != r->windows.end() && wi->first < k) {
+      auto nx = std::next(wi);
+      wi = (nx != r->windows.end() && nx->first >= k) ? nx : r->windows.lower_bound(k);
+    }
+    if (wi == r->windows.end() || wi->first != k) continue;
     Window& w = wi->second;
     const uint64_t view = k.first, seq = k.second;
     if (!w.pre_prepared_reported && w.have_pre_prepare) {
@@ -363,9 +368,10 @@ static void revert_segs(pbft_replica* r) {
 // wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
 // candidates leave the windows.  Segments [s0, s1) (whole windows: a window's segments stay on one thread, in
 // order); counts into st[3] = accepted, rejected_sig, rejected_digest; touched[g] = some candidate accepted.
-static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st[3], uint8_t* touched) {
+static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3], uint8_t* touched) {
   std::vector<int64_t> amap;
   std::vector<uint8_t> mism;
+  uint64_t st[3] = {0, 0, 0};  // local: the threads' st_out entries share cache lines
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
     Window* wp = g.w;
@@ -424,6 +430,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st[3], u
     p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
     touched[gi] = acc_n > 0;
   }
+  for (int k = 0; k < 3; ++k) st_out[k] += st[k];
 }
 
 static void apply_segs(pbft_replica* r) {
@@ -453,8 +460,8 @@ static void apply_segs(pbft_replica* r) {
     r->stats.rejected_sig += c[1];
     r->stats.rejected_digest += c[2];
   }
-  for (size_t gi = 0; gi < G; ++gi)
-    if (touched[gi]) r->dirty.insert(r->segs[gi].key);
+  for (size_t gi = 0; gi < G; ++gi)  // segments come in window (key) order: O(1) hinted inserts
+    if (touched[gi]) r->dirty.emplace_hint(r->dirty.end(), r->segs[gi].key);
   r->segs.clear();
   r->in_flight = false;
   r->erased_in_flight = false;
@@ -636,8 +643,20 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
 }
 
 // Verify every READY sub-window (force: every pending candidate) in one batch, asynchronously.
+static uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
+static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows);
 int pbft_replica_flush_submit(pbft_replica* r, int force, uint64_t* n_rows) {
   if (!r) return PBFT_EINVAL;
+  const auto t0 = std::chrono::steady_clock::now();
+  const int rc = flush_submit_impl(r, force, n_rows);
+  r->stats.submit_ns += ns_since(t0);
+  return rc;
+}
+
+static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   if (n_rows) *n_rows = 0;
   if (r->in_flight) return PBFT_EBUSY;
   if (!r->verify_fn && !r->vsub && !r->ctx) return PBFT_ENODEV;
@@ -732,24 +751,15 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
     else if (r->in_flight_via == 1) st = r->vpoll(r->vuser);
     if (st == 0) return 0;
     if (st < 0) { revert_segs(r); return st; }
-#ifdef PBFT_REPLICA_TIMING
-    auto t0 = std::chrono::steady_clock::now();
-#endif
+    const auto t0 = std::chrono::steady_clock::now();
     apply_segs(r);
-#ifdef PBFT_REPLICA_TIMING
-    auto t1 = std::chrono::steady_clock::now();
     evaluate(r);
-    auto t2 = std::chrono::steady_clock::now();
     gc(r);
-    auto t3 = std::chrono::steady_clock::now();
-    fprintf(stderr, "apply %.2f ms evaluate %.2f ms gc %.2f ms\n",
-            std::chrono::duration<double, std::milli>(t1 - t0).count(),
-            std::chrono::duration<double, std::milli>(t2 - t1).count(),
-            std::chrono::duration<double, std::milli>(t3 - t2).count());
-#endif
+    r->stats.apply_ns += ns_since(t0);
+  } else {
+    evaluate(r);
+    gc(r);
   }
-  evaluate(r);
-  gc(r);
   drain(r, events, max_events, n_events);
   return 1;
 }

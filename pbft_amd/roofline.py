@@ -32,7 +32,8 @@ the form r01 timed: that, not the VALU, was the gap to MI355X_MICROARCH.md's rat
 """
 import re
 
-FIN_M = 16
+FIN_M = 8            # finish signatures per lane at >= 2^19 signatures (pbft_verify.hip PBFT_FIN_FM_BIG)
+FIN_TREE_LEVELS = 6
 VALU_MAD_PEAK_PER_S = 31.19e12   # measured, profiles/r03/valu_clock.txt
 MAD_CYCLES_PER_WAVE_INSTR = 4.53  # per SIMD, at the measured clock
 MAD_CLOCK_HZ = 2.157e9            # in-kernel clock during that measurement
@@ -49,9 +50,9 @@ ENTRY_BYTES = 128
 INPUT_BYTES = 32 + 32 + 2 + 85  # R, S, key index, envelope
 
 
-# divsteps inversion (inv25519.h): per batch of 30 divsteps, [f, g] update 4 x 9 and [d, e] update 6 x 9
-# 32x32->64 products; 20 batches
-INV_PRODUCTS = 20 * (4 * 9 + 6 * 9)
+# wave-uniform inversion (inv25519.h fe_invert_wave): per batch of 30 divsteps the lane-parallel f, g update (4 x 9
+# lane products) and D, E update (4 x 10), ~18 batches, then one field multiply by 2^-30k
+INV_PRODUCTS = 18 * (4 * 9 + 4 * 10) + 100
 
 
 def products_comb(pb: int, pa: int) -> int:
@@ -60,9 +61,10 @@ def products_comb(pb: int, pa: int) -> int:
 
 
 def products_per_verify(pb: int, pa: int) -> int:
-    """comb_kernel + finish_kernel<16>: + one divsteps inversion per 16 signatures, 3 batch-inversion muls and 2
-    affine muls per signature."""
-    return products_comb(pb, pa) + INV_PRODUCTS // FIN_M + 5 * 100
+    """comb_kernel + finish_kernel<8, 6, 2>: 3 batch-inversion muls and 2 affine muls per signature, the product
+    tree's 12 muls per lane over FIN_M signatures, one wave inversion per 64 FIN_M signatures."""
+    return (products_comb(pb, pa) + 5 * 100 + 2 * FIN_TREE_LEVELS * 100 // FIN_M
+            + INV_PRODUCTS // (64 * FIN_M))
 
 
 def gather_bytes_per_verify(pb: int, pa: int) -> int:

@@ -24,7 +24,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in ("pushed", "verified", "accepted", "rejected_sig", "rejected_digest",
                                                 "rejected_view", "duplicates", "batches", "rejected_watermark",
                                                 "rejected_signer", "dropped_flood", "windows_gc", "low_watermark",
-                                                "live_windows")]
+                                                "live_windows", "submit_ns", "apply_ns")]
 
 
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
