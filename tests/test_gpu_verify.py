@@ -190,8 +190,9 @@ def test_config4_full_size_properties(gv, coracle):
     sl = slice(int(idx.min()) // 64 * 64, int(idx.min()) // 64 * 64 + 16384)
     exp = oracle_bits(coracle, pub, R2[sl], S2[sl], K2[sl], M2[sl], 85)
     assert (got2[sl] == exp).all()
-    # sub-batch sizes that select the other finish-kernel widths (4 and 1 signatures per lane; the full round
-    # uses 16) and a ragged tail: the same bits as the full-round launch
+    # sub-batch sizes that select the other finish configurations (4 and 2 signatures per lane at one wave per
+    # SIMD; the full round uses 8 with the tree at two waves per SIMD) and a ragged tail: the same bits as the
+    # full-round launch
     for n in (300_007, 65_536 + 63, 4096):
         got4, _ = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
         assert (got4 == got2[:n]).all(), n
@@ -409,7 +410,8 @@ def test_config2_pipelined_window(gv, coracle):
     """BASELINE configs[1]: n = 4 replicas, 1,024 pipelined requests -> 8,192 Prepare + Commit signatures in one
     window batch (latency-mode kernel), 1 % adversarial, bit-exact with the C oracle; the same batch through the
     one-lane-per-signature kernels (PBFT_OPT_SPLIT_BELOW = 0) gives the same bits, with every finish width, with
-    and without the finish's cross-lane product tree, also on a ragged batch (partial last wave)."""
+    and without the finish's cross-lane product tree (its wave inversion, inv25519.h fe_invert_wave), compiled for
+    one or two waves per SIMD, also on a ragged batch (partial last wave)."""
     from pbft_amd import GpuBatchVerifier
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 4, 1024, tag=2)
     assert len(R) == 8192
@@ -436,14 +438,15 @@ def test_config2_pipelined_window(gv, coracle):
     try:
         v1.set_keys(pub)
         n2 = len(R2) - 37
-        for lv in (0, 6):
+        for lv, waves in ((0, 1), (6, 1), (6, 2)):  # (6, 2): the tree finish compiled for 2 waves per SIMD
             v1.set_option(v1.OPT_FINISH_TREE, lv)
+            v1.set_option(v1.OPT_FINISH_WAVES, waves)
             for fm in (1, 2, 4, 8, 16):
                 v1.set_option(v1.OPT_FINISH_WIDTH, fm)
                 got1, _ = verify(v1, R2, S2, K2, M2, 85)
-                assert (got1 == exp).all(), (fm, lv)
+                assert (got1 == exp).all(), (fm, lv, waves)
                 got2, _ = verify(v1, R2[:n2], S2[:n2], K2[:n2], M2[:n2], 85)
-                assert (got2 == exp[:n2]).all(), (fm, lv, n2)
+                assert (got2 == exp[:n2]).all(), (fm, lv, waves, n2)
         with pytest.raises(Exception):
             v1.set_option(v1.OPT_FINISH_WIDTH, 3)
     finally:
