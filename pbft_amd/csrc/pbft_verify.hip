@@ -381,7 +381,16 @@ struct stage_layout {
 // staging halves: the H2D copy of chunk c+1 (context copy stream) overlaps the
 // kernels of chunk c (context stream).  A multiple of 64: chunks own whole
 // bitmap words.  2^18 keeps every chunk in the one-lane-per-signature mode.
-static constexpr uint64_t PIPE_CHUNK = 1ull << 18;
+#ifndef PBFT_PIPE_CHUNK_LOG2
+#define PBFT_PIPE_CHUNK_LOG2 18
+#endif
+#ifndef PBFT_VOTES_CHUNK_LOG2
+#define PBFT_VOTES_CHUNK_LOG2 18
+#endif
+static constexpr uint64_t PIPE_CHUNK = 1ull << PBFT_PIPE_CHUNK_LOG2;
+// the votes form moves 70 B per signature instead of 151: its copies are about as long as the kernels, so a
+// smaller chunk shortens the pipeline's fill and drain (PBFT_VOTES_CHUNK_LOG2)
+static constexpr uint64_t VOTES_CHUNK = 1ull << PBFT_VOTES_CHUNK_LOG2;
 
 // Copy a host batch into the staging buffer and launch.  Result: the device bitmap.
 static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint8_t* M,
@@ -473,9 +482,9 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
                                   uint32_t rs_stride = 32) {
   const uint64_t words = (N + 63) / 64;
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
-  const uint64_t ch = N < PIPE_CHUNK ? N : PIPE_CHUNK;
+  const uint64_t ch = N < VOTES_CHUNK ? N : VOTES_CHUNK;
   const votes_layout L(ch);
-  int rc = ensure_stage(c, env_bytes + (N > PIPE_CHUNK ? 2 : 1) * L.bytes, words);
+  int rc = ensure_stage(c, env_bytes + (N > VOTES_CHUNK ? 2 : 1) * L.bytes, words);
   if (rc) return rc;
   // envelope table first (copy stream), then each chunk's columns; the kernels of chunk c run on the context
   // stream after its copies, overlapping the copies of chunk c+1
@@ -488,8 +497,8 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
   rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &dWK);
   if (rc) return rc;
   uint64_t chunk = 0;
-  for (uint64_t lo = 0; lo < N; lo += PIPE_CHUNK, ++chunk) {
-    const uint64_t n = N - lo < PIPE_CHUNK ? N - lo : PIPE_CHUNK;
+  for (uint64_t lo = 0; lo < N; lo += VOTES_CHUNK, ++chunk) {
+    const uint64_t n = N - lo < VOTES_CHUNK ? N - lo : VOTES_CHUNK;
     const int b = (int)(chunk & 1);
     uint8_t* base = c->d_stage + env_bytes + (size_t)b * L.bytes;
     if (chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
