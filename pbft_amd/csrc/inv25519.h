@@ -222,6 +222,9 @@ __host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t
 // ds_read_b64 plus ~8 dependent VALU operations on the critical path instead of ~5 x 18 (constant-time) or
 // the ctz / Newton-inverse chain of divsteps30_var.
 #define DS_TN 5
+#ifndef PBFT_INV_VALU_LOOKUP
+#define PBFT_INV_VALU_LOOKUP 1  // the divstep lookups on the VALU (row broadcast): -13 % inversion cycles (profiles/r03/ab_finish.txt)
+#endif
 #ifndef PBFT_INV_WAVE
 #define PBFT_INV_WAVE 1  // wave-uniform inversions: fe_invert_wave (limbs across lanes) instead of fe_invert_tab
 #endif
@@ -407,10 +410,26 @@ __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint6
   int32_t tp[4] = {1, 0, 0, 1};  // the previous batch's matrix: (D, E) lag one batch behind f, g
   int k = 0;
   for (; k < 20; ++k) {
+#if !PBFT_ABL_INV_NOLOOKUP
     if (__ballot(g != 0) == 0) break;  // g = 0: f = +-1
+#else
+    if (k == 18) break;
+#endif
     int32_t t[4];
+#if PBFT_ABL_INV_NOLOOKUP  // ablation (timing only, results wrong): a fixed matrix instead of the lookups
+    t[0] = 1 << 29; t[1] = (int32_t)(__builtin_amdgcn_readfirstlane(f) & 7); t[2] = 3; t[3] = 1 << 28;
+    zeta -= 30;
+#else
+#if PBFT_INV_VALU_LOOKUP
+    // limb 0 to every lane of its row by DPP (row_newbcast:0): the lookup chain then stays on the VALU (a scalar
+    // copy, v_readfirstlane, puts it on the SALU with two VALU <-> SALU crossings per lookup)
+    zeta = divsteps30_tab(zeta, (uint32_t)__builtin_amdgcn_update_dpp(0, f, 0x150, 0xF, 0xF, false),
+                          (uint32_t)__builtin_amdgcn_update_dpp(0, g, 0x150, 0xF, 0xF, false), t, tab);
+#else
     zeta = divsteps30_tab(zeta, (uint32_t)__builtin_amdgcn_readfirstlane(f),
                           (uint32_t)__builtin_amdgcn_readfirstlane(g), t, tab);
+#endif
+#endif
     // f, g <- (t [f, g]) / 2^30: the chain the next lookups wait for
     {
       const int64_t u = t[0], v = t[1], q = t[2], r = t[3];
