@@ -182,6 +182,9 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
     period = batch / offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else 0.0
     pending = [None] * n_ctx  # (ticket, scheduled time)
     lat, done = [], 0
+    import gc
+    gc.collect()
+    gc.disable()  # no collector pause inside the timed loop (a host-side tail, not the verifier's)
     t0 = time.perf_counter()
     k = 0
     while True:
@@ -206,6 +209,7 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
             pending[ci] = (ctxs[ci].submit(batches[k % len(batches)]), t_sched if period else time.perf_counter())
             k += 1
     wall = time.perf_counter() - t0
+    gc.enable()
     for c in ctxs:
         c.close()
     lat = np.array(lat)
