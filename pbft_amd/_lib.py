@@ -85,6 +85,9 @@ def load() -> ctypes.CDLL:
         "pbft_verify_votes_async": (i32, [vp, vp, vp, vp, vp, vp, u32, u64, vp]),
         "pbft_verify_votes_stage": (i32, [vp, u64, u32, vp]),
         "pbft_verify_votes_submit": (i32, [vp, u64, u32, vp]),
+        "pbft_verify_votes_submit_begin": (i32, [vp, u64, u32, vp]),
+        "pbft_verify_votes_submit_rows": (i32, [vp, u64]),
+        "pbft_verify_poll_rows": (i32, [vp, ctypes.POINTER(u64)]),
         "pbft_multi_create": (i32, [vp, u32, ctypes.POINTER(vp)]),
         "pbft_multi_destroy": (i32, [vp]),
         "pbft_multi_sync": (i32, [vp]),

@@ -21,11 +21,17 @@
 #include <cstdio>
 #endif
 #include <array>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <unordered_map>
 #include <utility>
@@ -146,6 +152,65 @@ struct Seg {
   uint8_t kind;   // 0 PrePrepare, 1 Prepare, 2 Commit
 };
 
+// Worker threads for the batch fill and the bitmap application: one pool per process, started on first use and
+// reused by every large batch of every replica (creating 16 threads costs about a millisecond in a process that
+// maps the GPU's memory); one job at a time (start() holds the pool until wait()).
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool* p = new WorkerPool();  // never destroyed: idle workers may outlive static destructors
+    return *p;
+  }
+  // run f(0) .. f(T - 1) on T workers; returns at once (wait() joins the round)
+  void start(size_t T, std::function<void(size_t)> f) {
+    job_mu_.lock();
+    while (th_.size() < T) {
+      const size_t id = th_.size();
+      th_.emplace_back([this, id] { loop(id); });
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = std::move(f);
+      active_ = T;
+      pending_ = T;
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      done_.wait(lk, [&] { return pending_ == 0; });
+    }
+    job_mu_.unlock();
+  }
+  void run(size_t T, std::function<void(size_t)> f) {
+    start(T, std::move(f));
+    wait();
+  }
+
+ private:
+  void loop(size_t id) {
+    uint64_t seen = 0;
+    for (;;) {  // (idle workers wait here until the process exits)
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen && id < active_; });
+        seen = gen_;
+      }
+      job_(id);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex job_mu_, mu_;
+  std::condition_variable cv_, done_;
+  std::function<void(size_t)> job_;
+  uint64_t gen_ = 0;
+  size_t active_ = 0, pending_ = 0;
+};
+
 }  // namespace
 
 struct pbft_replica {
@@ -175,6 +240,8 @@ struct pbft_replica {
   bool in_flight = false;
   int in_flight_via = 0;  // 0 GPU context, 1 votes override, 2 SoA override (already complete)
   std::vector<Seg> segs;
+  size_t seg_next = 0;            // segments [0, seg_next) already applied (progressive completion)
+  std::vector<uint8_t> touched;   // per segment: some candidate accepted
   uint64_t rows = 0;
   bool erased_in_flight = false;  // a stable checkpoint erased windows while the batch was in flight
   std::vector<uint64_t> bitmap;
@@ -351,15 +418,19 @@ static void drain(pbft_replica* r, pbft_round_event* events, uint32_t max_events
 }
 
 // Put every in-flight candidate back to pending (the batch failed: nothing was applied).
+static void mark_dirty(pbft_replica* r);
 static void revert_segs(pbft_replica* r) {
-  for (const Seg& g : r->segs) {
+  for (size_t gi = r->seg_next; gi < r->segs.size(); ++gi) {  // (segments applied before the failure stay)
+    const Seg& g = r->segs[gi];
     auto wi = r->windows.find(g.key);
     if (wi == r->windows.end()) continue;
     Phase& p = wi->second.ph[g.kind];
     for (uint32_t i = 0; i < g.count && i < p.size(); ++i)
       if (p.st[i] == V_IN_FLIGHT) { p.st[i] = V_PENDING; ++p.n_pending; }
   }
+  if (r->seg_next) mark_dirty(r);
   r->segs.clear();
+  r->seg_next = 0;
   r->in_flight = false;
   r->erased_in_flight = false;
 }
@@ -405,25 +476,49 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
       const uint32_t* dix = p.dix.data();
       uint32_t* acc = p.acc.data();
       uint8_t* cnt = p.cnt.data();
-      const bool one = p.digs.size() == 1;
-      if (one) amap[0] = p.acc_index(p.digs[0]);
-      for (uint32_t i = 0; i < g.count; ++i) {
-        const uint64_t row = g.row0 + i;
-        const uint32_t s = who[i];
-        if ((bm[row >> 6] >> (row & 63)) & 1) {
-          ++acc_n;
-          const uint32_t d = one ? 0 : dix[i];
-          if (amap[d] < 0) amap[d] = p.acc_index(p.digs[d]);
-          const uint32_t a = (uint32_t)amap[d] + 1;
-          if (acc[s] != a) {
-            if (acc[s]) --p.acc_cnt[acc[s] - 1];
-            acc[s] = a;
-            ++p.acc_cnt[a - 1];
+      uint32_t gone = 0;  // signers left with neither a candidate nor an accepted vote
+      if (p.digs.size() == 1) {
+        // the honest round: one digest -- its accepted-vote count is added once per segment, not per row
+        const uint32_t a = p.acc_index(p.digs[0]) + 1;
+        uint32_t gained = 0;
+        for (uint32_t i = 0; i < g.count; ++i) {
+          const uint64_t row = g.row0 + i;
+          const uint32_t s = who[i];
+          const uint32_t prev = acc[s];
+          if ((bm[row >> 6] >> (row & 63)) & 1) {
+            ++acc_n;
+            if (prev != a) {
+              if (prev) --p.acc_cnt[prev - 1];
+              acc[s] = a;
+              ++gained;
+            }
+            --cnt[s];
+          } else {
+            gone += --cnt[s] == 0 && !prev;
           }
-          st[2] += mism[d];
         }
-        if (--cnt[s] == 0 && !acc[s]) --p.distinct;
+        p.acc_cnt[a - 1] += gained;
+        st[2] += mism[0] ? acc_n : 0;
+      } else {
+        for (uint32_t i = 0; i < g.count; ++i) {
+          const uint64_t row = g.row0 + i;
+          const uint32_t s = who[i];
+          if ((bm[row >> 6] >> (row & 63)) & 1) {
+            ++acc_n;
+            const uint32_t d = dix[i];
+            if (amap[d] < 0) amap[d] = p.acc_index(p.digs[d]);
+            const uint32_t a = (uint32_t)amap[d] + 1;
+            if (acc[s] != a) {
+              if (acc[s]) --p.acc_cnt[acc[s] - 1];
+              acc[s] = a;
+              ++p.acc_cnt[a - 1];
+            }
+            st[2] += mism[d];
+          }
+          gone += --cnt[s] == 0 && !acc[s];
+        }
       }
+      p.distinct -= gone;
     }
     st[0] += acc_n;
     st[1] += g.count - acc_n;
@@ -433,42 +528,67 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
   for (int k = 0; k < 3; ++k) st_out[k] += st[k];
 }
 
-static void apply_segs(pbft_replica* r) {
-  ++r->stats.batches;
-  r->stats.verified += r->rows;
-  const size_t G = r->segs.size();
-  std::vector<uint8_t> touched(G, 0);
+// Threads for the batch fill and the bitmap application of large batches: PBFT_REPLICA_THREADS (default 16,
+// capped by the host; 16 vs 8: 2^20 round 5.3-5.7 vs 5.8-6.2 ms, profiles/r03/ab_threads.txt).
+static size_t host_threads() {
+  static const size_t t = [] {
+    const char* e = getenv("PBFT_REPLICA_THREADS");
+    const long v = e ? strtol(e, nullptr, 10) : 16;
+    return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+  }();
+  return t;
+}
+
+// Apply segments [s0, s1) of the batch (rows all verified); large ranges on several threads, cut at window
+// boundaries (balanced by rows).
+static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
+  if (s1 <= s0) return;
+  const uint64_t lo = r->segs[s0].row0, nrows = r->segs[s1 - 1].row0 + r->segs[s1 - 1].count - lo;
   const unsigned hw = std::thread::hardware_concurrency();
-  const size_t T = r->rows >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, 8), G) : 1;
+  const size_t T = nrows >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), s1 - s0) : 1;
   std::vector<std::array<uint64_t, 3>> st(T, {0, 0, 0});
   if (T <= 1) {
-    apply_range(r, 0, G, st[0].data(), touched.data());
+    apply_range(r, s0, s1, st[0].data(), r->touched.data());
   } else {
-    std::vector<std::thread> th;
-    size_t s0 = 0;
-    for (size_t t = 0; t < T && s0 < G; ++t) {  // balanced by rows, cut at window boundaries
-      const uint64_t hi_row = r->rows * (t + 1) / T;
-      size_t s1 = s0 + 1;
-      while (s1 < G && (t + 1 == T || r->segs[s1].row0 < hi_row || r->segs[s1].key == r->segs[s1 - 1].key)) ++s1;
-      th.emplace_back(apply_range, r, s0, s1, st[t].data(), touched.data());
-      s0 = s1;
+    std::vector<size_t> cut(T + 1, s1);
+    cut[0] = s0;
+    for (size_t t = 0; t < T && cut[t] < s1; ++t) {
+      const uint64_t hi_row = lo + nrows * (t + 1) / T;
+      size_t b = cut[t] + 1;
+      while (b < s1 && (t + 1 == T || r->segs[b].row0 < hi_row || r->segs[b].key == r->segs[b - 1].key)) ++b;
+      cut[t + 1] = b;
     }
-    for (auto& x : th) x.join();
+    WorkerPool::get().run(T, [&](size_t t) {
+      if (cut[t + 1] > cut[t]) apply_range(r, cut[t], cut[t + 1], st[t].data(), r->touched.data());
+    });
   }
   for (const auto& c : st) {
     r->stats.accepted += c[0];
     r->stats.rejected_sig += c[1];
     r->stats.rejected_digest += c[2];
   }
-  for (size_t gi = 0; gi < G; ++gi)  // segments come in window (key) order: O(1) hinted inserts
-    if (touched[gi]) r->dirty.emplace_hint(r->dirty.end(), r->segs[gi].key);
+  r->seg_next = s1;
+}
+
+// the batch is done: its windows with accepted candidates are evaluated next
+static void mark_dirty(pbft_replica* r) {
+  for (size_t gi = 0; gi < r->seg_next; ++gi)  // segments come in window (key) order: O(1) hinted inserts
+    if (r->touched[gi]) r->dirty.emplace_hint(r->dirty.end(), r->segs[gi].key);
+}
+
+static void finish_batch(pbft_replica* r) {
+  apply_segs(r, r->seg_next, r->segs.size());
+  ++r->stats.batches;
+  r->stats.verified += r->rows;
+  mark_dirty(r);
   r->segs.clear();
+  r->seg_next = 0;
   r->in_flight = false;
   r->erased_in_flight = false;
 }
 
 // Copy the candidates of segments [s0, s1) into the batch (pinned staging or the overrides' buffers).
-static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV) {
+static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
     Phase& p = g.w->ph[g.kind];
@@ -479,12 +599,67 @@ static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
     } else {
       for (uint32_t i = 0; i < g.count; ++i) IDX[g.row0 + i] = g.env0 + p.dix[i];
     }
-    for (size_t j = 0; j < p.digs.size(); ++j)
-      pbft_envelope(ENV + PBFT_ENVELOPE_BYTES * (size_t)(g.env0 + j), g.kind, g.key.first, g.key.second,
-                    p.digs[j].data());
     memset(p.st.data(), V_IN_FLIGHT, g.count);
     p.n_pending = 0;
   }
+}
+static void fill_envs(pbft_replica* r, size_t s0, size_t s1, uint8_t* ENV) {
+  for (size_t gi = s0; gi < s1; ++gi) {
+    const Seg& g = r->segs[gi];
+    const Phase& p = g.w->ph[g.kind];
+    for (size_t j = 0; j < p.digs.size(); ++j)
+      pbft_envelope(ENV + PBFT_ENVELOPE_BYTES * (size_t)(g.env0 + j), g.kind, g.key.first, g.key.second,
+                    p.digs[j].data());
+  }
+}
+static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV) {
+  fill_envs(r, s0, s1, ENV);
+  fill_rows(r, s0, s1, SIG, K, IDX);
+}
+
+// rows of one progressive step (the verify library's votes chunk, include/pbft_verify.h)
+static constexpr uint64_t FILL_STEP = 1ull << 18;
+
+// GPU path of a large batch: envelopes, then the rows in FILL_STEP steps on T threads while this thread launches
+// each step as soon as it is filled (pbft_verify_votes_submit_rows): the fill overlaps the copies and kernels.
+static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV,
+                           uint32_t E) {
+  const size_t G = r->segs.size();
+  const uint64_t N = r->rows;
+  fill_envs(r, 0, G, ENV);
+  int rc = pbft_verify_votes_submit_begin(r->ctx, N, E, r->bitmap.data());
+  if (rc) {
+    fill_rows(r, 0, G, SIG, K, IDX);  // (so that revert_segs finds every candidate in flight)
+    return rc;
+  }
+  const size_t W = (size_t)((N + FILL_STEP - 1) / FILL_STEP);
+  std::vector<size_t> cut(W + 1, G);  // step k = segments [cut[k], cut[k+1]): those starting below (k+1) FILL_STEP
+  cut[0] = 0;
+  auto first_at = [&](uint64_t row) {
+    return (size_t)(std::lower_bound(r->segs.begin(), r->segs.end(), row,
+                                     [](const Seg& g, uint64_t x) { return g.row0 < x; }) - r->segs.begin());
+  };
+  for (size_t k = 1; k < W; ++k) cut[k] = first_at(k * FILL_STEP);
+  std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[W]);
+  for (size_t k = 0; k < W; ++k) done[k].store(0, std::memory_order_relaxed);
+  WorkerPool::get().start(T, [&](size_t t) {
+      for (size_t k = 0; k < W; ++k) {
+        const size_t a = cut[k], b = cut[k + 1];
+        if (b > a) {  // part t of the step, balanced by rows
+          const uint64_t lo = r->segs[a].row0, hi = b < G ? r->segs[b].row0 : N;
+          const size_t x = t == 0 ? a : std::max(a, first_at(lo + (hi - lo) * t / T));
+          const size_t y = t + 1 == T ? b : std::min(b, first_at(lo + (hi - lo) * (t + 1) / T));
+          if (y > x) fill_rows(r, x, y, SIG, K, IDX);
+        }
+        done[k].fetch_add(1, std::memory_order_release);
+      }
+  });
+  for (size_t k = 0; k < W && rc == PBFT_OK; ++k) {
+    while (done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    rc = pbft_verify_votes_submit_rows(r->ctx, cut[k + 1] < G ? r->segs[cut[k + 1]].row0 : N);
+  }
+  WorkerPool::get().wait();
+  return rc;
 }
 
 extern "C" {
@@ -699,21 +874,31 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     SIG = st.sig; K = st.key_idx; IDX = st.env_idx; ENV = st.envelopes;
   }
   const size_t G = r->segs.size();
+  r->touched.assign(G, 0);
+  r->seg_next = 0;
   const unsigned hw = std::thread::hardware_concurrency();
-  const size_t T = N >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, 8), G) : 1;
+  const size_t T = N >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), G) : 1;
+  if (T > 1 && !r->verify_fn && !r->vsub) {
+    rc = fill_and_launch(r, T, SIG, K, IDX, ENV, E);
+    r->in_flight_via = 0;
+    if (rc) { revert_segs(r); return rc; }
+    r->in_flight = true;
+    return PBFT_OK;
+  }
   if (T <= 1) {
     fill_segs(r, 0, G, SIG, K, IDX, ENV);
   } else {
-    std::vector<std::thread> th;
-    size_t s0 = 0;
+    std::vector<size_t> cut(T + 1, G);
+    cut[0] = 0;
     for (size_t t = 0; t < T; ++t) {  // balanced by rows
       const uint64_t hi_row = N * (t + 1) / T;
-      size_t s1 = s0;
+      size_t s1 = cut[t];
       while (s1 < G && (t + 1 == T || r->segs[s1].row0 < hi_row)) ++s1;
-      if (s1 > s0) th.emplace_back(fill_segs, r, s0, s1, SIG, K, IDX, ENV);
-      s0 = s1;
+      cut[t + 1] = s1;
     }
-    for (auto& x : th) x.join();
+    WorkerPool::get().run(T, [&](size_t t) {
+      if (cut[t + 1] > cut[t]) fill_segs(r, cut[t], cut[t + 1], SIG, K, IDX, ENV);
+    });
   }
   // 3. launch
   if (r->verify_fn) {  // synchronous per-signature override: R, S columns and one envelope per signature
@@ -747,12 +932,24 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
   if (n_events) *n_events = 0;
   if (r->in_flight) {
     int st = 1;
-    if (r->in_flight_via == 0) st = pbft_verify_poll(r->ctx);
+    uint64_t rows_done = 0;
+    if (r->in_flight_via == 0) st = pbft_verify_poll_rows(r->ctx, &rows_done);
     else if (r->in_flight_via == 1) st = r->vpoll(r->vuser);
-    if (st == 0) return 0;
     if (st < 0) { revert_segs(r); return st; }
     const auto t0 = std::chrono::steady_clock::now();
-    apply_segs(r);
+    if (st == 0) {
+      // a large batch comes back chunk by chunk: apply the segments whose rows are all in while the GPU runs on
+      // (a window's segments stay in order: a prefix of the batch)
+      const size_t G = r->segs.size();
+      if (rows_done >= (r->seg_next < G ? r->segs[r->seg_next].row0 : r->rows) + (1u << 16)) {
+        size_t s1 = r->seg_next;
+        while (s1 < G && r->segs[s1].row0 + r->segs[s1].count <= rows_done) ++s1;
+        apply_segs(r, r->seg_next, s1);
+        r->stats.apply_ns += ns_since(t0);
+      }
+      return 0;
+    }
+    finish_batch(r);
     evaluate(r);
     gc(r);
     r->stats.apply_ns += ns_since(t0);

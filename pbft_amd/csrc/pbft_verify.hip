@@ -20,6 +20,7 @@
 #include <string>
 #include <type_traits>
 #include <vector>
+#include <vector>
 
 #include "../../include/pbft_verify.h"
 #include "../../include/pbft_wire.h"
@@ -170,6 +171,15 @@ struct pbft_ctx {
   uint64_t staged_n = 0;   // pbft_verify_votes_stage: the batch the staging is laid out for
   uint32_t staged_env = 0;
   bool staged = false;
+  // votes batch being launched chunk by chunk (stage_votes_and_launch, pbft_verify_votes_submit_begin / _rows)
+  uint64_t v_n = 0, v_next = 0, v_chunk = 0;  // batch rows, first row not launched, chunks launched
+  uint32_t v_env = 0;
+  size_t v_env_bytes = 0;
+  const uint64_t* v_wk = nullptr;
+  bool v_open = false;      // begun, not every chunk launched
+  bool v_readback = false;  // progressive: each chunk's bitmap words come back on their own (ev_rows)
+  std::vector<hipEvent_t> ev_rows;  // per chunk: its bitmap words are in h_bitmap
+  uint64_t rows_out = 0;            // rows whose bitmap words are in the caller's bitmap
 };
 
 #ifndef PBFT_ENV_SCHED
@@ -477,31 +487,52 @@ struct votes_layout {
 };
 
 // rs_stride 32: R and S are separate [N][32] host columns; 64: R = the [N][64] signature rows, S = R + 32.
-static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K,
-                                  const uint32_t* IDX, const uint8_t* ENV, uint32_t n_env, uint64_t N,
-                                  uint32_t rs_stride = 32) {
+// votes_begin copies the envelope table and launches its schedule; votes_launch then launches every whole chunk
+// inside rows [0, rows) (all the rest once rows >= N): the kernels of chunk c run on the context stream after
+// its copies (copy stream), overlapping the copies of chunk c+1.
+static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t N, bool readback) {
   const uint64_t words = (N + 63) / 64;
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
   const uint64_t ch = N < VOTES_CHUNK ? N : VOTES_CHUNK;
   const votes_layout L(ch);
   int rc = ensure_stage(c, env_bytes + (N > VOTES_CHUNK ? 2 : 1) * L.bytes, words);
   if (rc) return rc;
-  // envelope table first (copy stream), then each chunk's columns; the kernels of chunk c run on the context
-  // stream after its copies, overlapping the copies of chunk c+1
+  if (readback) {
+    const uint64_t chunks = (N + VOTES_CHUNK - 1) / VOTES_CHUNK;
+    while (c->ev_rows.size() < chunks) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      c->ev_rows.push_back(e);
+    }
+  }
   HIP_TRY(hipMemcpyAsync(c->d_stage, ENV, (size_t)PBFT_ENVELOPE_LEN * n_env, hipMemcpyHostToDevice, c->cstream));
   // the envelopes' block-2 schedule on the context stream once the table has landed (ev_copied[0] is
-  // re-recorded by chunk 0 below)
+  // re-recorded by chunk 0)
   HIP_TRY(hipEventRecord(c->ev_copied[0], c->cstream));
   HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[0], 0));
-  const uint64_t* dWK = nullptr;
-  rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &dWK);
+  rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &c->v_wk);
   if (rc) return rc;
-  uint64_t chunk = 0;
-  for (uint64_t lo = 0; lo < N; lo += VOTES_CHUNK, ++chunk) {
+  c->v_n = N;
+  c->v_next = 0;
+  c->v_chunk = 0;
+  c->v_env_bytes = env_bytes;
+  c->v_env = n_env;
+  c->v_open = true;
+  c->v_readback = readback;
+  c->rows_out = 0;
+  return PBFT_OK;
+}
+
+static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* IDX,
+                        uint32_t rs_stride, uint64_t rows) {
+  const uint64_t N = c->v_n;
+  const votes_layout L(N < VOTES_CHUNK ? N : VOTES_CHUNK);
+  while (c->v_next < N && (rows >= N || c->v_next + VOTES_CHUNK <= rows)) {
+    const uint64_t lo = c->v_next;
     const uint64_t n = N - lo < VOTES_CHUNK ? N - lo : VOTES_CHUNK;
-    const int b = (int)(chunk & 1);
-    uint8_t* base = c->d_stage + env_bytes + (size_t)b * L.bytes;
-    if (chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
+    const int b = (int)(c->v_chunk & 1);
+    uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
+    if (c->v_chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
     if (rs_stride == 64) {
       HIP_TRY(hipMemcpyAsync(base, R + 64 * lo, 64 * n, hipMemcpyHostToDevice, c->cstream));
     } else {
@@ -512,13 +543,32 @@ static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* 
     HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream));
     HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream));
     HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
-    rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS, (const uint16_t*)(base + L.offK),
-                       c->d_stage, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream,
-                       rs_stride, 2, nullptr, (const uint32_t*)(base + L.offI), n_env, dWK);
+    const int rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS,
+                                 (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n,
+                                 c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
+                                 (const uint32_t*)(base + L.offI), c->v_env, c->v_wk);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
+    if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
+      HIP_TRY(hipMemcpyAsync(c->h_bitmap + lo / 64, c->d_bitmap + lo / 64, (n + 63) / 64 * 8, hipMemcpyDeviceToHost,
+                             c->stream));
+      HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream));
+    }
+    c->v_next += n;
+    ++c->v_chunk;
   }
+  if (c->v_next >= N) c->v_open = false;
   return PBFT_OK;
+}
+
+static int stage_votes_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K,
+                                  const uint32_t* IDX, const uint8_t* ENV, uint32_t n_env, uint64_t N,
+                                  uint32_t rs_stride = 32) {
+  int rc = votes_begin(c, ENV, n_env, N, false);
+  if (rc) return rc;
+  rc = votes_launch(c, R, S, K, IDX, rs_stride, N);
+  c->v_open = false;
+  return rc;
 }
 
 // The base-point comb table is a constant of the curve: one copy per device,
@@ -638,6 +688,7 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
     if (c->ev_fin[b]) (void)hipEventDestroy(c->ev_fin[b]);
   }
   if (c->ev_comb) (void)hipEventDestroy(c->ev_comb);
+  for (hipEvent_t e : c->ev_rows) (void)hipEventDestroy(e);
   if (c->cstream) { (void)hipStreamSynchronize(c->cstream); (void)hipStreamDestroy(c->cstream); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -760,6 +811,7 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipEventRecord(c->ev_done, c->stream));
   c->in_flight = true;
+  c->v_readback = false;
   c->async_out = out;
   c->async_words = words;
   return PBFT_OK;
@@ -768,6 +820,7 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
 static int finish_async(pbft_ctx* c) {
   memcpy(c->async_out, c->h_bitmap, c->async_words * 8);
   c->in_flight = false;
+  c->rows_out = c->async_words * 64;
   // (only with timing events: on events never recorded the call fails and would leave an error that the next
   // launch's hipGetLastError reports; a failure here is cleared for the same reason)
   if (c->timing && hipEventElapsedTime(&c->last_ms, c->ev0, c->ev1) != hipSuccess) (void)hipGetLastError();
@@ -777,6 +830,7 @@ static int finish_async(pbft_ctx* c) {
 int pbft_verify_poll(pbft_ctx* c) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight) return 1;
+  if (c->v_open) return 0;  // progressive batch: not every chunk launched yet
   hipError_t e = hipEventQuery(c->ev_done);
   if (e == hipErrorNotReady) return 0;
   if (e != hipSuccess) {
@@ -790,6 +844,7 @@ int pbft_verify_poll(pbft_ctx* c) {
 int pbft_verify_wait(pbft_ctx* c) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight) return PBFT_OK;
+  if (c->v_open) return set_err(PBFT_EBUSY, "progressive votes batch not fully submitted");
   const hipError_t e = hipEventSynchronize(c->ev_done);
   if (e != hipSuccess) {
     c->in_flight = false;
@@ -807,6 +862,7 @@ static int votes_submit_from(pbft_ctx* c, const uint8_t* R, const uint8_t* S, co
   HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipEventRecord(c->ev_done, c->stream));
   c->in_flight = true;
+  c->v_readback = false;
   c->async_out = out;
   c->async_words = words;
   return PBFT_OK;
@@ -845,6 +901,70 @@ int pbft_verify_votes_submit(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* 
   uint8_t* h = c->h_stage;
   return votes_submit_from(c, h, h + 32, (const uint16_t*)(h + L.offK), (const uint32_t*)(h + L.offI), h + L.offE,
                            n_env, N, out, 64);
+}
+
+// Progressive form: the caller fills the staging front to back and launches as it goes.
+int pbft_verify_votes_submit_begin(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (!c->staged || N != c->staged_n || n_env != c->staged_env)
+    return set_err(PBFT_EINVAL, "pbft_verify_votes_stage was not called for this batch");
+  if (N == 0 || !out) return set_err(PBFT_EINVAL, "empty batch or null bitmap");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  c->staged = false;
+  HIP_TRY(hipSetDevice(c->device));
+  const host_votes_layout L(N, n_env);
+  int rc = votes_begin(c, c->h_stage + L.offE, n_env, N, true);
+  if (rc) return rc;
+  c->in_flight = true;  // (pbft_verify_poll reports "running" until every chunk is launched and done)
+  c->async_out = out;
+  c->async_words = (N + 63) / 64;
+  return PBFT_OK;
+}
+
+int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (!c->in_flight || !c->v_open) return set_err(PBFT_EINVAL, "no progressive votes batch open");
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t N = c->v_n;
+  const host_votes_layout L(N, c->v_env);
+  uint8_t* h = c->h_stage;
+  int rc = votes_launch(c, h, h + 32, (const uint16_t*)(h + L.offK), (const uint32_t*)(h + L.offI), 64, rows);
+  if (rc == PBFT_OK && !c->v_open)
+    rc = hipEventRecord(c->ev_done, c->stream) == hipSuccess ? PBFT_OK : set_err(PBFT_EHIP, "event record");
+  if (rc) {  // the batch is lost: drain what was launched, the context stays usable
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamSynchronize(c->cstream);
+    c->in_flight = false;
+    c->v_open = false;
+  }
+  return rc;
+}
+
+int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight && c->v_readback) {
+    while (c->rows_out < c->v_next) {  // launched chunks whose bitmap words have landed, in order
+      const hipError_t e = hipEventQuery(c->ev_rows[c->rows_out / VOTES_CHUNK]);
+      if (e == hipErrorNotReady) break;
+      if (e != hipSuccess) {
+        c->in_flight = false;
+        c->v_open = false;
+        HIP_TRY(e);
+      }
+      const uint64_t hi = c->rows_out + VOTES_CHUNK < c->v_n ? c->rows_out + VOTES_CHUNK : c->v_n;
+      memcpy(c->async_out + c->rows_out / 64, c->h_bitmap + c->rows_out / 64, (hi - c->rows_out + 63) / 64 * 8);
+      c->rows_out = hi;
+    }
+    if (c->v_open || c->rows_out < c->v_n) {
+      if (rows_done) *rows_done = c->rows_out;
+      return 0;
+    }
+  }
+  const bool progressive = c->in_flight && c->v_readback;
+  const int st = pbft_verify_poll(c);
+  if (rows_done) *rows_done = st == 1 ? c->rows_out : progressive ? c->rows_out : 0;
+  return st;
 }
 
 int pbft_verify_votes_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* I,

@@ -43,10 +43,82 @@ int pbft_verify_batch(pbft_ctx*, const uint8_t*, const uint8_t*, const uint16_t*
 int pbft_digest_blake2b512(pbft_ctx*, const uint8_t*, const uint64_t*, const uint32_t*, uint64_t, uint8_t*) {
   return PBFT_ENODEV;
 }
-int pbft_verify_votes_stage(pbft_ctx*, uint64_t, uint32_t, pbft_votes_staging*) { return PBFT_ENODEV; }
-int pbft_verify_votes_submit(pbft_ctx*, uint64_t, uint32_t, uint64_t*) { return PBFT_ENODEV; }
-int pbft_verify_poll(pbft_ctx*) { return PBFT_ENODEV; }
-int pbft_verify_wait(pbft_ctx*) { return PBFT_ENODEV; }
+}
+
+// A fake GPU context for the replica's progressive votes path (pbft_verify_votes_stage / _submit_begin / _rows /
+// pbft_verify_poll_rows): exactly-sized staging, key_idx pre-set to a sentinel so that a chunk launched before
+// its rows were filled is caught, and one 2^18-row chunk "completing" per poll.  A row verifies iff its
+// signature's first byte is not 0xEE (no curve arithmetic: the point is the host's threads and bookkeeping).
+struct FakeGpu {
+  std::vector<uint8_t> sig, env;
+  std::vector<uint16_t> K;
+  std::vector<uint32_t> I;
+  uint64_t N = 0, launched = 0, done = 0;
+  uint32_t n_env = 0, n_keys = 0;
+  uint64_t* out = nullptr;
+  bool staged = false, open = false, in_flight = false;
+  uint64_t batches = 0, chunk_launches = 0;
+};
+static constexpr uint64_t FAKE_CHUNK = 1ull << 18;
+
+extern "C" {
+int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_staging* st) {
+  FakeGpu* g = (FakeGpu*)c;
+  if (!g) return PBFT_ENODEV;
+  CHECK(!g->in_flight);
+  g->sig.assign(64 * N, 0);
+  g->K.assign(N, 0xFFFF);
+  g->I.assign(N, 0);
+  g->env.assign((size_t)PBFT_ENVELOPE_BYTES * n_env, 0);
+  st->sig = g->sig.data(); st->key_idx = g->K.data(); st->env_idx = g->I.data(); st->envelopes = g->env.data();
+  g->N = N; g->n_env = n_env; g->staged = true;
+  return 0;
+}
+int pbft_verify_votes_submit_begin(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && g->staged && N == g->N && n_env == g->n_env && out);
+  for (uint32_t e = 0; e < n_env; ++e) CHECK(memcmp(&g->env[(size_t)PBFT_ENVELOPE_BYTES * e], "PBFT", 4) == 0);
+  g->staged = false; g->open = true; g->in_flight = true; g->out = out; g->launched = g->done = 0;
+  ++g->batches;
+  return 0;
+}
+int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && g->open);
+  const uint64_t upto = rows >= g->N ? g->N : rows / FAKE_CHUNK * FAKE_CHUNK;
+  for (uint64_t i = g->launched; i < upto; ++i) CHECK(g->K[i] != 0xFFFF && g->I[i] < g->n_env);  // filled
+  if (upto > g->launched) { g->launched = upto; ++g->chunk_launches; }
+  if (g->launched == g->N) g->open = false;
+  return 0;
+}
+int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
+  FakeGpu* g = (FakeGpu*)c;
+  if (!g->in_flight) { *rows_done = g->N; return 1; }
+  if (g->done < g->launched) {  // one more chunk "lands"
+    const uint64_t hi = g->done + FAKE_CHUNK < g->launched ? g->done + FAKE_CHUNK : g->launched;
+    for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
+    for (uint64_t i = g->done; i < hi; ++i)
+      if (g->sig[64 * i] != 0xEE && g->K[i] < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
+    g->done = hi;
+  }
+  *rows_done = g->done;
+  if (g->open || g->done < g->N) return 0;
+  g->in_flight = false;
+  return 1;
+}
+int pbft_verify_votes_submit(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
+  int rc = pbft_verify_votes_submit_begin(c, N, n_env, out);
+  return rc ? rc : pbft_verify_votes_submit_rows(c, N);
+}
+int pbft_verify_poll(pbft_ctx* c) {
+  uint64_t r;
+  return pbft_verify_poll_rows(c, &r);
+}
+int pbft_verify_wait(pbft_ctx* c) {
+  uint64_t r;
+  while (pbft_verify_poll_rows(c, &r) == 0) {}
+  return 0;
+}
 }
 
 using PL = plan<40, 6, 14>;  // balanced 7/6-bit windows, incl. take_last (as the GPU plans)
@@ -491,6 +563,59 @@ static void test_replica_async(const Keys& k) {
   printf("replica async: %llu batches, %d commits\n", (unsigned long long)u.batches, committed);
 }
 
+// ---- 5. a large round through the GPU path (fake context above): the multithreaded fill launching chunk by
+// chunk, and the application of each chunk's rows while later chunks are "running" ------------------------------
+static void test_replica_progressive() {
+  const uint32_t n = 256, seqs = 1100;  // 2 x 256 x 1100 + 1100 = 564,300 rows: 3 chunks
+  std::vector<uint8_t> keys(32 * (size_t)n);
+  for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = (uint8_t)(i >> 8); }
+  FakeGpu g;
+  g.n_keys = n;
+  pbft_replica* r = nullptr;
+  CHECK(pbft_replica_create((pbft_ctx*)&g, n, 0, keys.data(), &r) == 0);
+  pbft_replica_set_digest_fn(r, host_digest, nullptr);
+  pbft_replica_set_log_window(r, 4096);
+  const char op[] = "testOperation";
+  uint8_t d[64];
+  digest_padded(d, (const uint8_t*)op, strlen(op));
+  uint8_t sg[64] = {1};
+  for (uint32_t q = 1; q <= seqs; ++q)
+    CHECK(pbft_replica_on_pre_prepare(r, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+  uint64_t bad = 0, pushed = 0;
+  for (uint32_t q = 1; q <= seqs; ++q)
+    for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})
+      for (uint32_t i = 0; i < n; ++i) {
+        // seq 7: 100 forged Prepares (no prepare quorum); seq 900 (third chunk): 90 forged Commits; + scattered
+        const bool forged = (q == 7 && kind == PBFT_KIND_PREPARE && i >= 2 && i < 102) ||
+                            (q == 900 && kind == PBFT_KIND_COMMIT && i < 90) || (pushed % 997 == 5);
+        sg[0] = forged ? 0xEE : 1;
+        sg[1] = (uint8_t)i;
+        bad += forged;
+        ++pushed;
+        CHECK(pbft_replica_push(r, kind, 1, q, d, i, sg) == 1);
+      }
+  uint64_t rows = 0;
+  CHECK(pbft_replica_flush_submit(r, 0, &rows) == 0 && rows == pushed + seqs);
+  CHECK(g.chunk_launches >= 2);  // launched in steps, not in one go
+  std::vector<pbft_round_event> ev(4 * seqs);
+  uint32_t ne = 0;
+  int polls = 0, st;
+  while ((st = pbft_replica_flush_poll(r, ev.data(), (uint32_t)ev.size(), &ne)) == 0) ++polls;
+  CHECK(st == 1 && polls >= 2);
+  uint32_t prepared = 0, committed = 0;
+  for (uint32_t e = 0; e < ne; ++e) {
+    if (ev[e].kind == PBFT_EVENT_PREPARED) { ++prepared; CHECK(ev[e].seq != 7); }
+    if (ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL) { ++committed; CHECK(ev[e].seq != 7 && ev[e].seq != 900); }
+  }
+  CHECK(prepared == seqs - 1 && committed == seqs - 2);
+  pbft_replica_stats s;
+  pbft_replica_get_stats(r, &s);
+  CHECK(s.rejected_sig == bad && s.accepted == pushed + seqs - bad && s.batches == 1);
+  pbft_replica_destroy(r);
+  printf("replica progressive: %llu rows in %llu launch steps, %d polls, %u commits\n", (unsigned long long)rows,
+         (unsigned long long)g.chunk_launches, polls, committed);
+}
+
 int main() {
   std::mt19937_64 rng(0x5EED);
   Keys k = make_keys(4, rng);
@@ -498,6 +623,7 @@ int main() {
   test_wire(rng);
   test_replica(k, rng);
   test_replica_async(k);
+  test_replica_progressive();
   printf("sanitized host run ok\n");
   return 0;
 }

@@ -602,6 +602,59 @@ def test_async_host_forms_pinned_staging(gv, coracle):
     gv.wait(t)
 
 
+def test_progressive_votes_submit(gv, coracle):
+    """pbft_verify_votes_submit_begin / _rows + pbft_verify_poll_rows (what pbft_replica_flush_submit and
+    _flush_poll use): the staging is launched chunk by chunk as it is filled, each chunk's bitmap words come back
+    on their own; until the last rows are submitted the batch reads "running" and a blocking wait is refused.
+    2^19 + 3 rows = chunks of 2^18, 2^18 and 3; every prefix reported done equals the oracle."""
+    import ctypes
+    from pbft_amd import PbftError, bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=47)   # 65,536 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(47)
+    R, S, K, M, _ = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R, S, K, M, 85)
+    env, inv = np.unique(M, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    N = (1 << 19) + 3
+    reps = N // len(R) + 1
+    RR, SS, KK, II, EE = (np.concatenate([a] * reps)[:N] for a in (R, S, K, ei, exp))
+    L, ctx = gv._lib, gv._ctx
+    st = gv.stage_votes(N, len(env))
+    st["envelopes"][:] = env
+    out = np.zeros((N + 63) // 64, np.uint64)
+    rows_done = ctypes.c_uint64()
+    # the first chunk's rows only
+    h = 1 << 18
+    st["sig"][:h, :32], st["sig"][:h, 32:], st["key_idx"][:h], st["env_idx"][:h] = RR[:h], SS[:h], KK[:h], II[:h]
+    assert L.pbft_verify_votes_submit_begin(ctx, N, len(env), out.ctypes.data) == 0
+    assert L.pbft_verify_votes_submit_rows(ctx, 1000) == 0                # no whole chunk yet
+    assert L.pbft_verify_votes_submit_rows(ctx, h + 5) == 0               # chunk 0
+    assert L.pbft_verify_poll(ctx) == 0
+    with pytest.raises(PbftError):
+        from pbft_amd._lib import check
+        check(L.pbft_verify_wait(ctx))
+    seen = 0
+    while seen < h:
+        assert L.pbft_verify_poll_rows(ctx, ctypes.byref(rows_done)) == 0
+        assert rows_done.value in (0, h)
+        seen = rows_done.value
+    assert (bitmap_to_bool(out[: h // 64], h) == EE[:h]).all()
+    st["sig"][h:, :32], st["sig"][h:, 32:], st["key_idx"][h:], st["env_idx"][h:] = RR[h:], SS[h:], KK[h:], II[h:]
+    assert L.pbft_verify_votes_submit_rows(ctx, N) == 0
+    prev = h
+    while True:
+        rc = L.pbft_verify_poll_rows(ctx, ctypes.byref(rows_done))
+        assert rc in (0, 1) and rows_done.value >= prev
+        prev = rows_done.value
+        assert (bitmap_to_bool(out[: min(prev, N) // 64], min(prev, N) // 64 * 64) == EE[: min(prev, N) // 64 * 64]).all()
+        if rc == 1:
+            break
+    assert prev >= N and (bitmap_to_bool(out, N) == EE).all()
+    # a second, one-shot batch on the same context is unaffected (no chunk read-back)
+    assert (bitmap_to_bool(gv.verify_votes(R, S, K, ei, env), len(R)) == exp).all()
+
+
 def test_multi_gpu_rccl_allgather_one_rank(gv, coracle):
     """pbft_multi_create / pbft_verify_batch_device_multi on the one GPU of this box: a
     1-rank RCCL communicator, the shard verified into its slice of the padded rank-major bitmap, then
