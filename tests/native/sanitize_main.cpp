@@ -600,17 +600,25 @@ static void test_replica_progressive() {
   std::vector<pbft_round_event> ev(4 * seqs);
   uint32_t ne = 0;
   int polls = 0, st;
+  // the first chunk lands and is applied while the rest "runs"; then a stable checkpoint erases seqs 1..10 (their
+  // rows still in flight or already applied) and a late vote arrives for an in-flight window
+  CHECK(pbft_replica_flush_poll(r, ev.data(), (uint32_t)ev.size(), &ne) == 0 && ne == 0);
+  CHECK(pbft_replica_stable_checkpoint(r, 10) == 0);
+  sg[0] = 1;
+  sg[1] = 0x77;
+  CHECK(pbft_replica_push(r, PBFT_KIND_COMMIT, 1, 1000, d, 3, sg) == 1);
   while ((st = pbft_replica_flush_poll(r, ev.data(), (uint32_t)ev.size(), &ne)) == 0) ++polls;
-  CHECK(st == 1 && polls >= 2);
+  CHECK(st == 1 && polls >= 1);
   uint32_t prepared = 0, committed = 0;
   for (uint32_t e = 0; e < ne; ++e) {
-    if (ev[e].kind == PBFT_EVENT_PREPARED) { ++prepared; CHECK(ev[e].seq != 7); }
-    if (ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL) { ++committed; CHECK(ev[e].seq != 7 && ev[e].seq != 900); }
+    CHECK(ev[e].seq > 10);
+    if (ev[e].kind == PBFT_EVENT_PREPARED) ++prepared;
+    if (ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL) { ++committed; CHECK(ev[e].seq != 900); }
   }
-  CHECK(prepared == seqs - 1 && committed == seqs - 2);
+  CHECK(prepared == seqs - 10 && committed == seqs - 11);
   pbft_replica_stats s;
   pbft_replica_get_stats(r, &s);
-  CHECK(s.rejected_sig == bad && s.accepted == pushed + seqs - bad && s.batches == 1);
+  CHECK(s.batches == 1 && s.accepted + s.rejected_sig <= pushed + seqs);
   pbft_replica_destroy(r);
   printf("replica progressive: %llu rows in %llu launch steps, %d polls, %u commits\n", (unsigned long long)rows,
          (unsigned long long)g.chunk_launches, polls, committed);
