@@ -358,7 +358,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
         rep = ctypes.c_void_p()
         assert L.pbft_replica_create(v._ctx, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
         for q in range(n_seq):
-            assert L.pbft_replica_on_pre_prepare(rep, 1, q + 1, ops[q], len(ops[q]), digs[2 * n_rep * q].tobytes(),
+            assert L.pbft_replica_on_pre_prepare(rep, primary, 1, q + 1, ops[q], len(ops[q]), digs[2 * n_rep * q].tobytes(),
                                                  pR[q].tobytes() + pS[q].tobytes(), None) == 1
         qd = ctypes.c_uint64()
         t = time.perf_counter()

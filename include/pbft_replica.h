@@ -50,7 +50,8 @@
  *   - at most one batch is in flight per replica; pushes during the flight are
  *     queued (a duplicate of an in-flight candidate is a duplicate) and go into
  *     the next batch;
- *   - a PrePrepare frame is taken only from the primary's own connection;
+ *   - a PrePrepare is taken only from the primary's own connection (frames and
+ *     pbft_replica_on_pre_prepare alike: both take the authenticated peer);
  *   - events are decided when a batch is applied, whether or not the caller's
  *     event buffer has room: undelivered events wait in the replica's queue for
  *     the next flush / flush_poll, and GC never waits for delivery;
@@ -149,14 +150,21 @@ void pbft_envelope(uint8_t out[PBFT_ENVELOPE_BYTES], uint8_t kind, uint64_t view
                    const uint8_t digest[64]);
 
 /* A PrePrepare for (view, seq) carrying the client operation bytes and the
- * primary's signature (R || S over the kind-0 envelope of the claimed digest).
- * Recomputes the Blake2b-512 digest (GPU, or the digest override); returns 1 if
- * queued for signature verification (PBFT_EVENT_PRE_PREPARED at the flush that
- * accepts it), 0 if dropped (digest mismatch / wrong view / out of window /
- * conflicting digest already accepted for (view, seq)).  digest_out (optional)
- * receives the recomputed digest. */
-int pbft_replica_on_pre_prepare(pbft_replica *r, uint64_t view, uint64_t seq, const uint8_t *op, uint32_t op_len,
-                                const uint8_t claimed_digest[64], const uint8_t primary_sig[64],
+ * primary's signature (R || S over the kind-0 envelope of the claimed digest),
+ * received from replica `peer_idx` -- the AUTHENTICATED sender (the connection's
+ * peer, pbft_replica_peer_index; inject_node_event's peer_id, src/behavior.rs:304,
+ * PrePrepare arm :310-318), never a field of the message.  Unless peer_idx is the
+ * view's primary the PrePrepare is dropped before any work (counted in
+ * rejected_signer): a backup relaying junk PrePrepares cannot fill the window's
+ * PBFT_MAX_CANDIDATES slots ahead of the primary's real one.  Recomputes the
+ * Blake2b-512 digest (GPU, or the digest override); returns 1 if queued for
+ * signature verification (PBFT_EVENT_PRE_PREPARED at the flush that accepts it),
+ * 0 if dropped (not from the primary / digest mismatch / wrong view / out of
+ * window / conflicting digest already accepted for (view, seq)).  digest_out
+ * (optional) receives the recomputed digest (left untouched when the sender is
+ * rejected). */
+int pbft_replica_on_pre_prepare(pbft_replica *r, uint32_t peer_idx, uint64_t view, uint64_t seq, const uint8_t *op,
+                                uint32_t op_len, const uint8_t claimed_digest[64], const uint8_t primary_sig[64],
                                 uint8_t digest_out[64]);
 
 /* A signed Prepare/Commit from replica `signer` (sig = R || S).  `signer` must be

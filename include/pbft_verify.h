@@ -126,7 +126,9 @@ int pbft_verify_votes_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, c
                             uint64_t *bitmap_out);
 /* Zero-copy votes form: pbft_verify_votes_stage returns the context's pinned host staging for a batch of N
  * signatures over n_env envelopes -- sig[N][64] (the 64-byte signature R || S as it travels), key_idx[N],
- * env_idx[N], envelopes[n_env][85]; valid until the next stage call -- the caller fills it in place and
+ * env_idx[N], envelopes[n_env][85]; valid until the next call on this context that uses the staging (another
+ * stage, or any host-buffer submit: pageable inputs are copied there, and a bigger batch reallocates it; such a
+ * call also voids the stage, so a later pbft_verify_votes_submit fails with PBFT_EINVAL) -- the caller fills it in place and
  * pbft_verify_votes_submit launches it asynchronously (DMA straight from the staging, the kernels read R and S
  * at a 64-byte stride).  This is what pbft_replica_flush_submit uses. */
 typedef struct {

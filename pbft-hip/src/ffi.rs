@@ -194,8 +194,8 @@ extern "C" {
     pub fn pbft_replica_set_digest_fn(r: *mut pbft_replica, f: pbft_digest_fn, user: *mut c_void) -> c_int;
     pub fn pbft_replica_set_log_window(r: *mut pbft_replica, log_window: u64) -> c_int;
     pub fn pbft_envelope(out: *mut u8, kind: u8, view: u64, seq: u64, digest: *const u8);
-    pub fn pbft_replica_on_pre_prepare(r: *mut pbft_replica, view: u64, seq: u64, op: *const u8, op_len: u32,
-                                       claimed_digest: *const u8, primary_sig: *const u8,
+    pub fn pbft_replica_on_pre_prepare(r: *mut pbft_replica, peer_idx: u32, view: u64, seq: u64, op: *const u8,
+                                       op_len: u32, claimed_digest: *const u8, primary_sig: *const u8,
                                        digest_out: *mut u8) -> c_int;
     pub fn pbft_replica_push(r: *mut pbft_replica, kind: u8, view: u64, seq: u64, digest: *const u8, signer: u32,
                              sig: *const u8) -> c_int;

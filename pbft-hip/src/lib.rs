@@ -19,6 +19,7 @@
 //! point used here is exercised through ctypes by tests/ (CPU) and tests/ -m gpu (MI355X).
 use std::ffi::CStr;
 use std::fmt;
+use std::marker::PhantomData;
 use std::os::raw::{c_int, c_void};
 use std::ptr;
 
@@ -103,8 +104,17 @@ impl VotesBatch {
     pub fn is_empty(&self) -> bool {
         self.r.is_empty()
     }
+    /// Err(PBFT_EINVAL) unless `s`, `key_idx` and `env_idx` have one entry per signature (`r`).
+    pub fn check_columns(&self) -> Result<()> {
+        let n = self.r.len();
+        if self.s.len() != n || self.key_idx.len() != n || self.env_idx.len() != n {
+            return Err(Error { code: ffi::PBFT_EINVAL, message: "VotesBatch: column lengths differ".into() });
+        }
+        Ok(())
+    }
     /// The per-signature form (every signature carrying its own envelope), for verifiers without a votes form.
-    pub fn to_sig_batch(&self) -> SigBatch {
+    pub fn to_sig_batch(&self) -> Result<SigBatch> {
+        self.check_columns()?;
         let mut b = SigBatch::default();
         for i in 0..self.len() {
             let e = self.envelopes.get(self.env_idx[i] as usize).copied().unwrap_or([0u8; ffi::PBFT_ENVELOPE_BYTES]);
@@ -115,7 +125,7 @@ impl VotesBatch {
             let k = if (self.env_idx[i] as usize) < self.envelopes.len() { self.key_idx[i] } else { u16::MAX };
             b.push(k, e, &sig);
         }
-        b
+        Ok(b)
     }
 }
 
@@ -182,6 +192,7 @@ impl GpuVerifier {
         if self.inflight.is_some() {
             return Err(Error { code: ffi::PBFT_EBUSY, message: "one batch in flight per context".into() });
         }
+        batch.check_columns()?; // the C side reads n entries of every column
         let n = batch.len();
         let mut out = Bitmap::zeros(n);
         check(unsafe {
@@ -372,11 +383,16 @@ pub enum RoundEvent {
     CommittedLocal { view: u64, seq: u64 },
 }
 
-/// The round batcher + quorum state machine of one replica (include/pbft_replica.h).
-pub struct Replica {
+/// The round batcher + quorum state machine of one replica (include/pbft_replica.h).  It borrows the
+/// `GpuVerifier` whose context it submits to (`'a`): the context must outlive the replica, whose Drop may
+/// still wait on a batch in flight there.
+pub struct Replica<'a> {
     raw: *mut ffi::pbft_replica,
     // a Rust BatchVerifier installed as the replica's asynchronous votes verifier (None: the GPU context)
     verifier: Option<Box<Backend>>,
+    // event buffer reused by every flush_poll / flush (the event loop polls ~1,500 times per 2^20 round)
+    events: Vec<ffi::pbft_round_event>,
+    _gpu: PhantomData<&'a GpuVerifier>,
 }
 
 // A BatchVerifier behind the replica's submit / poll callbacks (pbft_replica_set_votes_verifier).
@@ -404,7 +420,11 @@ extern "C" fn votes_submit_trampoline(user: *mut c_void, sig: *const u8, key_idx
         vb.env_idx.extend_from_slice(std::slice::from_raw_parts(env_idx, n));
         vb.envelopes.extend_from_slice(std::slice::from_raw_parts(envelopes as *const Envelope, n_env as usize));
     }
-    match b.v.submit(vb.to_sig_batch()) {
+    let batch = match vb.to_sig_batch() {
+        Ok(batch) => batch,
+        Err(e) => return e.code,
+    };
+    match b.v.submit(batch) {
         Ok(t) => {
             b.pending = Some((t, bitmap_out, (n + 63) / 64));
             0
@@ -441,16 +461,16 @@ fn round_events(ev: &[ffi::pbft_round_event]) -> Vec<RoundEvent> {
     }).collect()
 }
 
-impl Replica {
+impl<'a> Replica<'a> {
     /// `gpu`: the context whose key set is `keys` (pbft_verify_set_keys); replica ids are
     /// positions in `keys` (network.json's "nodes" order); f = (n - 1) / 3.
-    pub fn new(gpu: Option<&GpuVerifier>, self_id: u32, keys: &[[u8; 32]]) -> Result<Self> {
+    pub fn new(gpu: Option<&'a GpuVerifier>, self_id: u32, keys: &[[u8; 32]]) -> Result<Self> {
         let mut raw = ptr::null_mut();
         let ctx = gpu.map(|g| g.raw()).unwrap_or(ptr::null_mut());
         check(unsafe {
             ffi::pbft_replica_create(ctx, keys.len() as u32, self_id, keys.as_ptr() as *const u8, &mut raw)
         })?;
-        Ok(Replica { raw, verifier: None })
+        Ok(Replica { raw, verifier: None, events: vec![ffi::pbft_round_event::default(); 4096], _gpu: PhantomData })
     }
     /// Back the batcher with any BatchVerifier (e.g. CpuVerifier) instead of the GPU context; its
     /// submit / poll become the replica's flush_submit / flush_poll.
@@ -463,11 +483,13 @@ impl Replica {
         self.verifier = Some(boxed);
         Ok(())
     }
-    /// PrePrepare ingress (validate_pre_prepare, src/behavior.rs:126-157, plus the signature TODO :127).
-    pub fn on_pre_prepare(&mut self, view: u64, seq: u64, operation: &[u8], digest: &[u8; 64],
+    /// PrePrepare ingress (validate_pre_prepare, src/behavior.rs:126-157, plus the signature TODO :127) from
+    /// replica `peer` -- the AUTHENTICATED connection's replica index (`peer_index` of inject_node_event's
+    /// peer_id, src/behavior.rs:304); dropped unless it is the view's primary.
+    pub fn on_pre_prepare(&mut self, peer: u32, view: u64, seq: u64, operation: &[u8], digest: &[u8; 64],
                           primary_sig: &[u8; 64]) -> Result<bool> {
         let rc = check(unsafe {
-            ffi::pbft_replica_on_pre_prepare(self.raw, view, seq, operation.as_ptr(), operation.len() as u32,
+            ffi::pbft_replica_on_pre_prepare(self.raw, peer, view, seq, operation.as_ptr(), operation.len() as u32,
                                              digest.as_ptr(), primary_sig.as_ptr(), ptr::null_mut())
         })?;
         Ok(rc == 1)
@@ -515,20 +537,23 @@ impl Replica {
     /// Call from NetworkBehaviour::poll (src/behavior.rs:416-426): None while the GPU works, else the round
     /// events decided by the finished batch (and any still queued).
     pub fn flush_poll(&mut self) -> Result<Option<Vec<RoundEvent>>> {
-        let mut ev = vec![ffi::pbft_round_event::default(); 4096];
         let mut n = 0u32;
-        let rc = check(unsafe { ffi::pbft_replica_flush_poll(self.raw, ev.as_mut_ptr(), ev.len() as u32, &mut n) })?;
+        let rc = check(unsafe {
+            ffi::pbft_replica_flush_poll(self.raw, self.events.as_mut_ptr(), self.events.len() as u32, &mut n)
+        })?;
         if rc == 0 {
             return Ok(None);
         }
-        Ok(Some(round_events(&ev[..n as usize])))
+        Ok(Some(round_events(&self.events[..n as usize])))
     }
     /// Blocking: verify every ready sub-window in one batch and report new round events.
     pub fn flush(&mut self, force: bool) -> Result<Vec<RoundEvent>> {
-        let mut ev = vec![ffi::pbft_round_event::default(); 4096];
         let mut n = 0u32;
-        check(unsafe { ffi::pbft_replica_flush(self.raw, force as c_int, ev.as_mut_ptr(), ev.len() as u32, &mut n) })?;
-        Ok(round_events(&ev[..n as usize]))
+        check(unsafe {
+            ffi::pbft_replica_flush(self.raw, force as c_int, self.events.as_mut_ptr(), self.events.len() as u32,
+                                    &mut n)
+        })?;
+        Ok(round_events(&self.events[..n as usize]))
     }
     /// The replica index of an authenticated connection's PeerId (None: not a replica).
     pub fn peer_index(&self, peer_id: &[u8]) -> Option<u32> {
@@ -545,7 +570,7 @@ impl Replica {
     }
 }
 
-impl Drop for Replica {
+impl Drop for Replica<'_> {
     fn drop(&mut self) {
         // destroy completes a batch in flight (through the installed verifier) before `verifier` is dropped
         unsafe { ffi::pbft_replica_destroy(self.raw) };
@@ -553,18 +578,20 @@ impl Drop for Replica {
 }
 
 /// Several GPUs of this process with the round's bitmap words all-gathered on RCCL
-/// (pbft_multi_create / pbft_verify_batch_device_multi).
-pub struct MultiGpu {
+/// (pbft_multi_create / pbft_verify_batch_device_multi).  Borrows its `GpuVerifier`s (`'a`):
+/// their contexts must outlive it (Drop synchronises their streams).
+pub struct MultiGpu<'a> {
     raw: *mut ffi::pbft_multi,
+    _gpus: PhantomData<&'a GpuVerifier>,
 }
 
-impl MultiGpu {
+impl<'a> MultiGpu<'a> {
     /// One context per device, in rank order.
-    pub fn new(gpus: &[&GpuVerifier]) -> Result<Self> {
+    pub fn new(gpus: &[&'a GpuVerifier]) -> Result<Self> {
         let ctxs: Vec<*mut ffi::pbft_ctx> = gpus.iter().map(|g| g.raw()).collect();
         let mut raw = ptr::null_mut();
         check(unsafe { ffi::pbft_multi_create(ctxs.as_ptr(), ctxs.len() as u32, &mut raw) })?;
-        Ok(MultiGpu { raw })
+        Ok(MultiGpu { raw, _gpus: PhantomData })
     }
     /// Enqueue: rank r verifies its device-resident shard; every rank's `d_bitmap[r]` then holds the round
     /// (rank-major, `words_per_rank` words per rank).  # Safety: device pointers as in include/pbft_verify.h.
@@ -581,7 +608,7 @@ impl MultiGpu {
     }
 }
 
-impl Drop for MultiGpu {
+impl Drop for MultiGpu<'_> {
     fn drop(&mut self) {
         unsafe { ffi::pbft_multi_destroy(self.raw) };
     }

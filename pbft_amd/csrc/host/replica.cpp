@@ -16,10 +16,7 @@
 // launch, return) and pbft_replica_flush_poll (apply the bitmap, emit events) so
 // that the loop never blocks on the GPU.
 #include <algorithm>
-#ifdef PBFT_REPLICA_TIMING
 #include <chrono>
-#include <cstdio>
-#endif
 #include <array>
 #include <atomic>
 #include <cstdlib>
@@ -33,6 +30,7 @@
 #include <functional>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -163,6 +161,20 @@ class WorkerPool {
   }
   // run f(0) .. f(T - 1) on T workers; returns at once (wait() joins the round)
   void start(size_t T, std::function<void(size_t)> f) {
+    if (pid_ != getpid()) {
+      // a fork()ed child inherits the vector but none of the threads (and maybe locked mutexes): start over
+      // with fresh state.  The parent's std::thread objects are leaked, not destroyed (destroying a joinable
+      // one terminates, and their handles name threads that do not exist in this process).
+      new std::vector<std::thread>(std::move(th_));
+      th_ = std::vector<std::thread>();
+      new (&job_mu_) std::mutex();
+      new (&mu_) std::mutex();
+      new (&cv_) std::condition_variable();
+      new (&done_) std::condition_variable();
+      gen_ = 0;
+      active_ = pending_ = 0;
+      pid_ = getpid();
+    }
     job_mu_.lock();
     while (th_.size() < T) {
       const size_t id = th_.size();
@@ -209,6 +221,7 @@ class WorkerPool {
   std::function<void(size_t)> job_;
   uint64_t gen_ = 0;
   size_t active_ = 0, pending_ = 0;
+  pid_t pid_ = getpid();  // the process whose threads th_ holds
 };
 
 }  // namespace
@@ -729,11 +742,18 @@ int pbft_replica_set_log_window(pbft_replica* r, uint64_t log_window) {
 }
 
 // validate_pre_prepare (src/behavior.rs:126-157) + State::insert_pre_prepare (src/state.rs:40-47);
-// the signature (TODO :127) is checked by the next flush, batched with the votes.
-int pbft_replica_on_pre_prepare(pbft_replica* r, uint64_t view, uint64_t seq, const uint8_t* op, uint32_t op_len,
-                                const uint8_t claimed_digest[64], const uint8_t primary_sig[64],
+// the signature (TODO :127) is checked by the next flush, batched with the votes.  peer_idx is the
+// authenticated sender (inject_node_event's peer_id, src/behavior.rs:304, arm :310-318): only the view's
+// primary may fill a window's PrePrepare candidate slots, so a relaying backup cannot crowd out the real one.
+int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t view, uint64_t seq, const uint8_t* op,
+                                uint32_t op_len, const uint8_t claimed_digest[64], const uint8_t primary_sig[64],
                                 uint8_t digest_out[64]) {
   if (!r || (!op && op_len) || !claimed_digest || !primary_sig) return PBFT_EINVAL;
+  if (peer_idx != primary_of(r, view)) {  // checked before the digest: a backup's relay costs no hashing
+    ++r->stats.pushed;
+    ++r->stats.rejected_signer;
+    return 0;
+  }
   uint8_t d[64];
   int rc;
   if (r->digest_fn) {
@@ -1021,10 +1041,10 @@ int pbft_replica_push_frames(pbft_replica* r, uint32_t peer_idx, const uint8_t* 
       // only on the primary's own connection (the reference receives it from the primary, src/behavior.rs:89-95):
       // a relayed PrePrepare could otherwise fill the window's candidate slots ahead of the real one
       const uint32_t p = r->n ? primary_of(r, m.view) : 0;
-      if (r->n == 0 || m.replica != p || peer_idx != p) ++r->stats.rejected_signer;
-      else
-        got = pbft_replica_on_pre_prepare(r, m.view, m.seq, (const uint8_t*)m.operation, m.operation_len, m.digest,
-                                          m.sig, nullptr);
+      if (r->n == 0 || m.replica != p) ++r->stats.rejected_signer;
+      else  // (on_pre_prepare rejects a connection that is not the primary's)
+        got = pbft_replica_on_pre_prepare(r, peer_idx, m.view, m.seq, (const uint8_t*)m.operation, m.operation_len,
+                                          m.digest, m.sig, nullptr);
     }
     if (got < 0) { rc = got; break; }
     if (got == 1) ++np; else ++nd;

@@ -187,7 +187,10 @@ struct pbft_ctx {
 #endif
 
 // Pinned host staging (grow-only: hipHostMalloc costs milliseconds).  Never while a batch is in flight.
+// Every user of the staging calls this first: whatever pbft_verify_votes_stage handed out is void from here on
+// (a later pbft_verify_votes_submit must not launch what another path wrote there).
 static int ensure_host_stage(pbft_ctx* c, size_t bytes) {
+  c->staged = false;
   if (bytes <= c->h_stage_cap) return PBFT_OK;
   if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
   c->h_stage = nullptr;
@@ -397,6 +400,8 @@ struct stage_layout {
 #ifndef PBFT_VOTES_CHUNK_LOG2
 #define PBFT_VOTES_CHUNK_LOG2 18
 #endif
+// chunks own whole 64-bit bitmap words (the kernels write d_bitmap + lo / 64, readbacks copy (n + 63) / 64 words)
+static_assert(PBFT_PIPE_CHUNK_LOG2 >= 6 && PBFT_VOTES_CHUNK_LOG2 >= 6, "chunks must be multiples of 64 rows");
 static constexpr uint64_t PIPE_CHUNK = 1ull << PBFT_PIPE_CHUNK_LOG2;
 // the votes form moves 70 B per signature instead of 151: its copies are about as long as the kernels, so a
 // smaller chunk shortens the pipeline's fill and drain (PBFT_VOTES_CHUNK_LOG2)

@@ -86,6 +86,8 @@ class MultiGpu:
     def __init__(self, verifiers):
         self._lib = load()
         self._m = ctypes.c_void_p()
+        # the contexts must outlive the communicator (destroy synchronises their streams): hold the verifiers
+        self._verifiers = list(verifiers)
         arr = (ctypes.c_void_p * len(verifiers))(*[v._ctx.value for v in verifiers])
         check(self._lib.pbft_multi_create(arr, len(verifiers), ctypes.byref(self._m)))
         self.n = len(verifiers)
@@ -104,6 +106,13 @@ class MultiGpu:
         if self._m:
             self._lib.pbft_multi_destroy(self._m)
             self._m = ctypes.c_void_p()
+        self._verifiers = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class GpuBatchVerifier:
@@ -216,7 +225,9 @@ class GpuBatchVerifier:
 
     def stage_votes(self, n: int, n_env: int) -> dict:
         """pbft_verify_votes_stage: numpy views of the context's pinned staging for an (n, n_env) votes batch
-        (sig rows R || S, key_idx, env_idx, envelopes), to be filled in place and launched by submit_staged."""
+        (sig rows R || S, key_idx, env_idx, envelopes), to be filled in place and launched by submit_staged.
+        The views are valid only until the next call on this context that uses the staging (another stage_votes,
+        or any host-buffer submit / verify): do not touch them afterwards."""
         st = VotesStaging()
         check(self._lib.pbft_verify_votes_stage(self._ctx, n, n_env, ctypes.byref(st)))
 

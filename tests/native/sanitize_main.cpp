@@ -389,8 +389,8 @@ static void test_replica(const Keys& k, std::mt19937_64& rng) {
     uint8_t ps[64];
     env_sign(k, primary, PBFT_KIND_PREPREPARE, 1, (uint64_t)q, d, ps);
     for (int i = 0; i < n; ++i)
-      CHECK(pbft_replica_on_pre_prepare(reps[i], 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d, ps,
-                                        nullptr) == 1);
+      CHECK(pbft_replica_on_pre_prepare(reps[i], primary, 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d,
+                                        ps, nullptr) == 1);
   }
   std::vector<std::vector<std::tuple<uint8_t, uint64_t, int, std::array<uint8_t, 64>>>> inbox(n);
   int committed = 0;
@@ -518,7 +518,10 @@ static void test_replica_async(const Keys& k) {
   for (int q = 1; q <= S; ++q) {
     uint8_t ps[64];
     env_sign(k, primary, PBFT_KIND_PREPREPARE, 1, (uint64_t)q, d, ps);
-    CHECK(pbft_replica_on_pre_prepare(r, 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d, ps, nullptr) == 1);
+    CHECK(pbft_replica_on_pre_prepare(r, primary, 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d, ps,
+                                      nullptr) == 1);
+    CHECK(pbft_replica_on_pre_prepare(r, 2, 1, (uint64_t)q, (const uint8_t*)op, (uint32_t)strlen(op), d, ps,
+                                      nullptr) == 0);  // relayed by a backup: dropped at the door
     for (int i = 0; i < n; ++i) {
       env_sign(k, i, PBFT_KIND_PREPARE, 1, (uint64_t)q, d, prep[q * n + i].data());
       env_sign(k, i, PBFT_KIND_COMMIT, 1, (uint64_t)q, d, com[q * n + i].data());
@@ -580,7 +583,7 @@ static void test_replica_progressive() {
   digest_padded(d, (const uint8_t*)op, strlen(op));
   uint8_t sg[64] = {1};
   for (uint32_t q = 1; q <= seqs; ++q)
-    CHECK(pbft_replica_on_pre_prepare(r, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+    CHECK(pbft_replica_on_pre_prepare(r, 1, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
   uint64_t bad = 0, pushed = 0;
   for (uint32_t q = 1; q <= seqs; ++q)
     for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})

@@ -44,7 +44,7 @@ def lib():
     L.pbft_replica_destroy.argtypes = [vp]
     L.pbft_replica_set_verifier.argtypes = [vp, VERIFY_FN, vp]
     L.pbft_replica_set_digest_fn.argtypes = [vp, DIGEST_FN, vp]
-    L.pbft_replica_on_pre_prepare.argtypes = [vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
+    L.pbft_replica_on_pre_prepare.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
                                               ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
     L.pbft_replica_push_frames.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, vp, vp, vp]
     L.pbft_replica_set_log_window.argtypes = [vp, ctypes.c_uint64]
@@ -216,12 +216,15 @@ class Cluster:
     def primary(self, view=1):
         return view % self.n
 
-    def pre_prepare(self, i, view, seq, op, digest=None, sig=None):
-        """Deliver the primary's signed PrePrepare for (view, seq) to replica i."""
+    def pre_prepare(self, i, view, seq, op, digest=None, sig=None, peer=None):
+        """Deliver the primary's signed PrePrepare for (view, seq) to replica i over the connection of replica
+        `peer` (default: the view's primary, its legitimate sender)."""
         d = hashlib.blake2b(op, digest_size=64).digest() if digest is None else digest
         if sig is None:
             sig = self.sign(self.primary(view), KIND_PREPREPARE, view, seq, d)
-        return self.L.pbft_replica_on_pre_prepare(self.reps[i], view, seq, op, len(op), d, sig, None)
+        if peer is None:
+            peer = self.primary(view)
+        return self.L.pbft_replica_on_pre_prepare(self.reps[i], peer, view, seq, op, len(op), d, sig, None)
 
     def stats(self, i):
         s = Stats()

@@ -70,6 +70,28 @@ def test_gpu_forged_pre_prepare_rejected_by_the_kernels(gpu_cluster):
     c.close()
 
 
+def test_gpu_relayed_pre_prepares_do_not_crowd_out_the_primary(gpu_cluster):
+    """VERDICT r03 item 1 on the GPU: a backup relays 4 forged PrePrepares for seq 1 through
+    pbft_replica_on_pre_prepare (its authenticated peer index), then the primary's real one arrives; the relays are
+    dropped at the door, and the real one is verified by the kernels and reaches PRE_PREPARED with
+    dropped_flood == 0 (the GPU Blake2b computes the digest)."""
+    from test_replica import D, OP
+    from replica_sim import EV_PRE_PREPARED, KIND_PREPREPARE
+    v = gpu_cluster
+    c = Cluster(4, ctx=v._ctx, use_oracle_verifier=False, tag=23)
+    assert v.set_keys(np.frombuffer(c.keys, dtype=np.uint8)).all()
+    for k in range(4):
+        forged = bytearray(c.sign(c.primary(), KIND_PREPREPARE, 1, 1, D))
+        forged[33 + k] ^= 1
+        assert c.pre_prepare(0, 1, 1, OP, sig=bytes(forged), peer=3) == 0
+    assert c.pre_prepare(0, 1, 1, OP) == 1
+    assert c.flush_async(0) == [(1, 1, EV_PRE_PREPARED)]
+    st = c.stats(0)
+    assert st["dropped_flood"] == 0 and st["rejected_signer"] == 4 and st["rejected_sig"] == 0
+    assert st["verified"] == 1 and st["accepted"] == 1
+    c.close()
+
+
 def test_gpu_phase_ordered_rounds_async_flush(gpu_cluster):
     """The phase-ordered simulation with every flush non-blocking (flush_submit + flush_poll) on the GPU."""
     v = gpu_cluster
@@ -127,7 +149,7 @@ def test_gpu_replica_2p20_round(gpu_cluster):
     assert L.pbft_replica_set_digest_fn(rep, dfn, None) == 0
     for q in range(1, seqs + 1):
         op = b"op-" + str(q).encode()
-        assert L.pbft_replica_on_pre_prepare(rep, 1, q, op, len(op), dig[q - 1].tobytes(),
+        assert L.pbft_replica_on_pre_prepare(rep, 1, 1, q, op, len(op), dig[q - 1].tobytes(),
                                              (pR[q - 1].tobytes() + pS[q - 1].tobytes()), None) == 1
     view = np.ones(N, np.uint64)
     digs = np.ascontiguousarray(dig[seq.astype(np.int64) - 1])

@@ -86,10 +86,14 @@ def test_validation_rules():
     L = c.L
     bad = hashlib.blake2b(b"nope", digest_size=64).digest()
     psig = c.sign(c.primary(), KIND_PREPREPARE, 1, 5, D)
-    assert L.pbft_replica_on_pre_prepare(r0, 1, 5, OP, len(OP), bad, psig, None) == 0   # digest mismatch
-    assert L.pbft_replica_on_pre_prepare(r0, 2, 5, OP, len(OP), D, psig, None) == 0     # wrong view
-    assert L.pbft_replica_on_pre_prepare(r0, 1, 5, OP, len(OP), D, psig, None) == 1
-    assert L.pbft_replica_on_pre_prepare(r0, 1, 5, OP, len(OP), D, psig, None) == 0     # duplicate
+    P = c.primary()
+    assert L.pbft_replica_on_pre_prepare(r0, P, 1, 5, OP, len(OP), bad, psig, None) == 0   # digest mismatch
+    assert L.pbft_replica_on_pre_prepare(r0, 2, 2, 5, OP, len(OP), D, psig, None) == 0     # wrong view (its primary)
+    assert c.stats(0)["rejected_view"] == 1
+    assert L.pbft_replica_on_pre_prepare(r0, 2, 1, 5, OP, len(OP), D, psig, None) == 0     # not from the primary
+    assert c.stats(0)["rejected_signer"] == 1
+    assert L.pbft_replica_on_pre_prepare(r0, P, 1, 5, OP, len(OP), D, psig, None) == 1
+    assert L.pbft_replica_on_pre_prepare(r0, P, 1, 5, OP, len(OP), D, psig, None) == 0     # duplicate
     sig = c.sign(2, KIND_PREPARE, 1, 5, D)
     assert L.pbft_replica_push(r0, KIND_PREPARE, 1, 5, D, 2, sig) == 1
     assert L.pbft_replica_push(r0, KIND_PREPARE, 1, 5, D, 2, sig) == 0                  # duplicate
@@ -102,6 +106,43 @@ def test_validation_rules():
     # a second backup's Prepare completes 2f: the sub-window closes on its own count
     assert L.pbft_replica_push(r0, KIND_PREPARE, 1, 5, D, 3, c.sign(3, KIND_PREPARE, 1, 5, D)) == 1
     assert c.flush(0) == [(1, 5, EV_PREPARED)]
+    c.close()
+
+
+@pytest.mark.parametrize("relay_first", [True, False])
+def test_relayed_pre_prepares_cannot_fill_the_primarys_slots(relay_first):
+    """a backup relays PBFT_MAX_CANDIDATES (4) junk PrePrepares for a predictable seq through
+    pbft_replica_on_pre_prepare (the reference dispatcher's PrePrepare arm with its peer_id, src/behavior.rs:304,
+    :310-318); they are dropped at the door (rejected_signer), so the primary's real one -- before or after them --
+    is queued, verified and reaches PRE_PREPARED with dropped_flood == 0."""
+    c = Cluster(4)
+    r0 = c.reps[0]
+    backup = 2
+    assert backup != c.primary()
+    junk = [bytes([k]) * 64 for k in range(1, 5)]
+    if not relay_first:
+        assert c.pre_prepare(0, 1, 7, OP) == 1
+    for j in junk:
+        assert c.pre_prepare(0, 1, 7, OP, sig=j, peer=backup) == 0
+    # the backup may even relay the primary's VALID PrePrepare: still not its connection's to deliver
+    assert c.pre_prepare(0, 1, 7, OP, peer=backup) == 0
+    if relay_first:
+        assert c.pre_prepare(0, 1, 7, OP) == 1
+    assert c.flush(0) == [(1, 7, EV_PRE_PREPARED)]
+    st = c.stats(0)
+    assert st["dropped_flood"] == 0 and st["rejected_signer"] == 5 and st["rejected_sig"] == 0 and st["verified"] == 1
+    c.close()
+
+
+def test_primary_own_pre_prepare_slots_bounded():
+    """The flood bound still holds on the primary's own connection (a faulty primary): 4 candidates, the rest
+    dropped_flood."""
+    c = Cluster(4)
+    for k in range(1, 7):
+        c.pre_prepare(0, 1, 9, OP, sig=bytes([k]) * 64)
+    st = c.stats(0)
+    assert st["dropped_flood"] == 2 and st["rejected_signer"] == 0
+    assert c.flush(0) == [] and c.stats(0)["rejected_sig"] == 4
     c.close()
 
 

@@ -95,7 +95,7 @@ def test_flush_submit_of_a_2p20_round_returns_before_poll_reports_done():
         sig[1:9] = q.to_bytes(8, "little")
         sig[9:11] = primary.to_bytes(2, "little")
         op = b"op-" + str(q).encode()
-        assert L.pbft_replica_on_pre_prepare(rep, 1, q, op, len(op), digests[q], bytes(sig), None) == 1
+        assert L.pbft_replica_on_pre_prepare(rep, primary, 1, q, op, len(op), digests[q], bytes(sig), None) == 1
     # 2^20 votes, in (seq, kind, signer) order, as columns for pbft_replica_push_many
     N = seqs * 2 * n
     seq = np.repeat(np.arange(1, seqs + 1, dtype=np.uint64), 2 * n)
