@@ -141,7 +141,7 @@ def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
 
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
-    same command, tools/gpu_pmc_cur.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
+    same command, tools/gpu_prof.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
     for rel in ("r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
         p = os.path.join(ROOT, "profiles", rel, "derived.json")
         try:
@@ -421,11 +421,41 @@ def plan_legs(v, pub, d, n, stream, torch):
         t = time.perf_counter()
         assert v.set_keys(pub).all()
         ms_keys = (time.perf_counter() - t) * 1e3
+        ks = v.key_stats()
         pb, pa = v.positions()
         time_device(v, stream, d, n, 3, torch)
         k, w = time_device(v, stream, d, n, 20, torch)
         out[name] = {"positions": [pb, pa], "steps": pb + pa, "set_keys_ms": ms_keys, "kernel_ms": k,
-                     "verifies_per_s": n / (k * 1e-3), "key_tables_gb": per_key.get(pa, 0) * len(pub) / 1e9}
+                     "verifies_per_s": n / (k * 1e-3), "key_tables_gb": per_key.get(pa, 0) * len(pub) / 1e9,
+                     "phases_ms": {x: round(ks[x + "_ms"], 2) for x in ("free", "alloc", "build", "meminfo")},
+                     "reused_allocation": bool(ks["reused"])}
+    return out
+
+
+def rekey_legs(v, pub, d, n, stream, torch, expect):
+    """a re-key of the SAME n = 256 set (same plan: the table allocation is kept and rebuilt in
+    place) and the replacement of ONE replica's key (pbft_verify_update_keys: only its tables are rebuilt, as when
+    a peer is admitted later -- the reference's add_peer, src/behavior.rs:45-61); the round's bitmap is checked
+    after each."""
+    from pbft_amd import bitmap_to_bool
+    out = {}
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    assert v.set_keys(pub).all()
+    out["rekey_ms"] = (time.perf_counter() - t) * 1e3
+    ks = v.key_stats()
+    out["rekey_phases_ms"] = {x: round(ks[x + "_ms"], 2) for x in ("free", "alloc", "build", "meminfo")}
+    out["rekey_reused_allocation"] = bool(ks["reused"])
+    times = []
+    for slot in (17, 200, 17):
+        t = time.perf_counter()
+        assert v.update_keys([slot], pub[slot:slot + 1]).all()
+        times.append((time.perf_counter() - t) * 1e3)
+    out["update_one_key_ms"] = float(np.median(times))
+    out["update_one_key_ms_all"] = times
+    time_device(v, stream, d, n, 2, torch)
+    got = bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), n)
+    assert (got == expect[:n]).all(), "bitmap after re-key / update differs"
     return out
 
 
@@ -539,6 +569,8 @@ def main():
     t_keys = time.perf_counter()
     key_ok = v.set_keys(pub)
     set_keys_ms = (time.perf_counter() - t_keys) * 1e3  # n = 256: decompression, small-order check, comb tables
+    ks0 = v.key_stats()
+    set_keys_phases = {x: round(ks0[x + "_ms"], 2) for x in ("free", "alloc", "build", "meminfo")}
     assert key_ok.all()
     pb, pa = v.positions()  # the key plan set_keys chose for this key set
 
@@ -711,6 +743,8 @@ def main():
         extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect)
         extras["shuffled_2^20"] = shuffled_leg(v, d, n, stream, torch, dev, expect)
         extras["set_keys_ms"] = set_keys_ms
+        extras["set_keys_phases_ms"] = set_keys_phases
+        extras.update(rekey_legs(v, pub, d, n, stream, torch, expect))
         extras["key_plans_2^20"] = plan_legs(v, pub, d, n, stream, torch)
 
     if rank == 0:

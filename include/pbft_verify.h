@@ -58,8 +58,36 @@ int pbft_verify_ctx_destroy(pbft_ctx *ctx);
 /* Install the replica key set A[n][32] (n <= 65535).  Decompresses every key,
  * rejects small-order keys, and builds each key's -A comb table in HBM.
  * key_ok (optional, n bytes): 1 = key usable, 0 = every signature under it
- * rejects (bad encoding or small order).  Replaces any previous key set. */
+ * rejects (bad encoding or small order).  Replaces any previous key set.
+ * A re-key with the same comb plan and at most as many keys as the current
+ * set's allocation reuses that allocation (tables rebuilt in place; no HBM
+ * freed or allocated) unless a clone shares the set; a plan change frees the
+ * old tables first.  The context is busy (blocking call) throughout. */
 int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *key_ok);
+
+/* Replace m keys of the installed set: key idx[i] (< n, distinct) becomes
+ * A[i][32]; only those m keys' tables are rebuilt (the reference admits peers
+ * one at a time: Pbft::add_peer src/behavior.rs:45-61, fed by mDNS discovery
+ * src/network_behaviour_composer.rs:24-33 -- a replica slot can be installed
+ * with a placeholder key, key_ok 0, and filled here when its peer appears).
+ * key_ok (optional, m bytes) as for set_keys.  The set is updated in place for
+ * every context sharing it (pbft_verify_ctx_clone): no batch may be in flight
+ * on any of them (the call synchronises the device first). */
+int pbft_verify_update_keys(pbft_ctx *ctx, const uint32_t *idx, const uint8_t *A, uint32_t m, uint8_t *key_ok);
+
+/* Phases of the last pbft_verify_set_keys / pbft_verify_update_keys on this
+ * context (host wall time, ms). */
+typedef struct {
+  double total_ms;
+  double meminfo_ms;     /* hipMemGetInfo (plan selection)                         */
+  double free_ms;        /* releasing the previous key tables (hipFree)            */
+  double alloc_ms;       /* allocating the new ones (hipMalloc)                    */
+  double build_ms;       /* key upload + decompression + comb-table kernels + sync */
+  uint32_t keys_built;   /* keys whose tables were (re)built                       */
+  uint32_t reused;       /* 1: the existing table allocation was kept              */
+  uint64_t table_bytes;  /* HBM held by the key tables                             */
+} pbft_key_stats;
+int pbft_verify_key_stats(pbft_ctx *ctx, pbft_key_stats *out);
 
 /* A second context on the same device that shares the parent's base-point
  * table and its CURRENT key set (reference-counted; a later set_keys on either

@@ -84,6 +84,20 @@ pub struct pbft_replica_stats {
     pub apply_ns: u64,
 }
 
+/// Phases of the last pbft_verify_set_keys / pbft_verify_update_keys (host wall time, ms).
+#[repr(C)]
+#[derive(Clone, Copy, Debug, Default)]
+pub struct pbft_key_stats {
+    pub total_ms: f64,
+    pub meminfo_ms: f64,
+    pub free_ms: f64,
+    pub alloc_ms: f64,
+    pub build_ms: f64,
+    pub keys_built: u32,
+    pub reused: u32,
+    pub table_bytes: u64,
+}
+
 #[repr(C)]
 pub struct pbft_wire_msg {
     pub kind: u32,
@@ -131,6 +145,9 @@ extern "C" {
     pub fn pbft_verify_ctx_create(device: c_int, out: *mut *mut pbft_ctx) -> c_int;
     pub fn pbft_verify_ctx_destroy(ctx: *mut pbft_ctx) -> c_int;
     pub fn pbft_verify_set_keys(ctx: *mut pbft_ctx, a: *const u8, n: u32, key_ok: *mut u8) -> c_int;
+    pub fn pbft_verify_update_keys(ctx: *mut pbft_ctx, idx: *const u32, a: *const u8, m: u32,
+                                   key_ok: *mut u8) -> c_int;
+    pub fn pbft_verify_key_stats(ctx: *mut pbft_ctx, out: *mut pbft_key_stats) -> c_int;
     pub fn pbft_verify_ctx_clone(parent: *mut pbft_ctx, out: *mut *mut pbft_ctx) -> c_int;
     pub fn pbft_verify_batch(ctx: *mut pbft_ctx, r: *const u8, s: *const u8, key_idx: *const u16, msg: *const u8,
                              msg_len: u32, msg_stride: u32, n: u64, bitmap_out: *mut u64) -> c_int;

@@ -211,6 +211,26 @@ impl GpuVerifier {
         check(unsafe { ffi::pbft_verify_ctx_clone(self.ctx, &mut ctx) })?;
         Ok(GpuVerifier { ctx, inflight: None, next: 0 })
     }
+    /// Replace keys `idx[i]` of the installed set by `keys[i]` in place (only their tables are rebuilt): a peer
+    /// admitted later (Pbft::add_peer, src/behavior.rs:45-61) fills the slot its replica id reserves.
+    /// Returns key_ok of the new keys.
+    pub fn update_keys(&mut self, idx: &[u32], keys: &[[u8; 32]]) -> Result<Vec<bool>> {
+        if idx.len() != keys.len() {
+            return Err(Error { code: ffi::PBFT_EINVAL, message: "update_keys: idx and keys lengths differ".into() });
+        }
+        let mut ok = vec![0u8; keys.len()];
+        check(unsafe {
+            ffi::pbft_verify_update_keys(self.ctx, idx.as_ptr(), keys.as_ptr() as *const u8, keys.len() as u32,
+                                         ok.as_mut_ptr())
+        })?;
+        Ok(ok.into_iter().map(|b| b == 1).collect())
+    }
+    /// Where the last set_keys / update_keys spent its time.
+    pub fn key_stats(&self) -> ffi::pbft_key_stats {
+        let mut s = ffi::pbft_key_stats::default();
+        unsafe { ffi::pbft_verify_key_stats(self.ctx, &mut s) };
+        s
+    }
     pub fn set_option(&mut self, option: i32, value: u64) -> Result<()> {
         check(unsafe { ffi::pbft_verify_set_option(self.ctx, option, value) }).map(|_| ())
     }

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("PBFT_VERIFY_LIB") or os.path.join(_HERE, "libpbft_ver
 # every symbol include/pbft_verify.h declares
 EXPORTS = (
     "pbft_verify_ctx_create", "pbft_verify_ctx_destroy", "pbft_verify_ctx_clone", "pbft_verify_set_keys",
+    "pbft_verify_update_keys", "pbft_verify_key_stats",
     "pbft_verify_batch", "pbft_verify_batch_multi", "pbft_verify_batch_async", "pbft_verify_poll", "pbft_verify_wait",
     "pbft_verify_batch_device", "pbft_verify_reserve", "pbft_digest_blake2b512", "pbft_digest_sha256",
     "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms", "pbft_verify_ctx_info",
@@ -64,6 +65,8 @@ def load() -> ctypes.CDLL:
         "pbft_verify_ctx_destroy": (i32, [vp]),
         "pbft_verify_ctx_clone": (i32, [vp, ctypes.POINTER(vp)]),
         "pbft_verify_set_keys": (i32, [vp, u8p, u32, u8p]),
+        "pbft_verify_update_keys": (i32, [vp, vp, u8p, u32, u8p]),
+        "pbft_verify_key_stats": (i32, [vp, vp]),
         "pbft_verify_batch": (i32, [vp, u8p, u8p, vp, u8p, u32, u32, u64, vp]),
         "pbft_verify_batch_async": (i32, [vp, u8p, u8p, vp, u8p, u32, u32, u64, vp]),
         "pbft_verify_batch_multi": (i32, [vp, u32, u8p, u8p, vp, u8p, u32, u32, u64, vp]),

@@ -15,11 +15,12 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <type_traits>
-#include <vector>
 #include <vector>
 
 #include "../../include/pbft_verify.h"
@@ -105,8 +106,15 @@ struct keyset {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n = 0;
+  uint32_t cap = 0;  // keys the buffers hold (a later set_keys of <= cap keys with the same plan reuses them)
   int pa = 0;  // positions of the key plan (identifies PLA_HUGE / PLA_BIG / PLA_MID / PLA_SMALL)
 };
+static size_t plan_table_words(int pa) {
+  return pa == PLA_HUGE::P ? PLA_HUGE::TABLE_WORDS
+       : pa == PLA_BIG::P  ? PLA_BIG::TABLE_WORDS
+       : pa == PLA_MID::P  ? PLA_MID::TABLE_WORDS
+                           : PLA_SMALL::TABLE_WORDS;
+}
 static void keyset_release(keyset* k) {
   if (k && --k->refs == 0) {
     (void)hipFree(k->d_tabA); (void)hipFree(k->d_keys); (void)hipFree(k->d_key_ok);
@@ -132,6 +140,7 @@ struct pbft_ctx {
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
+  pbft_key_stats kstats{};             // the last pbft_verify_set_keys / _update_keys (pbft_verify_key_stats)
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
@@ -700,48 +709,72 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   return PBFT_OK;
 }
 
+static double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// Install a key set.  Where the time of a re-key went: freeing and re-allocating the 69-172 GB
+// of key tables took seconds on MI355X (the table build itself ~0.25 s), so a key set of at most the current
+// capacity with the same plan is rebuilt IN PLACE -- no hipFree, no hipMalloc -- when this context alone holds it;
+// pbft_verify_key_stats reports the phases of the last call.
 int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key_ok) {
   if (!c || (!A && n)) return set_err(PBFT_EINVAL, "null argument");
   if (n == 0 || n > 65535) return set_err(PBFT_EINVAL, "key count must be 1..65535");
   if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  const auto t_all = std::chrono::steady_clock::now();
+  pbft_key_stats ks{};
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  c->adopt(nullptr);
-  // The widest key window whose tables fit the budget (PBFT_KEY_TABLE_BUDGET_MB, default 96 GiB of the
-  // 288 GB HBM) and the free memory: 18-bit (252 MB/key, <= 390 keys by default), 16-bit (67 MB/key), else
-  // 8-bit (0.5 MB/key).  Entry indices are 32-bit (n * P * E < 2^32).
+  // this context's key set, if no clone shares it: its tables may be overwritten in place
+  keyset* own = (c->ks && c->ks->refs.load() == 1) ? c->ks : nullptr;
+  const size_t own_bytes = own ? plan_table_words(own->pa) * 4 * (size_t)own->cap : 0;
+  // The widest key plan whose tables fit the budget (PBFT_OPT_KEY_TABLE_BUDGET_MB / env, default 70 % of the HBM
+  // free once the old key set is gone: ~180 GB on a 288-GB MI355X after the 30-GB base-point table) and the free
+  // memory.  Entry indices are 32-bit (n * entries per key < 2^32).
+  auto t = std::chrono::steady_clock::now();
   size_t free_b = 0, total_b = 0;
   HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-  // default budget: 70 % of the HBM still free (after the 30-GB base-point table: ~180 GB on a 288-GB MI355X)
-  size_t budget_mb = free_b / 1048576 * 7 / 10;
+  ks.meminfo_ms = ms_since(t);
+  const size_t avail = free_b + own_bytes;  // (a key set shared with clones stays allocated for them)
+  size_t budget_mb = avail / 1048576 * 7 / 10;
   if (const char* e = getenv("PBFT_KEY_TABLE_BUDGET_MB")) budget_mb = strtoull(e, nullptr, 10);
   if (c->key_budget_mb) budget_mb = c->key_budget_mb;
   auto fits = [&](size_t table_words, uint64_t entries_per_key) {
     const size_t bytes = table_words * 4 * (size_t)n;
     return (uint64_t)n * entries_per_key < (1ull << 32) && bytes <= budget_mb * (size_t)1048576 &&
-           bytes + ((size_t)4 << 30) < free_b;
+           bytes + ((size_t)4 << 30) < avail;
   };
   int pa = PLA_SMALL::P;
-  size_t tab_words = PLA_SMALL::TABLE_WORDS;
-  if (fits(PLA_HUGE::TABLE_WORDS, PLA_HUGE::ENTRIES)) {
-    pa = PLA_HUGE::P;
-    tab_words = PLA_HUGE::TABLE_WORDS;
-  } else if (fits(PLA_BIG::TABLE_WORDS, PLA_BIG::ENTRIES)) {
-    pa = PLA_BIG::P;
-    tab_words = PLA_BIG::TABLE_WORDS;
-  } else if (fits(PLA_MID::TABLE_WORDS, PLA_MID::ENTRIES)) {
-    pa = PLA_MID::P;
-    tab_words = PLA_MID::TABLE_WORDS;
+  if (fits(PLA_HUGE::TABLE_WORDS, PLA_HUGE::ENTRIES)) pa = PLA_HUGE::P;
+  else if (fits(PLA_BIG::TABLE_WORDS, PLA_BIG::ENTRIES)) pa = PLA_BIG::P;
+  else if (fits(PLA_MID::TABLE_WORDS, PLA_MID::ENTRIES)) pa = PLA_MID::P;
+  const size_t tab_words = plan_table_words(pa);
+  keyset* k = nullptr;
+  if (own && own->pa == pa && n <= own->cap) {
+    // same plan, fits the allocation: rebuild in place.  Launches on callers' streams (device forms) may still
+    // read the old tables.
+    k = own;
+    ks.reused = 1;
+    HIP_TRY(hipDeviceSynchronize());
+  } else {
+    t = std::chrono::steady_clock::now();
+    c->adopt(nullptr);  // (hipFree of an own key set: the slow part of a plan change)
+    ks.free_ms = ms_since(t);
+    t = std::chrono::steady_clock::now();
+    k = new keyset();
+    k->pa = pa;
+    k->cap = n;
+    if (hipMalloc(&k->d_tabA, tab_words * 4 * (size_t)n) != hipSuccess ||
+        hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess || hipMalloc(&k->d_key_ok, n) != hipSuccess) {
+      (void)hipGetLastError();
+      keyset_release(k);
+      c->kstats = ks;
+      return set_err(PBFT_ENOMEM, "key table alloc");
+    }
+    ks.alloc_ms = ms_since(t);
   }
-  const size_t tab_bytes = tab_words * 4 * (size_t)n;
-  keyset* k = new keyset();
-  k->pa = pa;
   k->n = n;
-  if (hipMalloc(&k->d_tabA, tab_bytes) != hipSuccess || hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess ||
-      hipMalloc(&k->d_key_ok, n) != hipSuccess) {
-    keyset_release(k);
-    return set_err(PBFT_ENOMEM, "key table alloc");
-  }
+  t = std::chrono::steady_clock::now();
   int rc = PBFT_OK;
   if (hipMemcpyAsync(k->d_keys, A, 32 * (size_t)n, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key upload");
@@ -752,11 +785,77 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   if (!rc && key_ok && hipMemcpyAsync(key_ok, k->d_key_ok, n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key_ok download");
   if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
+  ks.build_ms = ms_since(t);
+  ks.keys_built = n;
   if (rc) {
-    keyset_release(k);
+    if (k == c->ks) c->adopt(nullptr);  // half-rebuilt tables: no key set rather than a wrong one
+    else keyset_release(k);
+    c->kstats = ks;
     return rc;
   }
-  c->adopt(k);
+  if (k != c->ks) c->adopt(k);
+  else c->n_keys = k->n;  // rebuilt in place: same buffers and plan, new count
+  ks.table_bytes = tab_words * 4 * (size_t)k->cap;
+  ks.total_ms = ms_since(t_all);
+  c->kstats = ks;
+  return PBFT_OK;
+}
+
+// Replace m keys of the installed set in place (the reference admits peers one at a time,
+// src/behavior.rs:45-61 add_peer via src/network_behaviour_composer.rs:24-33): only their tables are rebuilt.
+int pbft_verify_update_keys(pbft_ctx* c, const uint32_t* idx, const uint8_t* A, uint32_t m, uint8_t* key_ok) {
+  if (!c || (m && (!idx || !A))) return set_err(PBFT_EINVAL, "null argument");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (!c->ks) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  std::vector<uint32_t> sorted(idx, idx + m);
+  std::sort(sorted.begin(), sorted.end());
+  for (uint32_t i = 0; i < m; ++i)
+    if (sorted[i] >= c->n_keys || (i && sorted[i] == sorted[i - 1]))
+      return set_err(PBFT_EINVAL, "key index out of range or repeated");
+  const auto t_all = std::chrono::steady_clock::now();
+  pbft_key_stats ks{};
+  ks.reused = 1;
+  if (m == 0) { c->kstats = ks; return PBFT_OK; }
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // no launch (this context's, a clone's, a device form's) reads the old tables
+  keyset* k = c->ks;
+  uint8_t* d_tmp = nullptr;  // [m] slots (u32) then [m][32] encodings
+  const size_t off_enc = ((size_t)4 * m + 255) & ~(size_t)255;
+  if (hipMalloc(&d_tmp, off_enc + 32 * (size_t)m) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(PBFT_ENOMEM, "update staging alloc");
+  }
+  int rc = PBFT_OK;
+  if (hipMemcpyAsync(d_tmp, idx, 4 * (size_t)m, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(d_tmp + off_enc, A, 32 * (size_t)m, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = set_err(PBFT_EHIP, "key upload");
+  if (!rc && build_comb_tables(k->pa, (const uint32_t*)(d_tmp + off_enc), m, 1, k->d_tabA, k->d_key_ok, c->stream,
+                               (const uint32_t*)d_tmp, k->d_keys) != hipSuccess)
+    rc = set_err(PBFT_EHIP, "key table build");
+  std::vector<uint8_t> ok_all;
+  if (!rc && key_ok) {
+    ok_all.resize(k->n);
+    if (hipMemcpyAsync(ok_all.data(), k->d_key_ok, k->n, hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+      rc = set_err(PBFT_EHIP, "key_ok download");
+  }
+  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
+  (void)hipFree(d_tmp);
+  if (rc) {
+    c->adopt(nullptr);  // tables of the updated slots may be half-written
+    return rc;
+  }
+  if (key_ok)
+    for (uint32_t i = 0; i < m; ++i) key_ok[i] = ok_all[idx[i]];
+  ks.keys_built = m;
+  ks.build_ms = ks.total_ms = ms_since(t_all);
+  ks.table_bytes = plan_table_words(k->pa) * 4 * (size_t)k->cap;
+  c->kstats = ks;
+  return PBFT_OK;
+}
+
+int pbft_verify_key_stats(pbft_ctx* c, pbft_key_stats* out) {
+  if (!c || !out) return set_err(PBFT_EINVAL, "null argument");
+  *out = c->kstats;
   return PBFT_OK;
 }
 

@@ -11,15 +11,20 @@
 // Comb tables for a set of points given by encoding (negate: tables of -P).
 // Pass 1, one thread per (key, position): decompress, key_ok, and the
 // position's base point 2^bitoff(pos) * (+-P) by bitoff(pos) doublings.
+// slot (optional): key k of this build goes to slot slot[k] of the tables / key_ok / keys_out (a partial
+// rebuild, pbft_verify_update_keys); keys_out (optional) receives the raw encodings at their slots.
 template <class PL>
 __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __restrict__ enc, uint32_t n_keys,
                                                           int negate, ge* __restrict__ bases,
-                                                          uint8_t* __restrict__ dec_ok, uint8_t* __restrict__ key_ok) {
+                                                          uint8_t* __restrict__ dec_ok, uint8_t* __restrict__ key_ok,
+                                                          const uint32_t* __restrict__ slot,
+                                                          uint32_t* __restrict__ keys_out) {
   constexpr int P = PL::P;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= (uint64_t)P * n_keys) return;
   const uint32_t key = (uint32_t)(tid / P);
   const int pos = (int)(tid % P);
+  const uint32_t sl = slot ? slot[key] : key;
   uint32_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = enc[8 * key + i];
@@ -27,7 +32,11 @@ __global__ void __launch_bounds__(BLOCK) comb_base_kernel(const uint32_t* __rest
   const bool dec = ge_decompress(A, w);
   if (pos == 0) {
     dec_ok[key] = dec ? 1 : 0;
-    if (key_ok) key_ok[key] = (dec && !ge_is_small_order(A)) ? 1 : 0;
+    if (key_ok) key_ok[sl] = (dec && !ge_is_small_order(A)) ? 1 : 0;
+    if (keys_out) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) keys_out[8 * sl + i] = w[i];
+    }
   }
   if (!dec) ge_identity(A);
   if (negate) { ge t; ge_neg(t, A); A = t; }
@@ -52,7 +61,8 @@ __host__ __device__ constexpr uint32_t plan_runs_total() {
 template <class PL>
 __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict__ bases,
                                                            const uint8_t* __restrict__ dec_ok, uint32_t n_keys,
-                                                           uint32_t* __restrict__ tables) {
+                                                           uint32_t* __restrict__ tables,
+                                                           const uint32_t* __restrict__ slot) {
   constexpr int P = PL::P;
   const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t per_key = plan_runs_total<PL>();  // runs of entries 1 .. 2^(width-1) over all positions
@@ -62,7 +72,7 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
   int pos = 0;
   while (run >= plan_runs<PL>(pos)) run -= plan_runs<PL>(pos++);
   const uint32_t E = PL::entries(pos);
-  uint32_t* out = tables + (size_t)key * PL::TABLE_WORDS + (size_t)PL::offset(pos) * 32;
+  uint32_t* out = tables + (size_t)(slot ? slot[key] : key) * PL::TABLE_WORDS + (size_t)PL::offset(pos) * 32;
   if (run == 0) {
     niels id;
     niels_identity(id);
@@ -107,18 +117,18 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
 
 template <class PL>
 static hipError_t build_tables(const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables, uint8_t* d_key_ok,
-                        hipStream_t st) {
+                               hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out) {
   ge* d_bases = nullptr;
   uint8_t* d_dec = nullptr;
   PBFT_HIP_RET(hipMalloc(&d_bases, sizeof(ge) * (size_t)PL::P * n));
   PBFT_HIP_RET(hipMalloc(&d_dec, n));
   const uint64_t t1 = (uint64_t)PL::P * n;
   hipLaunchKernelGGL(comb_base_kernel<PL>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
-                     negate, d_bases, d_dec, d_key_ok);
+                     negate, d_bases, d_dec, d_key_ok, d_slot, d_keys_out);
   PBFT_HIP_RET(hipGetLastError());
   const uint64_t t2 = (uint64_t)plan_runs_total<PL>() * n;
   hipLaunchKernelGGL(comb_entry_kernel<PL>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
-                     d_dec, n, d_tables);
+                     d_dec, n, d_tables, d_slot);
   PBFT_HIP_RET(hipGetLastError());
   PBFT_HIP_RET(hipStreamSynchronize(st));
   PBFT_HIP_RET(hipFree(d_bases));
@@ -127,13 +137,13 @@ static hipError_t build_tables(const uint32_t* d_enc, uint32_t n, int negate, ui
 }
 
 hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
-                             uint8_t* d_key_ok, hipStream_t st) {
+                             uint8_t* d_key_ok, hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out) {
   switch (pa) {
-    case 0: return build_tables<PLB>(d_enc, n, negate, d_tables, d_key_ok, st);
-    case PLA_HUGE::P: return build_tables<PLA_HUGE>(d_enc, n, negate, d_tables, d_key_ok, st);
-    case PLA_BIG::P: return build_tables<PLA_BIG>(d_enc, n, negate, d_tables, d_key_ok, st);
-    case PLA_MID::P: return build_tables<PLA_MID>(d_enc, n, negate, d_tables, d_key_ok, st);
-    case PLA_SMALL::P: return build_tables<PLA_SMALL>(d_enc, n, negate, d_tables, d_key_ok, st);
+    case 0: return build_tables<PLB>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
+    case PLA_HUGE::P: return build_tables<PLA_HUGE>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
+    case PLA_BIG::P: return build_tables<PLA_BIG>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
+    case PLA_MID::P: return build_tables<PLA_MID>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
+    case PLA_SMALL::P: return build_tables<PLA_SMALL>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
     default: return hipErrorInvalidValue;
   }
 }

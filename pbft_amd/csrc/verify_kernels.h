@@ -726,9 +726,12 @@ hipError_t launch_comb_big(const comb_launch_args& a);
 hipError_t launch_comb_mid(const comb_launch_args& a);
 hipError_t launch_comb_small(const comb_launch_args& a);
 
-// tables.hip: comb tables of the base point (pa = 0, plan PLB) or of -A per key (pa = the key plan's positions)
+// tables.hip: comb tables of the base point (pa = 0, plan PLB) or of -A per key (pa = the key plan's positions).
+// d_slot (optional): key k goes to slot d_slot[k] of d_tables / d_key_ok / d_keys_out (partial rebuild);
+// d_keys_out (optional): the raw encodings, stored at their slots.
 hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
-                             uint8_t* d_key_ok, hipStream_t st);
+                             uint8_t* d_key_ok, hipStream_t st, const uint32_t* d_slot = nullptr,
+                             uint32_t* d_keys_out = nullptr);
 
 // finish.hip: batch-inversion finish of the one-lane comb: fm (1, 2, 4, 8, 16) signatures per lane, lv = 0
 // (one inversion per lane) or 6 (one per wave, cross-lane product tree), w = waves per SIMD it is compiled for

@@ -56,6 +56,13 @@ class SigBatch:
         return len(self.R)
 
 
+class KeyStats(ctypes.Structure):
+    """pbft_key_stats (include/pbft_verify.h): phases of the last set_keys / update_keys."""
+    _fields_ = [("total_ms", ctypes.c_double), ("meminfo_ms", ctypes.c_double), ("free_ms", ctypes.c_double),
+                ("alloc_ms", ctypes.c_double), ("build_ms", ctypes.c_double), ("keys_built", ctypes.c_uint32),
+                ("reused", ctypes.c_uint32), ("table_bytes", ctypes.c_uint64)]
+
+
 class VotesStaging(ctypes.Structure):
     """pbft_votes_staging (include/pbft_verify.h)."""
     _fields_ = [("sig", ctypes.c_void_p), ("key_idx", ctypes.c_void_p), ("env_idx", ctypes.c_void_p),
@@ -141,6 +148,23 @@ class GpuBatchVerifier:
         check(self._lib.pbft_verify_set_keys(self._ctx, _ptr(keys), len(keys), _ptr(ok)))
         self.n_keys = len(keys)
         return ok.astype(bool)
+
+    def update_keys(self, idx, keys: np.ndarray) -> np.ndarray:
+        """pbft_verify_update_keys: key idx[i] of the installed set becomes keys[i] (only those tables rebuilt);
+        returns key_ok of the new keys."""
+        idx = np.ascontiguousarray(idx, dtype=np.uint32).reshape(-1)
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1, 32)
+        if len(idx) != len(keys):
+            raise ValueError("idx and keys must have the same length")
+        ok = np.zeros(len(keys), dtype=np.uint8)
+        check(self._lib.pbft_verify_update_keys(self._ctx, _ptr(idx), _ptr(keys), len(keys), _ptr(ok)))
+        return ok.astype(bool)
+
+    def key_stats(self) -> dict:
+        """Phases of the last set_keys / update_keys (ms), keys built, whether the allocation was reused."""
+        st = KeyStats()
+        check(self._lib.pbft_verify_key_stats(self._ctx, ctypes.byref(st)))
+        return {k: getattr(st, k) for k, _ in KeyStats._fields_}
 
     # -- BatchVerifier -------------------------------------------------------
     def verify(self, b: SigBatch) -> np.ndarray:

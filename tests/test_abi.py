@@ -57,3 +57,5 @@ def test_null_arguments_are_errors_not_crashes():
     assert lib.pbft_verify_set_keys(None, None, 0, None) == -1
     assert lib.pbft_verify_batch(None, None, None, None, None, 0, 0, 0, None) == -1
     assert lib.pbft_verify_ctx_destroy(None) == 0
+    assert lib.pbft_verify_update_keys(None, None, None, 0, None) == -1
+    assert lib.pbft_verify_key_stats(None, None) == -1

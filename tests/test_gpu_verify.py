@@ -687,3 +687,59 @@ def test_multi_gpu_rccl_allgather_one_rank(gv, coracle):
     assert (bitmap_to_bool(words, n) == exp[:n]).all()
     assert (words[(n + 63) // 64:] == 0).all()                            # padding words zeroed
     assert int(words[n // 64]) >> (n % 64) == 0                          # bits past n
+
+
+def test_rekey_in_place_and_partial_update(gv, coracle):
+    """a re-key with the same plan reuses the table allocation (no hipFree / hipMalloc), a
+    smaller set too; pbft_verify_update_keys rebuilds only the named keys' tables -- a round signed under the
+    updated set equals the oracle's bitmap over that set, the replaced keys' old signatures now fail, a
+    small-order replacement key rejects everything under it; a plan change frees and re-allocates."""
+    from pbft_amd import PbftError
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 256, tag=31)   # 32,768 signatures
+    rng = np.random.default_rng(31)
+    R2, S2, K2, M2, _ = adversarial(rng, pub, R, S, key_idx, msg, frac=0.01)
+    assert gv.set_keys(pub).all()
+    assert gv.set_keys(pub).all()
+    st = gv.key_stats()
+    assert st["reused"] == 1 and st["free_ms"] == 0 and st["alloc_ms"] == 0 and st["keys_built"] == 64
+    got, _ = verify(gv, R2, S2, K2, M2, 85)
+    assert (got == oracle_bits(coracle, pub, R2, S2, K2, M2, 85)).all()
+    # a smaller set in the same allocation: key indices >= 48 are out of the set (bit 0)
+    assert gv.set_keys(pub[:48]).all() and gv.key_stats()["reused"] == 1
+    got, _ = verify(gv, R2, S2, K2, M2, 85)
+    exp = oracle_bits(coracle, np.ascontiguousarray(pub[:48]), R2, S2, K2, M2, 85)
+    assert (got == exp).all() and not got[key_idx >= 48].any()
+    assert gv.set_keys(pub).all() and gv.key_stats()["reused"] == 1
+    # replace replicas 5 and 40 (new identities); the round re-signed under the new set
+    slots = np.array([5, 40], np.uint32)
+    seeds_new = seeds.copy()
+    seeds_new[slots] = seeds_for(2, tag=32)
+    Rn, Sn, pub_new = gv.sign(seeds_new, key_idx, msg, 85)
+    assert (pub_new[np.setdiff1d(np.arange(64), slots)] == pub[np.setdiff1d(np.arange(64), slots)]).all()
+    assert gv.update_keys(slots, pub_new[slots]).all()
+    st = gv.key_stats()
+    assert st["keys_built"] == 2 and st["reused"] == 1
+    Rn2, Sn2, Kn2, Mn2, _ = adversarial(rng, pub_new, Rn, Sn, key_idx, msg, frac=0.01)
+    got, _ = verify(gv, Rn2, Sn2, Kn2, Mn2, 85)
+    assert (got == oracle_bits(coracle, pub_new, Rn2, Sn2, Kn2, Mn2, 85)).all()
+    old, _ = verify(gv, R, S, key_idx, msg, 85)
+    replaced = np.isin(key_idx, slots)
+    assert not old[replaced].any() and old[~replaced].all()
+    # a small-order replacement: key_ok 0, every signature under it rejects
+    so = np.frombuffer(bytes.fromhex(KAT["small_order_encodings"][0]), np.uint8).reshape(1, 32)
+    assert not gv.update_keys([7], so).any()
+    got, _ = verify(gv, Rn, Sn, key_idx, msg, 85)
+    assert not got[key_idx == 7].any() and got[(key_idx != 7)].all()
+    for bad in ([64], [3, 3]):
+        with pytest.raises(PbftError) as e:
+            gv.update_keys(bad, pub_new[: len(bad)])
+        assert e.value.code == -1
+    # a plan change (budget forced down, then back) frees and re-allocates
+    gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 1500)
+    try:
+        assert gv.set_keys(pub_new).all() and gv.positions()[1] == 16 and gv.key_stats()["reused"] == 0
+        got, _ = verify(gv, Rn2, Sn2, Kn2, Mn2, 85)
+        assert (got == oracle_bits(coracle, pub_new, Rn2, Sn2, Kn2, Mn2, 85)).all()
+    finally:
+        gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 0)
+    assert gv.set_keys(pub_new).all() and gv.key_stats()["reused"] == 0

@@ -58,7 +58,7 @@ for k in ("comb_kernel", "finish_kernel"):
 out["traffic_bytes_per_launch"] = tot
 out["valu_insts_per_sig_total"] = sum(out[k]["valu_insts_per_sig"] for k in ("comb_kernel", "finish_kernel"))
 out["note"] = ("rocprofv3 --pmc passes (one counter group per run, no tracing) of `python3 bench.py --steps 5 "
-               "--warmup 1 --no-cpu --no-extras` (tools/gpu_prof_r03.sh); FETCH_SIZE (KB) doubled per the "
+               "--warmup 1 --no-cpu --no-extras` (tools/gpu_prof.sh); FETCH_SIZE (KB) doubled per the "
                "gfx950 correction of MI355X_MICROARCH.md's HBM section; WRITE_SIZE taken as is")
 json.dump(out, open(os.path.join(d, "derived.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
