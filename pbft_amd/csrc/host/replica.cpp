@@ -17,6 +17,7 @@
 // that the loop never blocks on the GPU.
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <array>
 #include <atomic>
 #include <cstdlib>
@@ -226,7 +227,24 @@ class WorkerPool {
 
 }  // namespace
 
+// Flush timeline (PBFT_REPLICA_TRACE=1): host timestamps of the submit / fill / launch / land / apply steps of one
+// batch, printed to stderr when the batch completes (tools/replica_probe.py reads them).
+static const bool g_trace = getenv("PBFT_REPLICA_TRACE") != nullptr;
+struct TraceEv {
+  const char* what;
+  uint64_t ns, arg;
+};
+static uint64_t now_ns() {
+  return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+             std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+#define RTRACE(r, what, arg) \
+  do {                       \
+    if (g_trace) (r)->trace.push_back({what, now_ns(), (uint64_t)(arg)}); \
+  } while (0)
+
 struct pbft_replica {
+  std::vector<TraceEv> trace;
   pbft_ctx* ctx = nullptr;
   uint32_t n = 0, f = 0, self = 0;
   uint64_t current_view = 1;  // src/view.rs:5-8: the view starts at 1 (no view change)
@@ -667,9 +685,12 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
         done[k].fetch_add(1, std::memory_order_release);
       }
   });
+  RTRACE(r, "begin", N);
   for (size_t k = 0; k < W && rc == PBFT_OK; ++k) {
     while (done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    RTRACE(r, "filled", k);
     rc = pbft_verify_votes_submit_rows(r->ctx, cut[k + 1] < G ? r->segs[cut[k + 1]].row0 : N);
+    RTRACE(r, "launched", k);
   }
   WorkerPool::get().wait();
   return rc;
@@ -785,19 +806,19 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
   return 1;
 }
 
-// inject_node_event Prepare / Commit arms (src/behavior.rs:340-412): enqueue into the round window
-int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
-                      uint32_t signer, const uint8_t sig[64]) {
-  if (!r || !digest || !sig || (kind != PBFT_KIND_PREPARE && kind != PBFT_KIND_COMMIT)) return PBFT_EINVAL;
-  ++r->stats.pushed;
-  if (signer >= r->n || view != r->current_view) { ++r->stats.rejected_view; return 0; }  // validate_commit :187-190
-  if (!in_log(r, seq)) { ++r->stats.rejected_watermark; return 0; }
-  Window& w = window_at(r, {view, seq});
-  if (w.committed_reported) { ++r->stats.duplicates; return 0; }  // late vote for a decided round
+// Counters one push updates (the replica's own, or a worker thread's share in a parallel push_many).
+struct PushCounts {
+  uint64_t pushed = 0, rejected_view = 0, rejected_watermark = 0, duplicates = 0, dropped_flood = 0, queued = 0;
+};
+
+// The part of a push that touches one window (State::insert_* candidates, src/state.rs:49-67): 1 queued, 0 dropped.
+static int push_into(const pbft_replica* r, Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer,
+                     const uint8_t* sig, PushCounts& st) {
+  if (w.committed_reported) { ++st.duplicates; return 0; }  // late vote for a decided round
   Phase& p = w.ph[kind];
   p.init(r->n);
   if (p.acc[signer] && memcmp(p.acc_digs[p.acc[signer] - 1].data(), digest, 64) == 0) {
-    ++r->stats.duplicates;
+    ++st.duplicates;
     return 0;
   }
   const int64_t j = p.find_dig(digest);
@@ -805,10 +826,10 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
     if (j >= 0)
       for (size_t i = 0; i < p.size(); ++i)
         if (p.who[i] == signer && p.dix[i] == (uint32_t)j && memcmp(&p.sig[64 * i], sig, 64) == 0) {
-          ++r->stats.duplicates;
+          ++st.duplicates;
           return 0;
         }
-    if (p.cnt[signer] >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
+    if (p.cnt[signer] >= PBFT_MAX_CANDIDATES) { ++st.dropped_flood; return 0; }
   } else if (!p.acc[signer]) {
     ++p.distinct;
   }
@@ -818,23 +839,96 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
   }
   p.append(digest, j, signer, sig);
   ++p.cnt[signer];
+  ++st.queued;
   return 1;
 }
+
+static void add_counts(pbft_replica* r, const PushCounts& c) {
+  r->stats.pushed += c.pushed;
+  r->stats.rejected_view += c.rejected_view;
+  r->stats.rejected_watermark += c.rejected_watermark;
+  r->stats.duplicates += c.duplicates;
+  r->stats.dropped_flood += c.dropped_flood;
+}
+
+// inject_node_event Prepare / Commit arms (src/behavior.rs:340-412): enqueue into the round window
+int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
+                      uint32_t signer, const uint8_t sig[64]) {
+  if (!r || !digest || !sig || (kind != PBFT_KIND_PREPARE && kind != PBFT_KIND_COMMIT)) return PBFT_EINVAL;
+  PushCounts c;
+  ++c.pushed;
+  int rc = 0;
+  if (signer >= r->n || view != r->current_view) ++c.rejected_view;  // validate_commit :187-190
+  else if (!in_log(r, seq)) ++c.rejected_watermark;
+  else rc = push_into(r, window_at(r, {view, seq}), kind, digest, signer, sig, c);
+  add_counts(r, c);
+  return rc;
+}
+
+// push_many of at least this many rows runs on the worker pool (PBFT_REPLICA_THREADS threads)
+static constexpr uint64_t PUSH_PAR_MIN = 1u << 14;
 
 int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
                            const uint8_t* digests, const uint32_t* signer, const uint8_t* sigs, uint64_t* queued) {
   if (!r || (N && (!kind || !view || !seq || !digests || !signer || !sigs))) return PBFT_EINVAL;
+  // rows before the first invalid kind are pushed, then PBFT_EINVAL (as N single pushes would)
+  uint64_t n_ok = 0;
+  while (n_ok < N && (kind[n_ok] == PBFT_KIND_PREPARE || kind[n_ok] == PBFT_KIND_COMMIT)) ++n_ok;
+  const unsigned hw = std::thread::hardware_concurrency();
+  const size_t T = n_ok >= PUSH_PAR_MIN ? std::min<size_t>(hw ? hw : 1, host_threads()) : 1;
   uint64_t q = 0;
-  for (uint64_t i = 0; i < N; ++i) {
-    const int rc = pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
-    if (rc < 0) {
-      if (queued) *queued = q;
-      return rc;
+  if (T <= 1) {
+    for (uint64_t i = 0; i < n_ok; ++i)
+      q += (uint64_t)pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
+  } else {
+    // The windows are independent: every window's rows go to ONE thread, in input order (per-window order is
+    // all the state machine depends on: the last accepted vote of a signer wins).
+    //  1. (threads, by input slices) the per-row checks that need no window, and runs of consecutive rows with
+    //     one (view, seq); rejected rows are flagged and do not break a run;
+    struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; };
+    std::vector<std::vector<Run>> slice_runs(T);
+    std::vector<uint8_t> bad(n_ok);
+    std::vector<PushCounts> cnt(T);
+    WorkerPool::get().run(T, [&](size_t t) {
+      const uint64_t lo = n_ok * t / T, hi = n_ok * (t + 1) / T;
+      std::vector<Run>& runs = slice_runs[t];
+      PushCounts& c = cnt[t];
+      for (uint64_t i = lo; i < hi; ++i) {
+        ++c.pushed;
+        if (signer[i] >= r->n || view[i] != r->current_view) { ++c.rejected_view; bad[i] = 1; continue; }
+        if (!in_log(r, seq[i])) { ++c.rejected_watermark; bad[i] = 1; continue; }
+        bad[i] = 0;
+        if (runs.empty() || runs.back().seq != seq[i]) runs.push_back({i, i + 1, seq[i], nullptr, 0});
+        else runs.back().hi = i + 1;
+      }
+    });
+    //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
+    //     owner: the thread whose share of the rows its first run starts in;
+    std::vector<Run> runs;
+    for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
+    std::unordered_map<Window*, uint32_t> owner;
+    owner.reserve(runs.size() < 8192 ? runs.size() : 8192);
+    for (Run& u : runs) {
+      u.w = &window_at(r, {r->current_view, u.seq});
+      auto it = owner.emplace(u.w, (uint32_t)(u.lo * T / n_ok)).first;
+      u.owner = it->second;
     }
-    q += (uint64_t)rc;
+    //  3. (threads) every thread pushes the rows of the windows it owns, in input order.
+    WorkerPool::get().run(T, [&](size_t t) {
+      PushCounts& c = cnt[t];
+      for (const Run& u : runs) {
+        if (u.owner != t) continue;
+        for (uint64_t i = u.lo; i < u.hi; ++i)
+          if (!bad[i]) push_into(r, *u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c);
+      }
+    });
+    for (const PushCounts& c : cnt) {
+      add_counts(r, c);
+      q += c.queued;
+    }
   }
   if (queued) *queued = q;
-  return PBFT_OK;
+  return n_ok < N ? PBFT_EINVAL : PBFT_OK;
 }
 
 // Verify every READY sub-window (force: every pending candidate) in one batch, asynchronously.
@@ -848,12 +942,14 @@ int pbft_replica_flush_submit(pbft_replica* r, int force, uint64_t* n_rows) {
   const auto t0 = std::chrono::steady_clock::now();
   const int rc = flush_submit_impl(r, force, n_rows);
   r->stats.submit_ns += ns_since(t0);
+  RTRACE(r, "submit_end", rc);
   return rc;
 }
 
 static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   if (n_rows) *n_rows = 0;
   if (r->in_flight) return PBFT_EBUSY;
+  RTRACE(r, "submit", 0);
   if (!r->verify_fn && !r->vsub && !r->ctx) return PBFT_ENODEV;
   // 1. one segment per ready phase: its candidates (all pending between batches) and its envelopes, one per
   //    distinct (kind, view, seq, digest)
@@ -874,6 +970,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     }
   }
   r->rows = N;
+  RTRACE(r, "segs", r->segs.size());
   if (n_rows) *n_rows = N;
   if (N == 0) { r->segs.clear(); return PBFT_OK; }
   r->bitmap.assign((N + 63) / 64, 0);
@@ -962,17 +1059,30 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
       // (a window's segments stay in order: a prefix of the batch)
       const size_t G = r->segs.size();
       if (rows_done >= (r->seg_next < G ? r->segs[r->seg_next].row0 : r->rows) + (1u << 16)) {
+        RTRACE(r, "landed", rows_done);
         size_t s1 = r->seg_next;
         while (s1 < G && r->segs[s1].row0 + r->segs[s1].count <= rows_done) ++s1;
         apply_segs(r, r->seg_next, s1);
         r->stats.apply_ns += ns_since(t0);
+        RTRACE(r, "applied", s1);
       }
       return 0;
     }
+    RTRACE(r, "done", rows_done);
     finish_batch(r);
+    RTRACE(r, "finish_batch", 0);
     evaluate(r);
+    RTRACE(r, "evaluate", r->evq.size());
     gc(r);
     r->stats.apply_ns += ns_since(t0);
+    RTRACE(r, "gc", r->windows.size());
+    if (g_trace && !r->trace.empty()) {
+      const uint64_t t_0 = r->trace.front().ns;
+      fprintf(stderr, "replica-trace:");
+      for (const TraceEv& e : r->trace) fprintf(stderr, " %s:%llu@%.3f", e.what, (unsigned long long)e.arg, (e.ns - t_0) * 1e-6);
+      fprintf(stderr, "\n");
+      r->trace.clear();
+    }
   } else {
     evaluate(r);
     gc(r);

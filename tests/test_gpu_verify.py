@@ -735,7 +735,7 @@ def test_rekey_in_place_and_partial_update(gv, coracle):
             gv.update_keys(bad, pub_new[: len(bad)])
         assert e.value.code == -1
     # a plan change (budget forced down, then back) frees and re-allocates
-    gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 1500)
+    gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 5000)   # 64 keys x 63 MB: the 16-position plan
     try:
         assert gv.set_keys(pub_new).all() and gv.positions()[1] == 16 and gv.key_stats()["reused"] == 0
         got, _ = verify(gv, Rn2, Sn2, Kn2, Mn2, 85)

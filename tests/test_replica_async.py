@@ -283,3 +283,102 @@ def test_checkpoint_while_a_batch_is_in_flight():
     assert evs == [(1, 2, EV_PRE_PREPARED)]
     assert c.stats(0)["live_windows"] == 1
     c.close()
+
+
+def test_parallel_push_many_equals_serial_pushes():
+    """pbft_replica_push_many of >= 2^14 rows runs on the worker pool (each window's rows on one
+    thread, in input order).  On a shuffled adversarial mix -- duplicates, conflicting digests, candidate floods,
+    wrong views, unknown signers, out-of-window seqs -- it must leave the replica exactly as the same rows pushed
+    one at a time: same counters, same queued count, and the same events and counters after a forced flush."""
+    from replica_sim import Stats, lib
+    L = lib()
+    n, seqs = 64, 300
+    rng = np.random.default_rng(41)
+    rows = []
+    for q in range(1, seqs + 1):
+        d, d2 = _digest(q), _digest(q + 10_000)
+        for kind in (KIND_PREPARE, KIND_COMMIT):
+            for s in range(n):
+                rows.append((kind, 1, q, d, s, 0))
+            for s in rng.choice(n, 8, replace=False):          # duplicates (same signature bytes)
+                rows.append((kind, 1, q, d, int(s), 0))
+            for s in rng.choice(n, 4, replace=False):          # conflicting digest from the same signer
+                rows.append((kind, 1, q, d2, int(s), 1))
+            s = int(rng.integers(n))
+            for k in range(6):                                  # flood: 6 distinct candidates, 4 kept
+                rows.append((kind, 1, q, d, s, 2 + k))
+    for k in range(200):
+        rows.append((KIND_PREPARE, 2, 5, _digest(5), 3, 0))     # wrong view
+        rows.append((KIND_COMMIT, 1, 7, _digest(7), n + k, 0))  # unknown signer
+        rows.append((KIND_PREPARE, 1, 10_000 + k, _digest(9), 3, 0))  # out of the log window
+    # the first half of the rows in window order (long runs), the second half shuffled (a run per row)
+    half = len(rows) // 2
+    rows = rows[:half] + [rows[half + i] for i in rng.permutation(len(rows) - half)]
+    N = len(rows)
+    assert N >= 1 << 15
+    kind = np.array([r[0] for r in rows], np.uint8)
+    view = np.array([r[1] for r in rows], np.uint64)
+    seq = np.array([r[2] for r in rows], np.uint64)
+    digs = np.frombuffer(b"".join(r[3] for r in rows), np.uint8).reshape(N, 64).copy()
+    signer = np.array([r[4] for r in rows], np.uint32)
+    sigs = np.zeros((N, 64), np.uint8)
+    sigs[:, 0] = kind
+    sigs[:, 1:9] = seq.view(np.uint8).reshape(N, 8)
+    sigs[:, 9:11] = (signer & 0xFFFF).astype(np.uint16).view(np.uint8).reshape(N, 2)
+    var = np.array([r[5] for r in rows], np.uint8)
+    sigs[:, 32] = 2 * var                       # even: valid under ScriptedVotes
+    sigs[:, 33] = var
+    sigs[rng.random(N) < 0.05, 32] |= 1         # 5 % invalid signatures
+    keys = np.zeros((n, 32), np.uint8).tobytes()
+
+    def make():
+        rep = ctypes.c_void_p()
+        assert L.pbft_replica_create(None, n, 0, keys, ctypes.byref(rep)) == 0
+        return rep
+
+    def stats(rep):
+        st = Stats()
+        L.pbft_replica_get_stats(rep, ctypes.byref(st))
+        return {k: getattr(st, k) for k, _ in Stats._fields_ if not k.endswith("_ns")}
+
+    a, b = make(), make()
+    qa, qb = ctypes.c_uint64(), ctypes.c_uint64()
+    t = time.perf_counter()
+    assert L.pbft_replica_push_many(a, N, kind.ctypes.data, view.ctypes.data, seq.ctypes.data, digs.ctypes.data,
+                                    signer.ctypes.data, sigs.ctypes.data, ctypes.byref(qa)) == 0
+    t_par = time.perf_counter() - t
+    total = 0
+    for lo in range(0, N, 1000):   # below the parallel threshold: the serial path
+        hi = min(N, lo + 1000)
+        assert L.pbft_replica_push_many(b, hi - lo, kind[lo:].ctypes.data, view[lo:].ctypes.data, seq[lo:].ctypes.data,
+                                        digs[lo:].ctypes.data, signer[lo:].ctypes.data, sigs[lo:].ctypes.data,
+                                        ctypes.byref(qb)) == 0
+        total += qb.value
+    assert qa.value == total and stats(a) == stats(b), (qa.value, total)
+    assert stats(a)["dropped_flood"] > 0 and stats(a)["duplicates"] > 0 and stats(a)["rejected_watermark"] == 200
+    evs = {}
+    for name, rep in (("a", a), ("b", b)):
+        v = ScriptedVotes()
+        v.release = True
+        assert L.pbft_replica_set_votes_verifier(rep, v.submit_cb, v.poll_cb, None) == 0
+        from replica_sim import DIGEST_FN
+        dfn = DIGEST_FN(lambda u, op, ln, out: ctypes.memmove(out, hashlib.blake2b(ctypes.string_at(op, ln),
+                                                                                    digest_size=64).digest(), 64) and 0)
+        assert L.pbft_replica_set_digest_fn(rep, dfn, None) == 0
+        for q in range(1, seqs + 1):
+            sig = bytearray(64)
+            sig[0] = KIND_PREPREPARE
+            sig[1:9] = q.to_bytes(8, "little")
+            sig[9:11] = (1).to_bytes(2, "little")
+            op = b"op-" + str(q).encode()
+            assert L.pbft_replica_on_pre_prepare(rep, 1, 1, q, op, len(op), _digest(q), bytes(sig), None) == 1
+        ev = (Event * 4096)()
+        ne = ctypes.c_uint32()
+        assert L.pbft_replica_flush(rep, 1, ev, 4096, ctypes.byref(ne)) == 0
+        evs[name] = sorted((e.view, e.seq, e.kind) for e in ev[: ne.value])
+        v.keep = dfn
+    assert evs["a"] == evs["b"] and stats(a) == stats(b)
+    assert sum(1 for e in evs["a"] if e[2] == EV_COMMITTED) > seqs // 2
+    L.pbft_replica_destroy(a)
+    L.pbft_replica_destroy(b)
+    print(f"push_many {N} rows: {t_par * 1e3:.1f} ms on the pool")
