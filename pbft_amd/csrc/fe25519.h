@@ -204,6 +204,44 @@ FE_FN uint64_t mad_acc(uint32_t a, uint32_t b, uint64_t acc) {
 #ifndef PBFT_CHAIN_FORM
 #define PBFT_CHAIN_FORM 0
 #endif
+#ifndef PBFT_COLUMN_ASM
+#define PBFT_COLUMN_ASM 1  // fe_mul_chain: one inline-asm block of 10 mads per (product, column)
+#endif
+
+// One column of a single-chain product (fe_mul_chain), device code: acc' = acc + sum_i fi[i] * gj[i] as TEN
+// v_mad_u64_u32 in ONE inline-asm block (FIRST: acc' = sum, no addend).  The block is opaque to LLVM, so the carry
+// that enters as the first mad's addend is never re-associated into a separate 64-bit add -- what the per-mad
+// laundering asm of mad_acc() achieved at the price of one hazard s_nop after nearly every mad: gfx950's
+// DstSel-forwarding hazard check assumes an inline-asm def may need one wait state before the next VALU that
+// touches it, so 715 launders per comb step cost 247 s_nop (profiles/r03/step_hist_chain.txt); one asm per
+// column leaves at most one per column, usually none (the other products' columns fill the slot).
+#if defined(__HIP_DEVICE_COMPILE__)
+template <bool FIRST>
+__device__ __forceinline__ void mad_column10(uint64_t& acc, const uint32_t fi[10], const uint32_t gj[10]) {
+  uint64_t cc;
+#define PBFT_MAD_COL_REST                                                                                         \
+  "v_mad_u64_u32 %0, %1, %4, %5, %0\n\t"                                                                            \
+  "v_mad_u64_u32 %0, %1, %6, %7, %0\n\t"                                                                            \
+  "v_mad_u64_u32 %0, %1, %8, %9, %0\n\t"                                                                            \
+  "v_mad_u64_u32 %0, %1, %10, %11, %0\n\t"                                                                          \
+  "v_mad_u64_u32 %0, %1, %12, %13, %0\n\t"                                                                          \
+  "v_mad_u64_u32 %0, %1, %14, %15, %0\n\t"                                                                          \
+  "v_mad_u64_u32 %0, %1, %16, %17, %0\n\t"                                                                          \
+  "v_mad_u64_u32 %0, %1, %18, %19, %0\n\t"                                                                          \
+  "v_mad_u64_u32 %0, %1, %20, %21, %0"
+#define PBFT_MAD_COL_IN                                                                                           \
+  "v"(fi[0]), "v"(gj[0]), "v"(fi[1]), "v"(gj[1]), "v"(fi[2]), "v"(gj[2]), "v"(fi[3]), "v"(gj[3]), "v"(fi[4]),    \
+      "v"(gj[4]), "v"(fi[5]), "v"(gj[5]), "v"(fi[6]), "v"(gj[6]), "v"(fi[7]), "v"(gj[7]), "v"(fi[8]), "v"(gj[8]), \
+      "v"(fi[9]), "v"(gj[9])
+  if constexpr (FIRST)
+    asm("v_mad_u64_u32 %0, %1, %2, %3, 0\n\t" PBFT_MAD_COL_REST : "=&v"(acc), "=&s"(cc) : PBFT_MAD_COL_IN);
+  else
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0\n\t" PBFT_MAD_COL_REST : "+v"(acc), "=&s"(cc) : PBFT_MAD_COL_IN);
+#undef PBFT_MAD_COL_REST
+#undef PBFT_MAD_COL_IN
+  (void)cc;
+}
+#endif
 // N independent products h[m] = f[m] g[m], each computed as ONE dependent chain over the columns: column k's
 // mads accumulate on top of column k-1's carry, so a carry costs one 64-bit shift and one mask and no 64-bit
 // add (fe_reduce_wide's single-chain arithmetic, PBFT_REDUCE_1CHAIN: identical outputs and bounds).  The N
@@ -221,6 +259,30 @@ FE_FN void fe_mul_chain(fe* const h[], const fe* const f[], const fe* const g[])
       fx[m][i] = (i & 1) ? dbl32(f[m]->v[i]) : f[m]->v[i];
     }
   }
+#if defined(__HIP_DEVICE_COMPILE__) && PBFT_COLUMN_ASM
+#ifndef PBFT_COLUMN_ASM_MOUTER
+#define PBFT_COLUMN_ASM_MOUTER 1
+#endif
+#pragma unroll
+  for (int kk = 0; kk < 10 * N; ++kk) {
+    // product by product (m outer): one product's operands live at a time; else column by column
+    const int k = PBFT_COLUMN_ASM_MOUTER ? kk % 10 : kk / N;
+    const int m = PBFT_COLUMN_ASM_MOUTER ? kk / 10 : kk % N;
+    {
+      uint32_t fi[10], gj[10];
+#pragma unroll
+      for (int i = 0; i < 10; ++i) {
+        const int j = k - i;  // g index; j < 0 wraps with x19; odd*odd limb products carry an extra factor 2
+        fi[i] = ((i & 1) && (j & 1)) ? fx[m][i] : f[m]->v[i];
+        gj[i] = j >= 0 ? g[m]->v[j] : g19[m][j + 10];
+      }
+      if (k == 0) mad_column10<true>(acc[m], fi, gj);
+      else mad_column10<false>(acc[m], fi, gj);
+      l[m][k] = (uint32_t)acc[m] & ((k & 1) ? M25 : M26);
+      acc[m] >>= (k & 1) ? 25 : 26;
+    }
+  }
+#else
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
 #pragma unroll
@@ -257,6 +319,7 @@ FE_FN void fe_mul_chain(fe* const h[], const fe* const f[], const fe* const g[])
       acc[m] >>= (k & 1) ? 25 : 26;
     }
   }
+#endif
 #pragma unroll
   for (int m = 0; m < N; ++m) {
     const uint64_t h0 = (uint64_t)l[m][0] + acc[m] * 19u;  // acc = the carry out of column 9
