@@ -137,6 +137,12 @@ typedef int (*pbft_digest_fn)(void *user, const uint8_t *op, uint32_t op_len, ui
  * verifier override is installed before the first flush.  The primary of view v
  * is replica v mod n (Castro-Liskov p = v mod |R|). */
 int pbft_replica_create(pbft_ctx *ctx, uint32_t n, uint32_t self_id, const uint8_t *keys, pbft_replica **out);
+/* Replica idx[i] (< n, distinct) gets the key A[i][32] -- a peer admitted after start-up (Pbft::add_peer,
+ * src/behavior.rs:45-61, fed by mDNS discovery src/network_behaviour_composer.rs:24-33): its PeerId now maps to
+ * replica idx[i] (pbft_replica_peer_index) and, with a GPU context, only its comb tables are rebuilt
+ * (pbft_verify_update_keys; key_ok as there).  Votes already accepted under the old key stay; candidates still
+ * pending are verified under the new key.  PBFT_EBUSY while a batch is in flight. */
+int pbft_replica_update_keys(pbft_replica *r, const uint32_t *idx, const uint8_t *A, uint32_t m, uint8_t *key_ok);
 int pbft_replica_destroy(pbft_replica *r);
 int pbft_replica_set_verifier(pbft_replica *r, pbft_batch_verify_fn fn, void *user);
 int pbft_replica_set_votes_verifier(pbft_replica *r, pbft_votes_submit_fn submit, pbft_votes_poll_fn poll,

@@ -205,6 +205,8 @@ extern "C" {
     pub fn pbft_replica_create(ctx: *mut pbft_ctx, n: u32, self_id: u32, keys: *const u8,
                                out: *mut *mut pbft_replica) -> c_int;
     pub fn pbft_replica_destroy(r: *mut pbft_replica) -> c_int;
+    pub fn pbft_replica_update_keys(r: *mut pbft_replica, idx: *const u32, a: *const u8, m: u32,
+                                    key_ok: *mut u8) -> c_int;
     pub fn pbft_replica_set_verifier(r: *mut pbft_replica, f: pbft_batch_verify_fn, user: *mut c_void) -> c_int;
     pub fn pbft_replica_set_votes_verifier(r: *mut pbft_replica, submit: pbft_votes_submit_fn,
                                            poll: pbft_votes_poll_fn, user: *mut c_void) -> c_int;

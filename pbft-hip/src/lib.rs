@@ -503,6 +503,19 @@ impl<'a> Replica<'a> {
         self.verifier = Some(boxed);
         Ok(())
     }
+    /// Peers admitted after start-up (Pbft::add_peer, src/behavior.rs:45-61): replica `idx[i]` gets `keys[i]`
+    /// (its PeerId resolves through `peer_index` from now on; with a GPU context only its tables are rebuilt).
+    pub fn update_keys(&mut self, idx: &[u32], keys: &[[u8; 32]]) -> Result<Vec<bool>> {
+        if idx.len() != keys.len() {
+            return Err(Error { code: ffi::PBFT_EINVAL, message: "update_keys: idx and keys lengths differ".into() });
+        }
+        let mut ok = vec![0u8; keys.len()];
+        check(unsafe {
+            ffi::pbft_replica_update_keys(self.raw, idx.as_ptr(), keys.as_ptr() as *const u8, keys.len() as u32,
+                                          ok.as_mut_ptr())
+        })?;
+        Ok(ok.into_iter().map(|b| b == 1).collect())
+    }
     /// PrePrepare ingress (validate_pre_prepare, src/behavior.rs:126-157, plus the signature TODO :127) from
     /// replica `peer` -- the AUTHENTICATED connection's replica index (`peer_index` of inject_node_event's
     /// peer_id, src/behavior.rs:304); dropped unless it is the view's primary.

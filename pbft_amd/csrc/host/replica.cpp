@@ -720,6 +720,30 @@ int pbft_replica_create(pbft_ctx* ctx, uint32_t n, uint32_t self_id, const uint8
   return PBFT_OK;
 }
 
+int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t* A, uint32_t m, uint8_t* key_ok) {
+  if (!r || (m && (!idx || !A))) return PBFT_EINVAL;
+  if (r->in_flight) return PBFT_EBUSY;
+  for (uint32_t i = 0; i < m; ++i) {
+    if (idx[i] >= r->n) return PBFT_EINVAL;
+    for (uint32_t j = 0; j < i; ++j)
+      if (idx[j] == idx[i]) return PBFT_EINVAL;
+  }
+  if (r->ctx && m) {
+    const int rc = pbft_verify_update_keys(r->ctx, idx, A, m, key_ok);
+    if (rc) return rc;
+  } else if (key_ok) {
+    memset(key_ok, 1, m);  // (no GPU context: the installed verifier override judges the keys)
+  }
+  for (uint32_t i = 0; i < m; ++i) {
+    uint8_t* k = &r->keys[32 * (size_t)idx[i]];
+    auto it = r->key_index.find(key_str(k));
+    if (it != r->key_index.end() && it->second == idx[i]) r->key_index.erase(it);
+    memcpy(k, A + 32 * (size_t)i, 32);
+    r->key_index.emplace(key_str(k), idx[i]);  // (a key another replica already has keeps its first index)
+  }
+  return PBFT_OK;
+}
+
 int pbft_replica_destroy(pbft_replica* r) {
   if (!r) return PBFT_OK;
   if (r->in_flight && r->in_flight_via == 0 && r->ctx) (void)pbft_verify_wait(r->ctx);

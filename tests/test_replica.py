@@ -11,6 +11,7 @@ peer (src/behavior.rs:346, :380) and the h/H watermarks (TODO :154, :192).
 import ctypes
 import hashlib
 
+import numpy as np
 import pytest
 
 from replica_sim import (EV_COMMITTED, EV_PRE_PREPARED, EV_PREPARED, KIND_COMMIT, KIND_PREPARE, KIND_PREPREPARE,
@@ -335,4 +336,39 @@ def test_peer_id_binding():
     assert L.pbft_key_from_peer_id_b58(b"12D3KooW0OIl", 12, out) == -1          # not base58
     stranger = bytes([0x00, 0x24, 0x08, 0x01, 0x12, 0x20]) + bytes(range(32))
     assert L.pbft_replica_peer_index(c.reps[0], stranger, 38) == -1             # not a replica
+    c.close()
+
+
+def test_replica_update_keys_admits_a_new_identity():
+    """pbft_replica_update_keys (the reference's add_peer, src/behavior.rs:45-61): replica 3 gets a new identity;
+    its new PeerId resolves to index 3, the old one no longer does, and votes signed with the new key verify
+    (the oracle verifier is handed the replica's current key set)."""
+    import ctypes
+    from replica_sim import seeds as mkseeds
+    c = Cluster(4)
+    L, r0 = c.L, c.reps[0]
+    new_seed = mkseeds(1, tag=99)[0]
+    pk = ctypes.create_string_buffer(32)
+    c.o.oracle_public_key(pk, new_seed)
+    old_pid, new_pid = ctypes.create_string_buffer(38), ctypes.create_string_buffer(38)
+    L.pbft_peer_id_from_key(c.keys[96:128], old_pid)
+    L.pbft_peer_id_from_key(pk.raw, new_pid)
+    assert L.pbft_replica_peer_index(r0, old_pid.raw, 38) == 3
+    idx = (ctypes.c_uint32 * 1)(3)
+    ok = (ctypes.c_uint8 * 1)()
+    assert L.pbft_replica_update_keys(r0, idx, pk.raw, 1, ok) == 0
+    assert L.pbft_replica_peer_index(r0, new_pid.raw, 38) == 3 and L.pbft_replica_peer_index(r0, old_pid.raw, 38) < 0
+    bad = (ctypes.c_uint32 * 2)(1, 1)
+    assert L.pbft_replica_update_keys(r0, bad, pk.raw * 2, 2, None) == -1          # repeated index
+    assert L.pbft_replica_update_keys(r0, (ctypes.c_uint32 * 1)(4), pk.raw, 1, None) == -1  # out of range
+    # the verifier override judges against the cluster's table: give it the new key too
+    keys = bytearray(c.keys)
+    keys[96:128] = pk.raw
+    c.keys_np = np.frombuffer(bytes(keys), np.uint8).copy()
+    c.seeds[3] = new_seed
+    assert c.pre_prepare(0, 1, 1, OP) == 1
+    for s in (2, 3):
+        assert L.pbft_replica_push(r0, KIND_PREPARE, 1, 1, D, s, c.sign(s, KIND_PREPARE, 1, 1, D)) == 1
+    evs = c.flush(0)
+    assert (1, 1, EV_PREPARED) in evs and c.stats(0)["rejected_sig"] == 0
     c.close()
