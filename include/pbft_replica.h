@@ -52,9 +52,12 @@
  *     the next batch;
  *   - a PrePrepare is taken only from the primary's own connection (frames and
  *     pbft_replica_on_pre_prepare alike: both take the authenticated peer);
- *   - events are decided when a batch is applied, whether or not the caller's
- *     event buffer has room: undelivered events wait in the replica's queue for
- *     the next flush / flush_poll, and GC never waits for delivery;
+ *   - events are decided as a batch is applied -- a window's as soon as its last
+ *     rows in the batch are (a large batch comes back chunk by chunk), in
+ *     (view, seq) order -- whether or not the caller's event buffer has room:
+ *     undelivered events wait in the replica's queue for the next flush /
+ *     flush_poll, and GC (the committed prefix, a stable checkpoint) never
+ *     waits for delivery;
  *   - every candidate vote of a (kind, signer) is kept until one verifies (at
  *     most PBFT_MAX_CANDIDATES): a forged vote cannot pre-empt the real one
  *     (votes are keyed by the authenticated sender, so only the signer's own

@@ -402,14 +402,37 @@ static void gc(pbft_replica* r) {
       r->dirty.erase(it->first);
       it = drop_window(r, it);
       ++r->stats.windows_gc;
+    } else if (it->first.first == ~0ull) {
+      break;
     } else {
-      ++it;
+      // every later window of this view has a higher seq: on to the next view
+      it = r->windows.lower_bound({it->first.first + 1, 0});
     }
   }
 }
 
-// Events (pre-prepared, prepared :177-182, committed_local :214-223) of every dirty window, in (view, seq)
-// order, into the replica's queue: the decision is recorded whether or not the caller has room for it.
+// The events one window's state now decides (pre-prepared, prepared :177-182, committed_local :214-223), appended
+// to `out`; a committed window drops its stragglers (nothing of it may be in flight: callers guarantee that).
+template <class Out>
+static void evaluate_window(const pbft_replica* r, uint64_t view, uint64_t seq, Window& w, Out& out) {
+  if (!w.pre_prepared_reported && w.have_pre_prepare) {
+    w.pre_prepared_reported = true;
+    out.push_back({view, seq, PBFT_EVENT_PRE_PREPARED});
+  }
+  if (!w.prepared_reported && is_prepared(r, view, w)) {
+    w.prepared_reported = true;
+    out.push_back({view, seq, PBFT_EVENT_PREPARED});
+  }
+  if (!w.committed_reported && is_committed_local(r, view, w)) {
+    w.committed_reported = true;
+    out.push_back({view, seq, PBFT_EVENT_COMMITTED_LOCAL});
+    for (Phase& p : w.ph) p.clear_candidates();  // decided: stragglers are never needed
+  }
+}
+
+// Events of every dirty window, in (view, seq) order, into the replica's queue: the decision is recorded whether
+// or not the caller has room for it.  (Windows completed by a batch are evaluated as they are applied,
+// apply_range; `dirty` holds the rest.)
 static void evaluate(pbft_replica* r) {
   auto wi = r->windows.begin();
   for (const Key& k : r->dirty) {
@@ -419,22 +442,7 @@ static void evaluate(pbft_replica* r) {
       wi = (nx != r->windows.end() && nx->first >= k) ? nx : r->windows.lower_bound(k);
     }
     if (wi == r->windows.end() || wi->first != k) continue;
-    Window& w = wi->second;
-    const uint64_t view = k.first, seq = k.second;
-    if (!w.pre_prepared_reported && w.have_pre_prepare) {
-      w.pre_prepared_reported = true;
-      r->evq.push_back({view, seq, PBFT_EVENT_PRE_PREPARED});
-    }
-    if (!w.prepared_reported && is_prepared(r, view, w)) {
-      w.prepared_reported = true;
-      r->evq.push_back({view, seq, PBFT_EVENT_PREPARED});
-    }
-    if (!w.committed_reported && is_committed_local(r, view, w)) {
-      w.committed_reported = true;
-      r->evq.push_back({view, seq, PBFT_EVENT_COMMITTED_LOCAL});
-      // decided: stragglers are never needed (nothing is in flight while events are evaluated)
-      for (Phase& p : w.ph) p.clear_candidates();
-    }
+    evaluate_window(r, k.first, k.second, wi->second, r->evq);
   }
   r->dirty.clear();
 }
@@ -470,7 +478,8 @@ static void revert_segs(pbft_replica* r) {
 // wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
 // candidates leave the windows.  Segments [s0, s1) (whole windows: a window's segments stay on one thread, in
 // order); counts into st[3] = accepted, rejected_sig, rejected_digest; touched[g] = some candidate accepted.
-static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3], uint8_t* touched) {
+static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3], uint8_t* touched,
+                        std::vector<pbft_round_event>& events) {
   std::vector<int64_t> amap;
   std::vector<uint8_t> mism;
   uint64_t st[3] = {0, 0, 0};  // local: the threads' st_out entries share cache lines
@@ -555,6 +564,13 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
     st[1] += g.count - acc_n;
     p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
     touched[gi] = acc_n > 0;
+    // the window's last segment of this batch: its events are decided now, on this thread (segments come in
+    // (view, seq) order and a window's stay on one thread, so the threads' event lists concatenate in order)
+    if (gi + 1 == r->segs.size() || r->segs[gi + 1].key != g.key) {
+      bool any = false;
+      for (size_t gj = gi + 1; gj-- > 0 && r->segs[gj].key == g.key;) any = any || touched[gj];
+      if (any) evaluate_window(r, g.key.first, g.key.second, w, events);
+    }
   }
   for (int k = 0; k < 3; ++k) st_out[k] += st[k];
 }
@@ -578,8 +594,9 @@ static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
   const unsigned hw = std::thread::hardware_concurrency();
   const size_t T = nrows >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), s1 - s0) : 1;
   std::vector<std::array<uint64_t, 3>> st(T, {0, 0, 0});
+  std::vector<std::vector<pbft_round_event>> ev(T);
   if (T <= 1) {
-    apply_range(r, s0, s1, st[0].data(), r->touched.data());
+    apply_range(r, s0, s1, st[0].data(), r->touched.data(), ev[0]);
   } else {
     std::vector<size_t> cut(T + 1, s1);
     cut[0] = s0;
@@ -590,9 +607,10 @@ static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
       cut[t + 1] = b;
     }
     WorkerPool::get().run(T, [&](size_t t) {
-      if (cut[t + 1] > cut[t]) apply_range(r, cut[t], cut[t + 1], st[t].data(), r->touched.data());
+      if (cut[t + 1] > cut[t]) apply_range(r, cut[t], cut[t + 1], st[t].data(), r->touched.data(), ev[t]);
     });
   }
+  for (const auto& e : ev) r->evq.insert(r->evq.end(), e.begin(), e.end());
   for (const auto& c : st) {
     r->stats.accepted += c[0];
     r->stats.rejected_sig += c[1];
@@ -608,10 +626,9 @@ static void mark_dirty(pbft_replica* r) {
 }
 
 static void finish_batch(pbft_replica* r) {
-  apply_segs(r, r->seg_next, r->segs.size());
+  apply_segs(r, r->seg_next, r->segs.size());  // (windows evaluated as their last segments are applied)
   ++r->stats.batches;
   r->stats.verified += r->rows;
-  mark_dirty(r);
   r->segs.clear();
   r->seg_next = 0;
   r->in_flight = false;
@@ -657,12 +674,6 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
                            uint32_t E) {
   const size_t G = r->segs.size();
   const uint64_t N = r->rows;
-  fill_envs(r, 0, G, ENV);
-  int rc = pbft_verify_votes_submit_begin(r->ctx, N, E, r->bitmap.data());
-  if (rc) {
-    fill_rows(r, 0, G, SIG, K, IDX);  // (so that revert_segs finds every candidate in flight)
-    return rc;
-  }
   const size_t W = (size_t)((N + FILL_STEP - 1) / FILL_STEP);
   std::vector<size_t> cut(W + 1, G);  // step k = segments [cut[k], cut[k+1]): those starting below (k+1) FILL_STEP
   cut[0] = 0;
@@ -673,6 +684,7 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
   for (size_t k = 1; k < W; ++k) cut[k] = first_at(k * FILL_STEP);
   std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[W]);
   for (size_t k = 0; k < W; ++k) done[k].store(0, std::memory_order_relaxed);
+  // the workers start on the rows at once; this thread meanwhile writes the envelope table and opens the batch
   WorkerPool::get().start(T, [&](size_t t) {
       for (size_t k = 0; k < W; ++k) {
         const size_t a = cut[k], b = cut[k + 1];
@@ -685,6 +697,9 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
         done[k].fetch_add(1, std::memory_order_release);
       }
   });
+  fill_envs(r, 0, G, ENV);
+  RTRACE(r, "envs", E);
+  int rc = pbft_verify_votes_submit_begin(r->ctx, N, E, r->bitmap.data());
   RTRACE(r, "begin", N);
   for (size_t k = 0; k < W && rc == PBFT_OK; ++k) {
     while (done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
@@ -692,7 +707,7 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
     rc = pbft_verify_votes_submit_rows(r->ctx, cut[k + 1] < G ? r->segs[cut[k + 1]].row0 : N);
     RTRACE(r, "launched", k);
   }
-  WorkerPool::get().wait();
+  WorkerPool::get().wait();  // (on failure too: every candidate is then marked in flight, as revert_segs expects)
   return rc;
 }
 
@@ -1011,6 +1026,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   } else {
     pbft_votes_staging st{};
     rc = pbft_verify_votes_stage(r->ctx, N, E, &st);
+    RTRACE(r, "stage", rc);
     if (rc) { r->segs.clear(); return rc; }
     SIG = st.sig; K = st.key_idx; IDX = st.env_idx; ENV = st.envelopes;
   }

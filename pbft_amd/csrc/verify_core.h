@@ -123,7 +123,10 @@ FE_FN uint32_t lane_mask(bool c) {
 #define PBFT_MADD_V2 1
 #endif
 #ifndef PBFT_CHAIN_MIN_N
-#define PBFT_CHAIN_MIN_N (1u << 19)  // comb_kernel uses the single-chain multiplies (CHAIN) from this batch size
+// comb_kernel uses the single-chain multiplies (CHAIN) from this batch size.  r03: 2^19 (the per-mad laundering
+// asm made the chain form slower on one wave of blocks); r04, with one asm block per column: 2^16 (131k shard
+// 0.1878 -> 0.1859 ms, 2^20 unchanged; profiles/r04/ab_column_asm.txt)
+#define PBFT_CHAIN_MIN_N (1u << 16)
 #endif
 // 2p - k per limb for canonical k (the conditional negation of the entry's d*x*y)
 FE_FN void fe_cneg_canon(fe& out, const fe& k, uint32_t m) {
@@ -146,10 +149,10 @@ FE_FN void ge_madd_ab(ge& r, const ge& p, const fe& qa, const fe& qb, const fe& 
   fe_cneg_canon(kk, k, lane_mask(neg));
   fe_sub(t, p.Y, p.X);
   if constexpr (CHAIN) {
-    // The 3 + 4 products as interleaved single-chain multiplies (fe_mul_chain: no 64-bit carry adds).  Fewer
-    // VALU instructions (-55 per step) but longer dependency chains: faster when many blocks per CU overlap
-    // (2^20: -1.8 %), slower on a single wave of blocks (131k: +6 %), so launch_comb_plan picks it by size
-    // (profiles/r03/ab_chain_mul.txt).
+    // The 3 + 4 products as single-chain multiplies (fe_mul_chain: no 64-bit carry adds; -55 VALU per step).
+    // r03 (a laundering asm per mad): faster when many blocks per CU overlap (2^20: -1.8 %), slower on a single
+    // wave of blocks (131k: +6 %, profiles/r03/ab_chain_mul.txt); r04 (one asm block per column, no hazard
+    // s_nop): faster at 131k too (-1.0 %), so launch_comb_plan uses it from PBFT_CHAIN_MIN_N = 2^16.
     fe t2;
     fe_add(t2, p.Y, p.X);
     {

@@ -43,6 +43,10 @@ int pbft_verify_batch(pbft_ctx*, const uint8_t*, const uint8_t*, const uint16_t*
 int pbft_digest_blake2b512(pbft_ctx*, const uint8_t*, const uint64_t*, const uint32_t*, uint64_t, uint8_t*) {
   return PBFT_ENODEV;
 }
+int pbft_verify_update_keys(pbft_ctx*, const uint32_t*, const uint8_t*, uint32_t m, uint8_t* key_ok) {
+  if (key_ok) memset(key_ok, 1, m);
+  return PBFT_OK;
+}
 }
 
 // A fake GPU context for the replica's progressive votes path (pbft_verify_votes_stage / _submit_begin / _rows /
@@ -612,9 +616,13 @@ static void test_replica_progressive() {
   CHECK(pbft_replica_push(r, PBFT_KIND_COMMIT, 1, 1000, d, 3, sg) == 1);
   while ((st = pbft_replica_flush_poll(r, ev.data(), (uint32_t)ev.size(), &ne)) == 0) ++polls;
   CHECK(st == 1 && polls >= 1);
+  // (events of seqs <= 10 were decided when the first chunk was applied, before the checkpoint erased their
+  // windows: they are delivered, as any decided event is; seq 7 never had a prepare quorum)
   uint32_t prepared = 0, committed = 0;
   for (uint32_t e = 0; e < ne; ++e) {
-    CHECK(ev[e].seq > 10);
+    CHECK(ev[e].seq != 7 || ev[e].kind == PBFT_EVENT_PRE_PREPARED);
+    if (e) CHECK(ev[e].seq >= ev[e - 1].seq);  // delivered in (view, seq) order
+    if (ev[e].seq <= 10) continue;
     if (ev[e].kind == PBFT_EVENT_PREPARED) ++prepared;
     if (ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL) { ++committed; CHECK(ev[e].seq != 900); }
   }

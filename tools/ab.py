@@ -2,7 +2,8 @@
 """Interleaved A/B timing of verify_kernel builds in ONE process (cdna guide §5.4 rule 24).
 
 usage: python tools/ab.py lib1.so lib2.so[@opt=value,...] ... [--rounds 8 --iters 10 --budget-mb X]
-Each lib gets its own context on the same synthetic 2^20-signature round; `@2=4,4=6,8=2` sets
+Each lib gets its own context (and its own 30-GB base-point table: with several libs give each a key-table
+budget, e.g. @3=20000 = the 16-position plan, or the second lib cannot allocate) on the same synthetic 2^20-signature round; `@2=4,4=6,8=2` sets
 pbft_verify_set_option(option, value) pairs on that context (the same library may appear with different options).
 """
 import argparse
