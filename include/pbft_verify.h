@@ -176,6 +176,19 @@ int pbft_verify_votes_submit(pbft_ctx *ctx, uint64_t N, uint32_t n_env, uint64_t
  * pbft_replica_flush_submit / _flush_poll use this.  Until _submit_rows(N) pbft_verify_poll reports "running"
  * and pbft_verify_wait fails with PBFT_EBUSY; a failing _submit_rows drops the batch. */
 int pbft_verify_votes_submit_begin(pbft_ctx *ctx, uint64_t N, uint32_t n_env, uint64_t *bitmap_out);
+/* Chunk schedule of the votes forms from host buffers (each chunk: its H2D on the copy stream, its kernels, and in
+ * the progressive form its bitmap words back): a batch of at most PBFT_VOTES_CHUNK_ROWS rows is one chunk; a larger
+ * one starts with a PBFT_VOTES_FIRST_ROWS-row chunk and a 2 x PBFT_VOTES_FIRST_ROWS-row one, so that the first copy
+ * starts after a small part of the rows is filled, then PBFT_VOTES_CHUNK_ROWS-row chunks.  The chunk starting at
+ * row lo of an n-row batch ends at PBFT_VOTES_CHUNK_END(lo, n). */
+#define PBFT_VOTES_CHUNK_ROWS (1u << 18)
+#define PBFT_VOTES_FIRST_ROWS (1u << 16)
+#define PBFT_VOTES_CHUNK_SIZE_AT(lo) \
+  ((lo) == 0 ? PBFT_VOTES_FIRST_ROWS : (lo) == PBFT_VOTES_FIRST_ROWS ? 2 * PBFT_VOTES_FIRST_ROWS : PBFT_VOTES_CHUNK_ROWS)
+#define PBFT_VOTES_CHUNK_END(lo, n)                                                            \
+  ((uint64_t)(n) <= PBFT_VOTES_CHUNK_ROWS                                   ? (uint64_t)(n)  \
+   : (uint64_t)(lo) + PBFT_VOTES_CHUNK_SIZE_AT(lo) < (uint64_t)(n) ? (uint64_t)(lo) + PBFT_VOTES_CHUNK_SIZE_AT(lo) \
+                                                                   : (uint64_t)(n))
 int pbft_verify_votes_submit_rows(pbft_ctx *ctx, uint64_t rows);
 int pbft_verify_poll_rows(pbft_ctx *ctx, uint64_t *rows_done);
 

@@ -665,23 +665,24 @@ static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
   fill_rows(r, s0, s1, SIG, K, IDX);
 }
 
-// rows of one progressive step (the verify library's votes chunk, include/pbft_verify.h)
-static constexpr uint64_t FILL_STEP = 1ull << 18;
 
-// GPU path of a large batch: envelopes, then the rows in FILL_STEP steps on T threads while this thread launches
+// GPU path of a large batch: envelopes, then the rows in steps (the library's votes chunks) on T threads while this thread launches
 // each step as soon as it is filled (pbft_verify_votes_submit_rows): the fill overlaps the copies and kernels.
 static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV,
                            uint32_t E) {
   const size_t G = r->segs.size();
   const uint64_t N = r->rows;
-  const size_t W = (size_t)((N + FILL_STEP - 1) / FILL_STEP);
-  std::vector<size_t> cut(W + 1, G);  // step k = segments [cut[k], cut[k+1]): those starting below (k+1) FILL_STEP
+  // one fill step per chunk of the library's votes schedule (PBFT_VOTES_CHUNK_END, include/pbft_verify.h)
+  std::vector<uint64_t> ends;
+  for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ends.push_back(PBFT_VOTES_CHUNK_END(lo, N));
+  const size_t W = ends.size();
+  std::vector<size_t> cut(W + 1, G);  // step k = segments [cut[k], cut[k+1]): those starting below ends[k]
   cut[0] = 0;
   auto first_at = [&](uint64_t row) {
     return (size_t)(std::lower_bound(r->segs.begin(), r->segs.end(), row,
                                      [](const Seg& g, uint64_t x) { return g.row0 < x; }) - r->segs.begin());
   };
-  for (size_t k = 1; k < W; ++k) cut[k] = first_at(k * FILL_STEP);
+  for (size_t k = 1; k < W; ++k) cut[k] = first_at(ends[k - 1]);
   std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[W]);
   for (size_t k = 0; k < W; ++k) done[k].store(0, std::memory_order_relaxed);
   // the workers start on the rows at once; this thread meanwhile writes the envelope table and opens the batch

@@ -189,6 +189,7 @@ struct pbft_ctx {
   bool v_readback = false;  // progressive: each chunk's bitmap words come back on their own (ev_rows)
   std::vector<hipEvent_t> ev_rows;  // per chunk: its bitmap words are in h_bitmap
   uint64_t rows_out = 0;            // rows whose bitmap words are in the caller's bitmap
+  uint64_t chunk_out = 0;           // chunks whose bitmap words are in the caller's bitmap
 };
 
 #ifndef PBFT_ENV_SCHED
@@ -406,9 +407,8 @@ struct stage_layout {
 #ifndef PBFT_PIPE_CHUNK_LOG2
 #define PBFT_PIPE_CHUNK_LOG2 18
 #endif
-#ifndef PBFT_VOTES_CHUNK_LOG2
-#define PBFT_VOTES_CHUNK_LOG2 18
-#endif
+#define PBFT_VOTES_CHUNK_LOG2 18  // PBFT_VOTES_CHUNK_ROWS (include/pbft_verify.h: the replica follows the schedule)
+static_assert(PBFT_VOTES_CHUNK_ROWS == (1u << PBFT_VOTES_CHUNK_LOG2) && PBFT_VOTES_FIRST_ROWS % 64 == 0, "");
 // chunks own whole 64-bit bitmap words (the kernels write d_bitmap + lo / 64, readbacks copy (n + 63) / 64 words)
 static_assert(PBFT_PIPE_CHUNK_LOG2 >= 6 && PBFT_VOTES_CHUNK_LOG2 >= 6, "chunks must be multiples of 64 rows");
 static constexpr uint64_t PIPE_CHUNK = 1ull << PBFT_PIPE_CHUNK_LOG2;
@@ -512,7 +512,8 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   int rc = ensure_stage(c, env_bytes + (N > VOTES_CHUNK ? 2 : 1) * L.bytes, words);
   if (rc) return rc;
   if (readback) {
-    const uint64_t chunks = (N + VOTES_CHUNK - 1) / VOTES_CHUNK;
+    uint64_t chunks = 0;
+    for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ++chunks;
     while (c->ev_rows.size() < chunks) {
       hipEvent_t e;
       HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -534,6 +535,7 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   c->v_open = true;
   c->v_readback = readback;
   c->rows_out = 0;
+  c->chunk_out = 0;
   return PBFT_OK;
 }
 
@@ -541,9 +543,9 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
                         uint32_t rs_stride, uint64_t rows) {
   const uint64_t N = c->v_n;
   const votes_layout L(N < VOTES_CHUNK ? N : VOTES_CHUNK);
-  while (c->v_next < N && (rows >= N || c->v_next + VOTES_CHUNK <= rows)) {
+  while (c->v_next < N && (rows >= N || PBFT_VOTES_CHUNK_END(c->v_next, N) <= rows)) {
     const uint64_t lo = c->v_next;
-    const uint64_t n = N - lo < VOTES_CHUNK ? N - lo : VOTES_CHUNK;
+    const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
     const int b = (int)(c->v_chunk & 1);
     uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
     if (c->v_chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
@@ -1049,16 +1051,17 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (c->in_flight && c->v_readback) {
     while (c->rows_out < c->v_next) {  // launched chunks whose bitmap words have landed, in order
-      const hipError_t e = hipEventQuery(c->ev_rows[c->rows_out / VOTES_CHUNK]);
+      const hipError_t e = hipEventQuery(c->ev_rows[c->chunk_out]);
       if (e == hipErrorNotReady) break;
       if (e != hipSuccess) {
         c->in_flight = false;
         c->v_open = false;
         HIP_TRY(e);
       }
-      const uint64_t hi = c->rows_out + VOTES_CHUNK < c->v_n ? c->rows_out + VOTES_CHUNK : c->v_n;
+      const uint64_t hi = PBFT_VOTES_CHUNK_END(c->rows_out, c->v_n);
       memcpy(c->async_out + c->rows_out / 64, c->h_bitmap + c->rows_out / 64, (hi - c->rows_out + 63) / 64 * 8);
       c->rows_out = hi;
+      ++c->chunk_out;
     }
     if (c->v_open || c->rows_out < c->v_n) {
       if (rows_done) *rows_done = c->rows_out;

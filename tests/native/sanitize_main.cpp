@@ -51,7 +51,7 @@ int pbft_verify_update_keys(pbft_ctx*, const uint32_t*, const uint8_t*, uint32_t
 
 // A fake GPU context for the replica's progressive votes path (pbft_verify_votes_stage / _submit_begin / _rows /
 // pbft_verify_poll_rows): exactly-sized staging, key_idx pre-set to a sentinel so that a chunk launched before
-// its rows were filled is caught, and one 2^18-row chunk "completing" per poll.  A row verifies iff its
+// its rows were filled is caught, and one chunk of the library's schedule (PBFT_VOTES_CHUNK_END) "completing" per poll.  A row verifies iff its
 // signature's first byte is not 0xEE (no curve arithmetic: the point is the host's threads and bookkeeping).
 struct FakeGpu {
   std::vector<uint8_t> sig, env;
@@ -63,7 +63,6 @@ struct FakeGpu {
   bool staged = false, open = false, in_flight = false;
   uint64_t batches = 0, chunk_launches = 0;
 };
-static constexpr uint64_t FAKE_CHUNK = 1ull << 18;
 
 extern "C" {
 int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_staging* st) {
@@ -89,7 +88,9 @@ int pbft_verify_votes_submit_begin(pbft_ctx* c, uint64_t N, uint32_t n_env, uint
 int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   FakeGpu* g = (FakeGpu*)c;
   CHECK(g && g->open);
-  const uint64_t upto = rows >= g->N ? g->N : rows / FAKE_CHUNK * FAKE_CHUNK;
+  uint64_t upto = g->launched;  // every whole chunk of the library's schedule inside [0, rows)
+  while (upto < g->N && PBFT_VOTES_CHUNK_END(upto, g->N) <= (rows >= g->N ? g->N : rows))
+    upto = PBFT_VOTES_CHUNK_END(upto, g->N);
   for (uint64_t i = g->launched; i < upto; ++i) CHECK(g->K[i] != 0xFFFF && g->I[i] < g->n_env);  // filled
   if (upto > g->launched) { g->launched = upto; ++g->chunk_launches; }
   if (g->launched == g->N) g->open = false;
@@ -99,7 +100,7 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   FakeGpu* g = (FakeGpu*)c;
   if (!g->in_flight) { *rows_done = g->N; return 1; }
   if (g->done < g->launched) {  // one more chunk "lands"
-    const uint64_t hi = g->done + FAKE_CHUNK < g->launched ? g->done + FAKE_CHUNK : g->launched;
+    const uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
     for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
     for (uint64_t i = g->done; i < hi; ++i)
       if (g->sig[64 * i] != 0xEE && g->K[i] < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
