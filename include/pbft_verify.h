@@ -262,7 +262,7 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *   PBFT_OPT_LAT_SPLIT            lanes per signature of the latency-mode kernel: 4 or 8; any other value = by
  *                                 batch size (8 up to 8,192 signatures, else 4)
  *   PBFT_OPT_FINISH_WAVES         product-tree finish compiled for 1 wave per SIMD (widths 1-16, X/Y/Z prefetched)
- *                                 or 2 (widths 2, 4, 8); any other value = by batch size
+ *                                 or 2 (widths 1, 2, 4, 8; width 1 prefetched); any other value = by batch size
  *   PBFT_OPT_KERNEL_TIMING        1 (default): two HIP events bracket every launch for pbft_last_kernel_ms; 0: none
  *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers) */
 #define PBFT_OPT_SPLIT_BELOW 1

@@ -65,6 +65,27 @@ extern "C" int pbft_debug_fin_stamps(uint64_t* out, uint32_t waves) {
 #define FIN_STAMP(k)
 #endif
 
+#ifndef PBFT_FIN_DPP
+#define PBFT_FIN_DPP 0  // 1: product-tree partners by DPP / ds_swizzle instead of ds_bpermute (r04 A/B: no difference)
+#endif
+// The partner of this lane at butterfly level k of a product tree over the wave: any involution that pairs the
+// level's two 2^k-lane halves of every 2^(k+1)-lane group works (after level k every lane holds the product of
+// its group).  Levels 0-3 in-row DPP (quad_perm [1,0,3,2] / [2,3,0,1], row_half_mirror l -> 7-l, row_mirror
+// l -> 15-l: a VALU op, no LDS round trip), level 4 ds_swizzle xor 16 (no LDS memory access), level 5
+// ds_bpermute xor 32.
+template <int K>
+__device__ __forceinline__ uint32_t tree_partner(uint32_t v) {
+#if PBFT_FIN_DPP
+  if constexpr (K == 0) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (K == 1) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (K == 2) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, false);
+  else if constexpr (K == 3) return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, false);
+  else if constexpr (K == 4) return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (0x10 << 10) | 0x1F);
+  else
+#endif
+    return (uint32_t)__shfl_xor((int)v, 1 << K);
+}
+
 // W: waves per SIMD the kernel is compiled for (register budget 512 / W); the prefetch of X, Y, Z needs W = 1
 template <int FM, int LV, int W>
 __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restrict__ R,
@@ -99,7 +120,7 @@ __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restr
   fe pre[FM];
   // PRE: small FM keeps every Z and issues the X, Y loads before the inversion, so the back-substitution
   // does not wait on memory (FM <= 4: ~100 more VGPRs, within the 2-waves-per-SIMD budget)
-  constexpr bool PRE = PBFT_FIN_PREFETCH && FM <= 4 && W == 1;
+  constexpr bool PRE = PBFT_FIN_PREFETCH && ((FM <= 4 && W == 1) || FM == 1);
   fe zs[PRE ? FM : 1], xs[PRE ? FM : 1], ys[PRE ? FM : 1];
   fin_unroll<FM>::up([&](auto mc) {
     constexpr int m = decltype(mc)::value;
@@ -122,7 +143,7 @@ __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restr
   static_for<LV>([&](auto kc) {
     constexpr int k = decltype(kc)::value;
 #pragma unroll
-    for (int u = 0; u < 10; ++u) tq[k].v[u] = (uint32_t)__shfl_xor((int)t.v[u], 1 << k);
+    for (int u = 0; u < 10; ++u) tq[k].v[u] = tree_partner<k>(t.v[u]);
     fe_mul(t, t, tq[k]);
   });
   FIN_STAMP(2);
@@ -215,10 +236,11 @@ hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_st
     else if (fm == 4) PBFT_LAUNCH_FIN(4, 0, FIN_WAVES_PER_EU);
     else if (fm == 2) PBFT_LAUNCH_FIN(2, 0, FIN_WAVES_PER_EU);
     else PBFT_LAUNCH_FIN(1, 0, FIN_WAVES_PER_EU);
-  } else if (w >= 2) {  // product tree at two waves per SIMD (no prefetch): large rounds
+  } else if (w >= 2) {  // product tree at two waves per SIMD (prefetch at width 1 only): large rounds, small shards
     if (fm >= 8) PBFT_LAUNCH_FIN(8, 6, 2);
     else if (fm == 4) PBFT_LAUNCH_FIN(4, 6, 2);
-    else PBFT_LAUNCH_FIN(2, 6, 2);
+    else if (fm == 2) PBFT_LAUNCH_FIN(2, 6, 2);
+    else PBFT_LAUNCH_FIN(1, 6, 2);
   } else {
     if (fm == 16) PBFT_LAUNCH_FIN(16, 6, 1);
     else if (fm == 8) PBFT_LAUNCH_FIN(8, 6, 1);

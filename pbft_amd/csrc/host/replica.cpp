@@ -926,6 +926,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //  1. (threads, by input slices) the per-row checks that need no window, and runs of consecutive rows with
     //     one (view, seq); rejected rows are flagged and do not break a run;
     struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; };
+    RTRACE(r, "push", n_ok);
     std::vector<std::vector<Run>> slice_runs(T);
     std::vector<uint8_t> bad(n_ok);
     std::vector<PushCounts> cnt(T);
@@ -944,6 +945,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     });
     //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
     //     owner: the thread whose share of the rows its first run starts in;
+    RTRACE(r, "push_checked", T);
     std::vector<Run> runs;
     for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
     std::unordered_map<Window*, uint32_t> owner;
@@ -953,6 +955,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       auto it = owner.emplace(u.w, (uint32_t)(u.lo * T / n_ok)).first;
       u.owner = it->second;
     }
+    RTRACE(r, "push_windows", runs.size());
     //  3. (threads) every thread pushes the rows of the windows it owns, in input order.
     WorkerPool::get().run(T, [&](size_t t) {
       PushCounts& c = cnt[t];
@@ -966,6 +969,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       add_counts(r, c);
       q += c.queued;
     }
+    RTRACE(r, "push_done", q);
   }
   if (queued) *queued = q;
   return n_ok < N ? PBFT_EINVAL : PBFT_OK;

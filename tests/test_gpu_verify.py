@@ -606,7 +606,8 @@ def test_progressive_votes_submit(gv, coracle):
     """pbft_verify_votes_submit_begin / _rows + pbft_verify_poll_rows (what pbft_replica_flush_submit and
     _flush_poll use): the staging is launched chunk by chunk as it is filled, each chunk's bitmap words come back
     on their own; until the last rows are submitted the batch reads "running" and a blocking wait is refused.
-    2^19 + 3 rows = chunks of 2^18, 2^18 and 3; every prefix reported done equals the oracle."""
+    2^19 + 3 rows = chunks [0, 2^16), [2^16, 3 * 2^16), [3 * 2^16, 7 * 2^16), [7 * 2^16, 2^19 + 3) (the schedule of
+    include/pbft_verify.h PBFT_VOTES_CHUNK_END); every prefix reported done equals the oracle."""
     import ctypes
     from pbft_amd import PbftError, bitmap_to_bool
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=47)   # 65,536 signatures
@@ -628,21 +629,22 @@ def test_progressive_votes_submit(gv, coracle):
     h = 1 << 18
     st["sig"][:h, :32], st["sig"][:h, 32:], st["key_idx"][:h], st["env_idx"][:h] = RR[:h], SS[:h], KK[:h], II[:h]
     assert L.pbft_verify_votes_submit_begin(ctx, N, len(env), out.ctypes.data) == 0
+    ends = [1 << 16, 3 << 16, 7 << 16, N]
     assert L.pbft_verify_votes_submit_rows(ctx, 1000) == 0                # no whole chunk yet
-    assert L.pbft_verify_votes_submit_rows(ctx, h + 5) == 0               # chunk 0
+    assert L.pbft_verify_votes_submit_rows(ctx, h + 5) == 0               # chunks 0 and 1 (the filled rows' whole chunks)
     assert L.pbft_verify_poll(ctx) == 0
     with pytest.raises(PbftError):
         from pbft_amd._lib import check
         check(L.pbft_verify_wait(ctx))
     seen = 0
-    while seen < h:
+    while seen < ends[1]:
         assert L.pbft_verify_poll_rows(ctx, ctypes.byref(rows_done)) == 0
-        assert rows_done.value in (0, h)
+        assert rows_done.value in (0, ends[0], ends[1])
         seen = rows_done.value
-    assert (bitmap_to_bool(out[: h // 64], h) == EE[:h]).all()
+    assert (bitmap_to_bool(out[: seen // 64], seen) == EE[:seen]).all()
     st["sig"][h:, :32], st["sig"][h:, 32:], st["key_idx"][h:], st["env_idx"][h:] = RR[h:], SS[h:], KK[h:], II[h:]
     assert L.pbft_verify_votes_submit_rows(ctx, N) == 0
-    prev = h
+    prev = seen
     while True:
         rc = L.pbft_verify_poll_rows(ctx, ctypes.byref(rows_done))
         assert rc in (0, 1) and rows_done.value >= prev

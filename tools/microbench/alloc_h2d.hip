@@ -1,7 +1,9 @@
 // Host-side costs on MI355X that bound the key-set install and the replica flush (round 4 probes):
 //  1. hipMalloc of large device buffers (the 172-GB key tables), against hipExtMallocWithFlags and
 //     hipMallocAsync on the default pool;
-//  2. H2D bandwidth from pinned host memory: one stream, two streams (two SDMA queues), several chunk sizes.
+//  2. H2D bandwidth from pinned host memory: one stream, two streams (two SDMA queues), several chunk sizes;
+//  3. a kernel reading pinned host memory directly (zero-copy gather of 64-B rows, as a replica's candidate rows
+//     would be gathered) into device memory.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -12,6 +14,19 @@
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e)); return 1; } } while (0)
 static double ms_since(std::chrono::steady_clock::time_point t) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// each lane copies one 64-B row (4 x 16 B); rows in 256-row runs at scattered host offsets (a segment table)
+__global__ void gather_rows(const uint4* __restrict__ host, const uint32_t* __restrict__ run_src, uint4* __restrict__ dev,
+                            uint64_t rows) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= rows) return;
+  const uint64_t src = (uint64_t)run_src[i >> 8] * 256 + (i & 255);
+  const uint4* s = host + 4 * src;
+  uint4* d = dev + 4 * i;
+  const uint4 a = s[0], b = s[1];
+  const uint4 c = s[2], e = s[3];
+  d[0] = a; d[1] = b; d[2] = c; d[3] = e;
 }
 
 int main(int argc, char** argv) {
@@ -53,6 +68,31 @@ int main(int argc, char** argv) {
     printf("hipMallocAsync %zu GB: %.1f ms, hipFreeAsync %.1f ms\n", big / GB, a, ms_since(t));
     CK(hipStreamDestroy(s));
   }
+  {  // the verifier's sequence: the 30-GB base-point table, then 172 GB of key tables (n = 256 at 13 positions)
+    void *b = nullptr, *k = nullptr;
+    auto t = std::chrono::steady_clock::now();
+    CK(hipMalloc(&b, 30 * GB));
+    double a1 = ms_since(t);
+    t = std::chrono::steady_clock::now();
+    CK(hipMalloc(&k, 172 * GB));
+    double a2 = ms_since(t);
+    t = std::chrono::steady_clock::now();
+    CK(hipMemsetAsync(k, 0, 172 * GB, 0));
+    CK(hipDeviceSynchronize());
+    double a3 = ms_since(t);
+    t = std::chrono::steady_clock::now();
+    CK(hipMemsetAsync(k, 1, 172 * GB, 0));
+    CK(hipDeviceSynchronize());
+    double a4 = ms_since(t);
+    CK(hipFree(k));
+    t = std::chrono::steady_clock::now();
+    CK(hipMalloc(&k, 172 * GB));
+    double a5 = ms_since(t);
+    CK(hipFree(k));
+    CK(hipFree(b));
+    printf("hipMalloc 30 GB %.1f ms, then 172 GB %.1f ms; first memset of the 172 GB %.1f ms, second %.1f ms; "
+           "re-allocation after free %.1f ms\n", a1, a2, a3, a4, a5);
+  }
   {  // many 1-GB pieces: is the cost per byte or per call?
     std::vector<void*> ps(16);
     auto t = std::chrono::steady_clock::now();
@@ -86,6 +126,32 @@ int main(int argc, char** argv) {
       }
       printf("H2D %zu MB in %zu-MB chunks on %d stream(s): %.3f ms = %.1f GB/s\n", bytes >> 20, chunk >> 20, streams,
              best, bytes / 1e6 / best);
+    }
+  }
+  {  // zero-copy gather: 2^20 rows of 64 B from pinned host memory, runs of 256 rows in a shuffled order
+    const uint64_t rows = 1ull << 20;
+    uint4 *hs = nullptr, *ds = nullptr;
+    uint32_t* runs = nullptr;
+    CK(hipHostMalloc(&hs, rows * 64, hipHostMallocDefault));
+    CK(hipMalloc(&ds, rows * 64));
+    CK(hipMalloc(&runs, 4 * (rows / 256)));
+    std::vector<uint32_t> perm(rows / 256);
+    for (uint32_t k = 0; k < perm.size(); ++k) perm[k] = k;
+    for (uint32_t k = (uint32_t)perm.size() - 1; k > 0; --k) std::swap(perm[k], perm[(k * 2654435761u) % (k + 1)]);
+    CK(hipMemcpy(runs, perm.data(), 4 * perm.size(), hipMemcpyHostToDevice));
+    memset(hs, 3, rows * 64);
+    for (int blk : {256, 1024}) {
+      double best = 1e9;
+      for (int rep = 0; rep < 8; ++rep) {
+        CK(hipDeviceSynchronize());
+        auto t = std::chrono::steady_clock::now();
+        hipLaunchKernelGGL(gather_rows, dim3((unsigned)((rows + blk - 1) / blk)), dim3(blk), 0, s0, hs, runs, ds, rows);
+        CK(hipStreamSynchronize(s0));
+        double m = ms_since(t);
+        if (m < best) best = m;
+      }
+      printf("zero-copy gather kernel, 2^20 x 64-B rows (256-row runs, shuffled), block %d: %.3f ms = %.1f GB/s\n",
+             blk, best, rows * 64 / 1e6 / best);
     }
   }
   return 0;
