@@ -933,15 +933,29 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     WorkerPool::get().run(T, [&](size_t t) {
       const uint64_t lo = n_ok * t / T, hi = n_ok * (t + 1) / T;
       std::vector<Run>& runs = slice_runs[t];
-      PushCounts& c = cnt[t];
+      // (locals: the byte stores below may alias anything, which would reload every field per row)
+      const uint32_t n = r->n;
+      const uint64_t cur = r->current_view, h = r->h, win = r->log_window;
+      uint64_t rv = 0, rw = 0, run_seq = ~0ull, run_lo = 0;
+      uint8_t* bd = bad.data();
       for (uint64_t i = lo; i < hi; ++i) {
-        ++c.pushed;
-        if (signer[i] >= r->n || view[i] != r->current_view) { ++c.rejected_view; bad[i] = 1; continue; }
-        if (!in_log(r, seq[i])) { ++c.rejected_watermark; bad[i] = 1; continue; }
-        bad[i] = 0;
-        if (runs.empty() || runs.back().seq != seq[i]) runs.push_back({i, i + 1, seq[i], nullptr, 0});
-        else runs.back().hi = i + 1;
+        const uint64_t q = seq[i];
+        const bool v_bad = signer[i] >= n || view[i] != cur;
+        const bool w_bad = !v_bad && !(q > h && q - h <= win);
+        rv += v_bad;
+        rw += w_bad;
+        bd[i] = v_bad | w_bad;
+        if (v_bad | w_bad) continue;
+        if (q != run_seq) {
+          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0});
+          run_seq = q;
+          run_lo = i;
+        }
       }
+      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0});
+      cnt[t].pushed += hi - lo;
+      cnt[t].rejected_view += rv;
+      cnt[t].rejected_watermark += rw;
     });
     //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
     //     owner: the thread whose share of the rows its first run starts in;
