@@ -59,10 +59,12 @@ int pbft_verify_ctx_destroy(pbft_ctx *ctx);
  * rejects small-order keys, and builds each key's -A comb table in HBM.
  * key_ok (optional, n bytes): 1 = key usable, 0 = every signature under it
  * rejects (bad encoding or small order).  Replaces any previous key set.
- * A re-key with the same comb plan and at most as many keys as the current
- * set's allocation reuses that allocation (tables rebuilt in place; no HBM
- * freed or allocated) unless a clone shares the set; a plan change frees the
- * old tables first.  The context is busy (blocking call) throughout. */
+ * A re-key whose tables fit the current set's allocation (at most as many
+ * keys, same or smaller comb plan) reuses that allocation (tables rebuilt in
+ * place; no HBM freed or allocated: freed VRAM is wiped by the driver before it
+ * can be handed out again, seconds for a key set) unless a clone shares the
+ * set; otherwise the old tables are freed first.  The context is busy
+ * (blocking call) throughout. */
 int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *key_ok);
 
 /* Replace m keys of the installed set: key idx[i] (< n, distinct) becomes

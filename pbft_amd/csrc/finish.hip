@@ -65,6 +65,11 @@ extern "C" int pbft_debug_fin_stamps(uint64_t* out, uint32_t waves) {
 #define FIN_STAMP(k)
 #endif
 
+#ifndef PBFT_FIN_LV
+#define PBFT_FIN_LV 4  // product-tree levels: 4 = one inversion per 16-lane row (fe_invert_wave<true>), 6 = one per wave
+                       // (r04 A/B, profiles/r04/ab_fin_lv4.txt: 131k shard -1.8 %, 2^20 -0.4 %)
+#endif
+static_assert(PBFT_FIN_LV == 4 || PBFT_FIN_LV == 6, "");
 #ifndef PBFT_FIN_DPP
 #define PBFT_FIN_DPP 0  // 1: product-tree partners by DPP / ds_swizzle instead of ds_bpermute (r04 A/B: no difference)
 #endif
@@ -97,10 +102,10 @@ __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restr
   const uint64_t wave = ((uint64_t)blockIdx.x * BLOCK + threadIdx.x) >> 6;
   const uint64_t base = wave * FM * 64 + lane;
 #if FIN_USE_TAB
-  // LV = 6: the divstep table (inv25519.h) goes to LDS; every wave of the block copies its share and meets the
+  // LV > 0: the divstep table (inv25519.h) goes to LDS; every wave of the block copies its share and meets the
   // one barrier before the inversion (waves past N included, so the barrier count always matches)
-  __shared__ uint64_t ds_tab[LV == 6 ? DS_TAB_ENTRIES : 1];
-  if constexpr (LV == 6) {
+  __shared__ uint64_t ds_tab[LV > 0 ? DS_TAB_ENTRIES : 1];
+  if constexpr (LV > 0) {
     const uint4* src = (const uint4*)g_ds_tab.e;
     uint4* dst = (uint4*)ds_tab;
 #pragma unroll
@@ -152,22 +157,26 @@ __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restr
 #elif PBFT_FIN_EXP  // A/B: z^(p-2) with latency-oriented carries
   fe_invert<true>(inv, t);
 #else
-  if constexpr (LV == 6) {
-    // every lane holds the wave's product: the variable-time divsteps never diverge (inv25519.h)
+  if constexpr (LV > 0) {
+    // every lane holds the product of its wave (LV 6) or row (LV 4): the variable-time divsteps never diverge
+    // (inv25519.h)
 #if FIN_USE_TAB
     __syncthreads();  // the block's divstep table is in LDS
-    #if PBFT_INV_WAVE
-    fe_invert_wave(inv, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
+#if PBFT_INV_WAVE
+    fe_invert_wave<(LV < 6)>(inv, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
 #else
+    static_assert(LV == 6, "");
     fe_invert_tab(inv, t, ds_tab);
 #endif
 #elif PBFT_FIN_STAMPS
+    static_assert(LV == 6, "");
     uint64_t prof[3];
     fe_invert_var(inv, t, prof);
     if (lane == 0 && wave < FIN_STAMP_WAVES) {
       g_fin_stamp[wave][8] = prof[0]; g_fin_stamp[wave][9] = prof[1]; g_fin_stamp[wave][10] = prof[2];
     }
 #else
+    static_assert(LV == 6, "");
     fe_invert_var(inv, t);
 #endif
   } else {
@@ -237,16 +246,16 @@ hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_st
     else if (fm == 2) PBFT_LAUNCH_FIN(2, 0, FIN_WAVES_PER_EU);
     else PBFT_LAUNCH_FIN(1, 0, FIN_WAVES_PER_EU);
   } else if (w >= 2) {  // product tree at two waves per SIMD (prefetch at width 1 only): large rounds, small shards
-    if (fm >= 8) PBFT_LAUNCH_FIN(8, 6, 2);
-    else if (fm == 4) PBFT_LAUNCH_FIN(4, 6, 2);
-    else if (fm == 2) PBFT_LAUNCH_FIN(2, 6, 2);
-    else PBFT_LAUNCH_FIN(1, 6, 2);
+    if (fm >= 8) PBFT_LAUNCH_FIN(8, PBFT_FIN_LV, 2);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4, PBFT_FIN_LV, 2);
+    else if (fm == 2) PBFT_LAUNCH_FIN(2, PBFT_FIN_LV, 2);
+    else PBFT_LAUNCH_FIN(1, PBFT_FIN_LV, 2);
   } else {
-    if (fm == 16) PBFT_LAUNCH_FIN(16, 6, 1);
-    else if (fm == 8) PBFT_LAUNCH_FIN(8, 6, 1);
-    else if (fm == 4) PBFT_LAUNCH_FIN(4, 6, 1);
-    else if (fm == 2) PBFT_LAUNCH_FIN(2, 6, 1);
-    else PBFT_LAUNCH_FIN(1, 6, 1);
+    if (fm == 16) PBFT_LAUNCH_FIN(16, PBFT_FIN_LV, 1);
+    else if (fm == 8) PBFT_LAUNCH_FIN(8, PBFT_FIN_LV, 1);
+    else if (fm == 4) PBFT_LAUNCH_FIN(4, PBFT_FIN_LV, 1);
+    else if (fm == 2) PBFT_LAUNCH_FIN(2, PBFT_FIN_LV, 1);
+    else PBFT_LAUNCH_FIN(1, PBFT_FIN_LV, 1);
   }
 #undef PBFT_LAUNCH_FIN
   return hipGetLastError();

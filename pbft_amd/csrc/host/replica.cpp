@@ -685,8 +685,12 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
   for (size_t k = 1; k < W; ++k) cut[k] = first_at(ends[k - 1]);
   std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[W]);
   for (size_t k = 0; k < W; ++k) done[k].store(0, std::memory_order_relaxed);
-  // the workers start on the rows at once; this thread meanwhile writes the envelope table and opens the batch
+  std::atomic<uint32_t> envs_done{0};
+  // the workers write the envelope table first (their share of the segments: one cache miss per window, 0.6 ms
+  // on one thread), then the rows step by step; this thread opens the batch once the table is complete
   WorkerPool::get().start(T, [&](size_t t) {
+      fill_envs(r, G * t / T, G * (t + 1) / T, ENV);
+      envs_done.fetch_add(1, std::memory_order_release);
       for (size_t k = 0; k < W; ++k) {
         const size_t a = cut[k], b = cut[k + 1];
         if (b > a) {  // part t of the step, balanced by rows
@@ -698,7 +702,7 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
         done[k].fetch_add(1, std::memory_order_release);
       }
   });
-  fill_envs(r, 0, G, ENV);
+  while (envs_done.load(std::memory_order_acquire) < T) std::this_thread::yield();
   RTRACE(r, "envs", E);
   int rc = pbft_verify_votes_submit_begin(r->ctx, N, E, r->bitmap.data());
   RTRACE(r, "begin", N);

@@ -368,9 +368,29 @@ __device__ __forceinline__ int32_t row_from_above(int32_t x) {  // lane j <- lan
   return __builtin_amdgcn_update_dpp(0, x, 0x101, 0xF, 0xF, true);  // row_shl:1, bound_ctrl
 }
 
+// Lane j of its row <- lane N of the same 16-lane row (DPP row_newbcast:N).
+template <int N>
+__device__ __forceinline__ int32_t row_lane(int32_t x) {
+  return __builtin_amdgcn_update_dpp(0, x, 0x150 + N, 0xF, 0xF, false);
+}
+
+// limb i of v = lane i of this lane's row, i = 0..9
+template <int I = 0>
+__device__ __forceinline__ void row_limbs(fe& v, int32_t x) {
+  if constexpr (I < 10) {
+    v.v[I] = (uint32_t)row_lane<I>(x);
+    row_limbs<I + 1>(v, x);
+  }
+}
+
 // out = z^-1 (0 -> 0) for a wave-uniform z (z as for fe_invert_gcd), divstep table `tab` in LDS.  Every lane
 // of the wave must call it (the limbs live across lanes); `out` is the same in every lane, carried.
+// ROWS: z need only be uniform within each 16-lane row -- the four rows invert their own values (every
+// cross-limb read stays inside the row; a row whose g reached 0 early keeps stepping with g = 0, which
+// multiplies D by 2^30 per batch as the shared batch count k expects, so its result is unchanged).
+template <bool ROWS = false>
 __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint64_t* tab) {
+  static_assert(!ROWS || PBFT_INV_VALU_LOOKUP, "row-wise inversions need the per-row (DPP) lookup operands");
   const int li = (int)(threadIdx.x & 15);  // limb held by this lane
   uint32_t w[8];
   fe_to_words(w, z);
@@ -398,11 +418,13 @@ __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint6
     const int64_t u = tp[0], v = tp[1], q = tp[2], r = tp[3];
     const int64_t ad = u * D + v * E, ae = q * D + r * E;
     const int32_t hd = (int32_t)(ad >> dsh), he = (int32_t)(ae >> dsh);
-    const int32_t hd9 = __builtin_amdgcn_readlane(hd, 9), he9 = __builtin_amdgcn_readlane(he, 9);
+    const int32_t hd9 = ROWS ? row_lane<9>(hd) : __builtin_amdgcn_readlane(hd, 9);
+    const int32_t he9 = ROWS ? row_lane<9>(he) : __builtin_amdgcn_readlane(he, 9);
     const int64_t nd = (int64_t)(int32_t)(((uint32_t)ad & dmask) + (uint32_t)row_from_below(hd)) + (int64_t)w19 * hd9;
     const int64_t ne = (int64_t)(int32_t)(((uint32_t)ae & dmask) + (uint32_t)row_from_below(he)) + (int64_t)w19 * he9;
     const int32_t kd = (int32_t)(nd >> dsh), ke = (int32_t)(ne >> dsh);
-    const int32_t kd9 = __builtin_amdgcn_readlane(kd, 9), ke9 = __builtin_amdgcn_readlane(ke, 9);
+    const int32_t kd9 = ROWS ? row_lane<9>(kd) : __builtin_amdgcn_readlane(kd, 9);
+    const int32_t ke9 = ROWS ? row_lane<9>(ke) : __builtin_amdgcn_readlane(ke, 9);
     D = ((int32_t)((uint32_t)nd & dmask) + row_from_below(kd) + w19 * kd9) & dlive;
     E = ((int32_t)((uint32_t)ne & dmask) + row_from_below(ke) + w19 * ke9) & dlive;
   };
@@ -445,12 +467,13 @@ __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint6
   }
   update_de(tp);
   // x^-1 = +-D 2^(-30 k): f = +1 iff its limb 0 is 1
-  const bool neg = ((uint32_t)__builtin_amdgcn_readfirstlane(f) & INV_M30) != 1u;
+  const bool neg = ((uint32_t)(ROWS ? row_lane<0>(f) : __builtin_amdgcn_readfirstlane(f)) & INV_M30) != 1u;
   fe d, c, p2;
+  if constexpr (ROWS) row_limbs(p2, D);
 #pragma unroll
   for (int i = 0; i < 10; ++i) {
+    if constexpr (!ROWS) p2.v[i] = (uint32_t)__builtin_amdgcn_readlane(D, i);
     // limbs in [-2^12, 2^26 + 2^12]: + 2p makes them positive and within fe_mul's operand bounds
-    p2.v[i] = (uint32_t)__builtin_amdgcn_readlane(D, i);
     d.v[i] = p2.v[i] + (i == 0 ? 0x7FFFFDAu : (i & 1) ? 0x3FFFFFEu : 0x7FFFFFEu);
     c.v[i] = DS_INV2K[k][i];
   }

@@ -106,7 +106,8 @@ struct keyset {
   uint32_t* d_keys = nullptr;
   uint8_t* d_key_ok = nullptr;
   uint32_t n = 0;
-  uint32_t cap = 0;  // keys the buffers hold (a later set_keys of <= cap keys with the same plan reuses them)
+  uint32_t cap = 0;      // keys d_keys / d_key_ok hold
+  size_t tab_bytes = 0;  // bytes of d_tabA (a later set_keys whose plan's tables fit reuses the buffers)
   int pa = 0;  // positions of the key plan (identifies PLA_HUGE / PLA_BIG / PLA_MID / PLA_SMALL)
 };
 static size_t plan_table_words(int pa) {
@@ -170,7 +171,8 @@ struct pbft_ctx {
   hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
   bool in_flight = false;
   uint64_t* async_out = nullptr;
-  uint64_t* h_bitmap = nullptr;  // pinned
+  uint64_t* h_bitmap = nullptr;      // pinned, fine-grained
+  uint64_t* h_bitmap_dev = nullptr;  // the same memory as the kernels address it (export_words)
   uint64_t async_words = 0;
   float last_ms = 0.f;
   // pinned host staging of the non-blocking host-buffer forms (pageable caller buffers are copied here,
@@ -195,6 +197,18 @@ struct pbft_ctx {
 #ifndef PBFT_ENV_SCHED
 #define PBFT_ENV_SCHED 1  // A/B: 0 = every signature expands its own block-2 schedule
 #endif
+
+// Bitmap words [lo, lo + n) to the pinned host copy, written by a kernel over PCIe.  A hipMemcpyAsync D2H of these
+// few KB blocked the calling thread for 6-8 ms at times on MI355X (PBFT_LAUNCH_TRACE in the replica's flush:
+// profiles/r04/launch_stalls.txt), stalling the launch loop behind it; a kernel launch returns at once.  The host
+// copy is fine-grained memory: the stores reach it without a cache writeback, and the event recorded after the
+// kernel orders them before the host's read.
+__global__ void export_words_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+  __threadfence_system();
+}
+static hipError_t export_words(pbft_ctx* c, uint64_t lo, uint64_t n, hipStream_t st);
 
 // Pinned host staging (grow-only: hipHostMalloc costs milliseconds).  Never while a batch is in flight.
 // Every user of the staging calls this first: whatever pbft_verify_votes_stage handed out is void from here on
@@ -247,6 +261,13 @@ struct host_batch_layout {
   }
 };
 
+static hipError_t export_words(pbft_ctx* c, uint64_t lo, uint64_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(export_words_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, c->d_bitmap + lo,
+                     c->h_bitmap_dev + lo, n);
+  return hipGetLastError();
+}
+
 static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
   if (bytes > c->stage_cap) {
     if (c->d_stage) HIP_TRY(hipFree(c->d_stage));
@@ -258,11 +279,12 @@ static int ensure_stage(pbft_ctx* c, size_t bytes, size_t words) {
   if (words > c->bitmap_cap) {
     if (c->d_bitmap) HIP_TRY(hipFree(c->d_bitmap));
     if (c->h_bitmap) HIP_TRY(hipHostFree(c->h_bitmap));
-    c->d_bitmap = nullptr; c->h_bitmap = nullptr;
+    c->d_bitmap = nullptr; c->h_bitmap = nullptr; c->h_bitmap_dev = nullptr;
     size_t cap = words + 64;
     if (hipMalloc(&c->d_bitmap, cap * 8) != hipSuccess) return set_err(PBFT_ENOMEM, "bitmap alloc");
-    if (hipHostMalloc(&c->h_bitmap, cap * 8, hipHostMallocDefault) != hipSuccess)
+    if (hipHostMalloc(&c->h_bitmap, cap * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
       return set_err(PBFT_ENOMEM, "pinned bitmap alloc");
+    HIP_TRY(hipHostGetDevicePointer((void**)&c->h_bitmap_dev, c->h_bitmap, 0));
     c->bitmap_cap = cap;
   }
   return PBFT_OK;
@@ -287,6 +309,22 @@ static inline size_t eidx_bytes(uint64_t N) {
   const size_t comb = 4 * (size_t)MAX_STEPS * Npad;
   return ((comb > split ? comb : split) + 255) & ~(size_t)255;
 }
+// PBFT_LAUNCH_TRACE=1: every HIP call of a votes chunk launch that blocks the host for more than 0.3 ms is reported
+// on stderr (the replica's flush timeline showed 6-7 ms stalls inside pbft_verify_votes_submit_rows)
+static bool launch_trace() {
+  static const bool on = getenv("PBFT_LAUNCH_TRACE") != nullptr;
+  return on;
+}
+#define LT(name, ...)                                                                                              \
+  do {                                                                                                             \
+    const auto lt_t0 = std::chrono::steady_clock::now();                                                           \
+    __VA_ARGS__;                                                                                                   \
+    if (launch_trace()) {                                                                                          \
+      const double lt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt_t0).count(); \
+      if (lt_ms > 0.3) fprintf(stderr, "launch-stall %s chunk %u: %.3f ms\n", name, (unsigned)c->v_chunk, lt_ms);  \
+    }                                                                                                              \
+  } while (0)
+
 // second xyz/flags half (pipelined form) after the entry-index region
 static inline size_t half1_offset(uint64_t N) { return eidx_offset(N) + eidx_bytes(N); }
 // The layout is a function of c->work_n only, never of the batch at hand: a smaller batch must not move
@@ -330,7 +368,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     c->half ^= 1;
   }
   if (c->fin_pending[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));  // a pipelined finish still reading half h
-  if (c->timing) HIP_TRY(hipEventRecord(c->ev0, st));
+  if (c->timing) LT("rec_ev0", HIP_TRY(hipEventRecord(c->ev0, st)));
   const uint64_t W = c->work_n;  // layout (>= N)
   uint8_t* hw = c->d_work + (h ? half1_offset(W) : 0);
   const bool latency_mode = N < c->split_below;
@@ -345,10 +383,10 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
-  HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
-          : c->pa == PLA_BIG::P ? launch_comb_big(a)
-          : c->pa == PLA_MID::P ? launch_comb_mid(a)
-                                : launch_comb_small(a));
+  LT("comb", HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
+                     : c->pa == PLA_BIG::P ? launch_comb_big(a)
+                     : c->pa == PLA_MID::P ? launch_comb_mid(a)
+                                           : launch_comb_small(a)));
   HIP_TRY(hipGetLastError());
   if (fst) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
@@ -367,7 +405,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
     const int fw = c->fin_waves ? c->fin_waves : (big ? PBFT_FIN_W_BIG : 1);
-    HIP_TRY(launch_finish(fm, lv, fw, dR, rs_stride, xyz, flags, N, dB, st));
+    LT("finish", HIP_TRY(launch_finish(fm, lv, fw, dR, rs_stride, xyz, flags, N, dB, st)));
     HIP_TRY(hipGetLastError());
   }
   if (fst) {
@@ -375,7 +413,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     c->fin_pending[h] = true;
     return PBFT_OK;
   }
-  if (c->timing) HIP_TRY(hipEventRecord(c->ev1, st));
+  if (c->timing) LT("rec_ev1", HIP_TRY(hipEventRecord(c->ev1, st)));
   return PBFT_OK;
 }
 
@@ -548,27 +586,27 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
     const int b = (int)(c->v_chunk & 1);
     uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
-    if (c->v_chunk >= 2) HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0));
+    if (c->v_chunk >= 2) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
     if (rs_stride == 64) {
-      HIP_TRY(hipMemcpyAsync(base, R + 64 * lo, 64 * n, hipMemcpyHostToDevice, c->cstream));
+      LT("h2d_sig", HIP_TRY(hipMemcpyAsync(base, R + 64 * lo, 64 * n, hipMemcpyHostToDevice, c->cstream)));
     } else {
       HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
       HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
     }
-    HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream));
-    HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream));
-    HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream));
-    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0));
-    const int rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS,
-                                 (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n,
-                                 c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
-                                 (const uint32_t*)(base + L.offI), c->v_env, c->v_wk);
+    LT("h2d_key", HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream)));
+    LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
+    LT("rec_copied", HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream)));
+    LT("wait_copied", HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0)));
+    int rc = 0;
+    LT("kernels", rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS,
+                                     (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN,
+                                     PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
+                                     (const uint32_t*)(base + L.offI), c->v_env, c->v_wk));
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream));
+    LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream)));
     if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
-      HIP_TRY(hipMemcpyAsync(c->h_bitmap + lo / 64, c->d_bitmap + lo / 64, (n + 63) / 64 * 8, hipMemcpyDeviceToHost,
-                             c->stream));
-      HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream));
+      LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, c->stream)));
+      LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream)));
     }
     c->v_next += n;
     ++c->v_chunk;
@@ -715,10 +753,13 @@ static double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// Install a key set.  Where the time of a re-key went: freeing and re-allocating the 69-172 GB
-// of key tables took seconds on MI355X (the table build itself ~0.25 s), so a key set of at most the current
-// capacity with the same plan is rebuilt IN PLACE -- no hipFree, no hipMalloc -- when this context alone holds it;
-// pbft_verify_key_stats reports the phases of the last call.
+// Install a key set.  Where the time of a re-key went: hipMalloc itself is ~0.3 ms even for
+// 172 GB, but VRAM that was written and then freed is wiped by the driver (~22 GB/s, tools/microbench/alloc_h2d:
+// re-allocating 202 GB right after freeing it took 9.3 s) and the next allocation waits for that -- a plan change
+// that freed 69 GB of tables paid 6.2 s in hipMalloc, the table build itself ~0.25 s.  So a key set whose tables
+// fit the current allocation (same plan and at most as many keys, or a smaller plan) is rebuilt IN PLACE -- no
+// hipFree, no hipMalloc -- when this context alone holds it; pbft_verify_key_stats reports the phases of the
+// last call.
 int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key_ok) {
   if (!c || (!A && n)) return set_err(PBFT_EINVAL, "null argument");
   if (n == 0 || n > 65535) return set_err(PBFT_EINVAL, "key count must be 1..65535");
@@ -729,7 +770,7 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   HIP_TRY(hipStreamSynchronize(c->stream));
   // this context's key set, if no clone shares it: its tables may be overwritten in place
   keyset* own = (c->ks && c->ks->refs.load() == 1) ? c->ks : nullptr;
-  const size_t own_bytes = own ? plan_table_words(own->pa) * 4 * (size_t)own->cap : 0;
+  const size_t own_bytes = own ? own->tab_bytes : 0;
   // The widest key plan whose tables fit the budget (PBFT_OPT_KEY_TABLE_BUDGET_MB / env, default 70 % of the HBM
   // free once the old key set is gone: ~180 GB on a 288-GB MI355X after the 30-GB base-point table) and the free
   // memory.  Entry indices are 32-bit (n * entries per key < 2^32).
@@ -752,10 +793,11 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
   else if (fits(PLA_MID::TABLE_WORDS, PLA_MID::ENTRIES)) pa = PLA_MID::P;
   const size_t tab_words = plan_table_words(pa);
   keyset* k = nullptr;
-  if (own && own->pa == pa && n <= own->cap) {
-    // same plan, fits the allocation: rebuild in place.  Launches on callers' streams (device forms) may still
+  if (own && n <= own->cap && tab_words * 4 * (size_t)n <= own->tab_bytes) {
+    // the tables fit the allocation: rebuild in place.  Launches on callers' streams (device forms) may still
     // read the old tables.
     k = own;
+    k->pa = pa;
     ks.reused = 1;
     HIP_TRY(hipDeviceSynchronize());
   } else {
@@ -766,7 +808,8 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
     k = new keyset();
     k->pa = pa;
     k->cap = n;
-    if (hipMalloc(&k->d_tabA, tab_words * 4 * (size_t)n) != hipSuccess ||
+    k->tab_bytes = tab_words * 4 * (size_t)n;
+    if (hipMalloc(&k->d_tabA, k->tab_bytes) != hipSuccess ||
         hipMalloc(&k->d_keys, 32 * (size_t)n) != hipSuccess || hipMalloc(&k->d_key_ok, n) != hipSuccess) {
       (void)hipGetLastError();
       keyset_release(k);
@@ -796,8 +839,8 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
     return rc;
   }
   if (k != c->ks) c->adopt(k);
-  else c->n_keys = k->n;  // rebuilt in place: same buffers and plan, new count
-  ks.table_bytes = tab_words * 4 * (size_t)k->cap;
+  else c->n_keys = k->n, c->pa = k->pa;  // rebuilt in place: same buffers, new count (and maybe plan)
+  ks.table_bytes = k->tab_bytes;
   ks.total_ms = ms_since(t_all);
   c->kstats = ks;
   return PBFT_OK;
@@ -914,7 +957,7 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   int rc = stage_and_launch(c, R, S, K, M, msg_len, msg_stride, N);
   if (rc) return rc;
   const uint64_t words = (N + 63) / 64;
-  HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(export_words(c, 0, words, c->stream));
   HIP_TRY(hipEventRecord(c->ev_done, c->stream));
   c->in_flight = true;
   c->v_readback = false;
@@ -965,7 +1008,7 @@ static int votes_submit_from(pbft_ctx* c, const uint8_t* R, const uint8_t* S, co
   int rc = stage_votes_and_launch(c, R, S, K, I, E, n_env, N, rs_stride);
   if (rc) return rc;
   const uint64_t words = (N + 63) / 64;
-  HIP_TRY(hipMemcpyAsync(c->h_bitmap, c->d_bitmap, words * 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(export_words(c, 0, words, c->stream));
   HIP_TRY(hipEventRecord(c->ev_done, c->stream));
   c->in_flight = true;
   c->v_readback = false;

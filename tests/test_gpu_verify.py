@@ -695,8 +695,9 @@ def test_rekey_in_place_and_partial_update(gv, coracle):
     """a re-key with the same plan reuses the table allocation (no hipFree / hipMalloc), a
     smaller set too; pbft_verify_update_keys rebuilds only the named keys' tables -- a round signed under the
     updated set equals the oracle's bitmap over that set, the replaced keys' old signatures now fail, a
-    small-order replacement key rejects everything under it; a plan change frees and re-allocates."""
-    from pbft_amd import PbftError
+    small-order replacement key rejects everything under it; plan changes rebuild in place while the tables fit
+    the allocation, a larger set re-allocates."""
+    from pbft_amd import GpuBatchVerifier, PbftError
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 256, tag=31)   # 32,768 signatures
     rng = np.random.default_rng(31)
     R2, S2, K2, M2, _ = adversarial(rng, pub, R, S, key_idx, msg, frac=0.01)
@@ -736,12 +737,26 @@ def test_rekey_in_place_and_partial_update(gv, coracle):
         with pytest.raises(PbftError) as e:
             gv.update_keys(bad, pub_new[: len(bad)])
         assert e.value.code == -1
-    # a plan change (budget forced down, then back) frees and re-allocates
+    # a plan change to smaller tables (budget forced down) rebuilds in the same allocation, and so does the
+    # change back (the allocation never shrinks)
+    pa0 = gv.positions()[1]
     gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 5000)   # 64 keys x 63 MB: the 16-position plan
     try:
-        assert gv.set_keys(pub_new).all() and gv.positions()[1] == 16 and gv.key_stats()["reused"] == 0
+        assert gv.set_keys(pub_new).all() and gv.positions()[1] == 16 and gv.key_stats()["reused"] == 1
         got, _ = verify(gv, Rn2, Sn2, Kn2, Mn2, 85)
         assert (got == oracle_bits(coracle, pub_new, Rn2, Sn2, Kn2, Mn2, 85)).all()
     finally:
         gv.set_option(gv.OPT_KEY_TABLE_BUDGET_MB, 0)
-    assert gv.set_keys(pub_new).all() and gv.key_stats()["reused"] == 0
+    assert gv.set_keys(pub_new).all() and gv.positions()[1] == pa0 and gv.key_stats()["reused"] == 1
+    got, _ = verify(gv, Rn2, Sn2, Kn2, Mn2, 85)
+    assert (got == oracle_bits(coracle, pub_new, Rn2, Sn2, Kn2, Mn2, 85)).all()
+    # a set larger than the allocation frees and re-allocates (a fresh context: 8 keys, then 64, then 8 again)
+    v2 = GpuBatchVerifier(0)
+    try:
+        assert v2.set_keys(pub_new[:8]).all() and v2.key_stats()["reused"] == 0
+        assert v2.set_keys(pub_new).all() and v2.key_stats()["reused"] == 0
+        got, _ = verify(v2, Rn2, Sn2, Kn2, Mn2, 85)
+        assert (got == oracle_bits(coracle, pub_new, Rn2, Sn2, Kn2, Mn2, 85)).all()
+        assert v2.set_keys(pub_new[:8]).all() and v2.key_stats()["reused"] == 1
+    finally:
+        v2.close()

@@ -2,7 +2,8 @@
 //  1. hipMalloc of large device buffers (the 172-GB key tables), against hipExtMallocWithFlags and
 //     hipMallocAsync on the default pool;
 //  2. H2D bandwidth from pinned host memory: one stream, two streams (two SDMA queues), several chunk sizes;
-//  3. a kernel reading pinned host memory directly (zero-copy gather of 64-B rows, as a replica's candidate rows
+//  3. H2D of one votes chunk while a kernel occupies every CU (copy engine or blit kernel);
+//  4. a kernel reading pinned host memory directly (zero-copy gather of 64-B rows, as a replica's candidate rows
 //     would be gathered) into device memory.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -30,6 +31,13 @@ __global__ void gather_rows(const uint4* __restrict__ host, const uint32_t* __re
   d[0] = a; d[1] = b; d[2] = c; d[3] = e;
 }
 
+// a compute load that fills every CU for a fixed number of dependent FMAs per lane (bounded: no spin on time)
+__global__ void busy_fma(float* out, int iters) {
+  float a = threadIdx.x * 1e-3f, b = 1.0001f, c = 1e-7f;
+  for (int i = 0; i < iters; ++i) a = fmaf(a, b, c);
+  if (a == 12345.f) out[blockIdx.x] = a;
+}
+
 int main(int argc, char** argv) {
   const size_t GB = 1ull << 30;
   const size_t big = (argc > 1 ? strtoull(argv[1], nullptr, 10) : 64) * GB;
@@ -38,6 +46,8 @@ int main(int argc, char** argv) {
   size_t fr, tot;
   CK(hipMemGetInfo(&fr, &tot));
   printf("free %.1f GB of %.1f GB\n", fr / 1e9, tot / 1e9);
+  const bool only_overlap = argc > 2 && !strcmp(argv[2], "overlap");  // usage: alloc_h2d [GB] [overlap]
+  if (!only_overlap) {
   for (int rep = 0; rep < 2; ++rep) {
     void* p = nullptr;
     auto t = std::chrono::steady_clock::now();
@@ -134,6 +144,7 @@ int main(int argc, char** argv) {
     CK(hipHostFree(pn));
     free(pm);
   }
+  }  // !only_overlap
   // H2D from pinned memory
   const size_t bytes = 72ull << 20;  // ~ a 2^20-vote round in the votes form (70 B per row)
   void *h = nullptr, *d = nullptr;
@@ -159,6 +170,44 @@ int main(int argc, char** argv) {
       }
       printf("H2D %zu MB in %zu-MB chunks on %d stream(s): %.3f ms = %.1f GB/s\n", bytes >> 20, chunk >> 20, streams,
              best, bytes / 1e6 / best);
+    }
+  }
+  {  // H2D while a kernel occupies every CU: do the copies overlap compute (SDMA) or queue behind it (blit kernel)?
+    float* junk = nullptr;
+    CK(hipMalloc(&junk, 4 << 20));
+    hipEvent_t e0, e1, e2, e3;
+    CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1)); CK(hipEventCreate(&e2)); CK(hipEventCreate(&e3));
+    const size_t chunk = 18ull << 20;  // one 2^18-row votes chunk
+    const dim3 grid(256 * 16), blk(256);
+    for (int iters : {20000, 80000}) {
+      for (int rep = 0; rep < 3; ++rep) {
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(e0, s0));
+        hipLaunchKernelGGL(busy_fma, grid, blk, 0, s0, junk, iters);
+        CK(hipEventRecord(e1, s0));
+        CK(hipStreamSynchronize(s0));
+        float kern = 0;
+        CK(hipEventElapsedTime(&kern, e0, e1));
+        // the same kernel, with a chunk copy enqueued on the other stream right after it
+        CK(hipDeviceSynchronize());
+        auto t = std::chrono::steady_clock::now();
+        CK(hipEventRecord(e0, s0));
+        hipLaunchKernelGGL(busy_fma, grid, blk, 0, s0, junk, iters);
+        CK(hipEventRecord(e1, s0));
+        CK(hipEventRecord(e2, s1));
+        CK(hipMemcpyAsync(d, h, chunk, hipMemcpyHostToDevice, s1));
+        CK(hipEventRecord(e3, s1));
+        CK(hipStreamSynchronize(s1));
+        const double copy_host = ms_since(t);
+        CK(hipStreamSynchronize(s0));
+        float kern2 = 0, copy = 0, copy_end = 0;
+        CK(hipEventElapsedTime(&kern2, e0, e1));
+        CK(hipEventElapsedTime(&copy, e2, e3));
+        CK(hipEventElapsedTime(&copy_end, e0, e3));
+        printf("H2D 18 MB beside a %d-iter busy kernel: kernel alone %.3f ms, with copy %.3f ms; copy %.3f ms, done "
+               "%.3f ms after the kernel started (host saw it at %.3f ms)\n", iters, kern, kern2, copy, copy_end,
+               copy_host);
+      }
     }
   }
   {  // zero-copy gather: 2^20 rows of 64 B from pinned host memory, runs of 256 rows in a shuffled order
