@@ -260,13 +260,18 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 70 % of the free HBM); selects the key
  *                                 comb plan
  *   PBFT_OPT_FINISH_TREE          cross-lane levels of the finish's batch inversion: 0 (one inversion per lane)
- *                                 or 6 (one per wave); any other value = by batch size
+ *                                 or 4 / 6 (the compiled product tree: one inversion per 16-lane row); any
+ *                                 other value = by batch size
  *   PBFT_OPT_LAT_SPLIT            lanes per signature of the latency-mode kernel: 4 or 8; any other value = by
  *                                 batch size (8 up to 8,192 signatures, else 4)
  *   PBFT_OPT_FINISH_WAVES         product-tree finish compiled for 1 wave per SIMD (widths 1-16, X/Y/Z prefetched)
  *                                 or 2 (widths 1, 2, 4, 8; width 1 prefetched); any other value = by batch size
  *   PBFT_OPT_KERNEL_TIMING        1 (default): two HIP events bracket every launch for pbft_last_kernel_ms; 0: none
- *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers) */
+ *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers)
+ *   PBFT_OPT_VOTES_ZERO_COPY      1 (default; env PBFT_VOTES_ZERO_COPY): votes rows that sit in the context's
+ *                                 pinned staging (pbft_verify_votes_stage / _submit_begin, the replica's flush,
+ *                                 pageable inputs copied there) are read by the kernels in place over PCIe; 0:
+ *                                 copied to HBM chunk by chunk first */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
@@ -274,6 +279,7 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 #define PBFT_OPT_LAT_SPLIT 5
 #define PBFT_OPT_KERNEL_TIMING 7
 #define PBFT_OPT_FINISH_WAVES 8
+#define PBFT_OPT_VOTES_ZERO_COPY 9
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

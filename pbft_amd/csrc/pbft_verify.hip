@@ -123,6 +123,14 @@ static void keyset_release(keyset* k) {
   }
 }
 
+// Votes rows in the context's pinned staging (the replica's flush, pbft_verify_votes_stage, pageable votes inputs)
+// are read by the comb kernel straight from host memory over PCIe instead of being copied to HBM first: the reads
+// overlap the arithmetic wave by wave instead of chunk by chunk (env PBFT_VOTES_ZERO_COPY, option
+// PBFT_OPT_VOTES_ZERO_COPY).
+#ifndef PBFT_VOTES_ZERO_COPY
+#define PBFT_VOTES_ZERO_COPY 1
+#endif
+
 struct pbft_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -136,7 +144,7 @@ struct pbft_ctx {
   int pa = 0;  // comb positions of the installed key tables' plan (PLA_HUGE, PLA_BIG, PLA_MID or PLA_SMALL)
   uint64_t split_below = SPLIT_BELOW;  // latency mode below this batch size (env PBFT_SPLIT_BELOW)
   int fin_m = 0;                       // finish-kernel signatures per lane (0 = by batch size)
-  int fin_tree = -1;                   // finish cross-lane tree levels (0 / 6; -1 = by batch size)
+  int fin_tree = -1;                   // finish cross-lane tree (0: none; 4 / 6: the compiled tree; -1 = by batch size)
   int fin_waves = 0;                   // product-tree finish compiled for 1 or 2 waves per SIMD (0 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
@@ -178,7 +186,9 @@ struct pbft_ctx {
   // pinned host staging of the non-blocking host-buffer forms (pageable caller buffers are copied here,
   // then DMA'd asynchronously; pbft_verify_votes_stage hands it out for in-place filling)
   uint8_t* h_stage = nullptr;
+  uint8_t* h_stage_dev = nullptr;  // the same memory as the kernels address it (zero-copy votes)
   size_t h_stage_cap = 0;
+  bool zero_copy = PBFT_VOTES_ZERO_COPY;  // votes rows in the staging: kernels read them in place (no H2D)
   uint64_t staged_n = 0;   // pbft_verify_votes_stage: the batch the staging is laid out for
   uint32_t staged_env = 0;
   bool staged = false;
@@ -218,11 +228,18 @@ static int ensure_host_stage(pbft_ctx* c, size_t bytes) {
   if (bytes <= c->h_stage_cap) return PBFT_OK;
   if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
   c->h_stage = nullptr;
+  c->h_stage_dev = nullptr;
   c->h_stage_cap = 0;
   const size_t cap = bytes + (bytes >> 2) + 4096;
-  if (hipHostMalloc(&c->h_stage, cap, hipHostMallocDefault) != hipSuccess) {
+  // fine-grained: kernels that read it in place see every host write, with no stale L2 lines
+  if (hipHostMalloc(&c->h_stage, cap, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
     (void)hipGetLastError();
+    c->h_stage = nullptr;
     return set_err(PBFT_ENOMEM, "pinned host staging alloc");
+  }
+  if (hipHostGetDevicePointer((void**)&c->h_stage_dev, c->h_stage, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    c->h_stage_dev = nullptr;  // (kernels then never read it in place)
   }
   c->h_stage_cap = cap;
   return PBFT_OK;
@@ -327,13 +344,17 @@ static bool launch_trace() {
 
 // second xyz/flags half (pipelined form) after the entry-index region
 static inline size_t half1_offset(uint64_t N) { return eidx_offset(N) + eidx_bytes(N); }
+// R copy [W][32] of a launch whose R is read from host memory (launch_verify r_host), after both halves
+static inline size_t rcopy_offset(uint64_t W, bool two) {
+  return ((two ? half1_offset(W) + eidx_offset(W) : half1_offset(W)) + 255) & ~(size_t)255;
+}
 // The layout is a function of c->work_n only, never of the batch at hand: a smaller batch must not move
 // the entry-index region onto the xyz/flags half a pipelined finish may still be reading.
 static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   if (N <= c->work_n && (!two_halves || c->work_two)) return PBFT_OK;
   const uint64_t W = N > c->work_n ? N : c->work_n;
   const bool two = two_halves || c->work_two;
-  const size_t need = (two ? half1_offset(W) + eidx_offset(W) : half1_offset(W)) + 256;
+  const size_t need = rcopy_offset(W, two) + 32 * (size_t)W + 256;
   // nothing may still read the old workspace: the finishes of earlier pipelined launches, then this stream
   for (int h = 0; h < 2; ++h)
     if (c->fin_pending[h]) { HIP_TRY(hipEventSynchronize(c->ev_fin[h])); c->fin_pending[h] = false; }
@@ -356,7 +377,8 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
                          uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
-                         const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr) {
+                         const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr,
+                         bool r_host = false) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
@@ -381,6 +403,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.eidx = (uint32_t*)(c->d_work + eidx_offset(W));
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
+  // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
+  if (r_host && !latency_mode) a.r_copy = (uint32_t*)(c->d_work + rcopy_offset(W, c->work_two));
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
   LT("comb", HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
@@ -398,14 +422,15 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     // signatures per finish lane, product tree and waves per SIMD by batch size (PBFT_FIN_* above)
     const bool big = N >= ((uint64_t)1 << 19);
     int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID : PBFT_FIN_FM_SMALL;
-    // cross-lane product tree (one variable-time inversion per wave) where few signatures share a
-    // lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
-    // (profiles/r02_ab_log.md)
+    // cross-lane product tree (one variable-time inversion per 16-lane row since r04, per wave before) where few
+    // signatures share a lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
+    // (profiles/r02_ab_log.md); lv is a flag here, finish.hip compiles the tree depth (PBFT_FIN_LV)
     int lv = fm <= PBFT_FIN_TREE_MAX_FM ? 6 : 0;
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
     const int fw = c->fin_waves ? c->fin_waves : (big ? PBFT_FIN_W_BIG : 1);
-    LT("finish", HIP_TRY(launch_finish(fm, lv, fw, dR, rs_stride, xyz, flags, N, dB, st)));
+    const uint8_t* fR = a.r_copy ? (const uint8_t*)a.r_copy : dR;
+    LT("finish", HIP_TRY(launch_finish(fm, lv, fw, fR, a.r_copy ? 32 : rs_stride, xyz, flags, N, dB, st)));
     HIP_TRY(hipGetLastError());
   }
   if (fst) {
@@ -538,6 +563,14 @@ struct votes_layout {
   }
 };
 
+// The kernels' address of [p, p + bytes) when it lies in the context's mapped staging and zero-copy reads are on,
+// else null (the rows are then copied to HBM first).
+static const uint8_t* zc_dev(const pbft_ctx* c, const void* p, size_t bytes) {
+  const uint8_t* q = (const uint8_t*)p;
+  if (!c->zero_copy || !c->h_stage_dev || q < c->h_stage || q + bytes > c->h_stage + c->h_stage_cap) return nullptr;
+  return c->h_stage_dev + (q - c->h_stage);
+}
+
 // rs_stride 32: R and S are separate [N][32] host columns; 64: R = the [N][64] signature rows, S = R + 32.
 // votes_begin copies the envelope table and launches its schedule; votes_launch then launches every whole chunk
 // inside rows [0, rows) (all the rest once rows >= N): the kernels of chunk c run on the context stream after
@@ -585,6 +618,24 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     const uint64_t lo = c->v_next;
     const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
     const int b = (int)(c->v_chunk & 1);
+    const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
+    const uint8_t* zS = rs_stride == 64 ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
+    const uint8_t* zK = zc_dev(c, K + lo, 2 * n);
+    const uint8_t* zI = zc_dev(c, IDX + lo, 4 * n);
+    if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
+      int rc = 0;
+      LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
+                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
+                                       (const uint32_t*)zI, c->v_env, c->v_wk, true));
+      if (rc) return rc;
+      if (c->v_readback) {
+        LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, c->stream)));
+        LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream)));
+      }
+      c->v_next += n;
+      ++c->v_chunk;
+      continue;
+    }
     uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
     if (c->v_chunk >= 2) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
     if (rs_stride == 64) {
@@ -696,6 +747,7 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   c->device = device;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
+  if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
@@ -921,6 +973,7 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->fin_waves = parent->fin_waves;
   c->lat_split = parent->lat_split;
   c->timing = parent->timing;
+  c->zero_copy = parent->zero_copy;
   c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
@@ -1503,10 +1556,11 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
         return set_err(PBFT_EINVAL, "finish width");
       c->fin_m = (int)value;
       return PBFT_OK;
-    case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 6) ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 4 || value == 6) ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_FINISH_WAVES: c->fin_waves = (value == 1 || value == 2) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
+    case PBFT_OPT_VOTES_ZERO_COPY: c->zero_copy = value != 0; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");

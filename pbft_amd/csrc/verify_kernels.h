@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
     uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg,
-    const uint64_t* __restrict__ wk) {
+    const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy) {
   using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -245,6 +245,11 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     uint32_t r[8], s[8], a[8];
     load32(r, R + (size_t)rs_stride * ii);
     load32(s, S + (size_t)rs_stride * ii);
+    if (r_copy && live) {  // R read from host memory (zero-copy votes): the finish reads this HBM copy instead
+      uint4* rc = (uint4*)(r_copy + 8 * i);
+      rc[0] = uint4{r[0], r[1], r[2], r[3]};
+      rc[1] = uint4{r[4], r[5], r[6], r[7]};
+    }
     uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
     kok = ki < n_keys;
     if (!kok) ki = 0;
@@ -387,6 +392,10 @@ static constexpr uint64_t LAT_WIDE_UPTO = PBFT_LAT_WIDE_UPTO;
 static constexpr int LAT_COMB_WAVES = PBFT_LAT_DECOMP ? 3 : 4;
 #ifndef PBFT_LAT_TAB
 #define PBFT_LAT_TAB (PBFT_LAT_TREE && !PBFT_LAT_DECOMP)  // table-driven divsteps for the wave's inversion
+#endif
+#ifndef PBFT_LAT_ROWS
+#define PBFT_LAT_ROWS 1  // the product tree per 16-lane row, four inversions per wave (fe_invert_wave<true>);
+                         // 0: per wave (r04 A/B, profiles/r04/ab_lat_rows.txt: 4k p50 -1.6 %, 8k -2.0 %)
 #endif
 // the divstep table of fe_invert_tab (inv25519.h), constant-initialised at compile time (40 KB); the kernels
 // that invert a wave-uniform value copy it to LDS per block
@@ -605,7 +614,9 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     // same product and the shorter variable-time divsteps (inv25519.h) never diverge; the down-sweep
     // peels the partners off again (1 / t_k = (1 / t_{k+1}) q_k).  Z is never 0 (complete formulas
     // over curve points; invalid keys have identity tables), so no lane poisons the others.
-    constexpr int LV = SPLIT == 4 ? 4 : 3;  // log2(signatures per wave)
+    // PBFT_LAT_ROWS: the tree stops at the 16-lane row and each row inverts its own product
+    // (fe_invert_wave<true>): two butterfly levels fewer each way, same inversion count per wave
+    constexpr int LV = PBFT_LAT_ROWS ? (SPLIT == 4 ? 2 : 1) : (SPLIT == 4 ? 4 : 3);  // log2(signatures per tree)
     fe t = P.Z, tq[LV];
     static_for<LV>([&](auto kc) {
       constexpr int k = decltype(kc)::value;
@@ -617,8 +628,9 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
 #elif PBFT_LAT_TAB
     __syncthreads();  // the block's divstep table is in LDS (copied at kernel start)
     #if PBFT_INV_WAVE
-    fe_invert_wave(zi, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
+    fe_invert_wave<PBFT_LAT_ROWS>(zi, t, ds_tab);  // limbs across lanes, DPP carries (inv25519.h)
 #else
+    static_assert(!PBFT_LAT_ROWS, "");
     fe_invert_tab(zi, t, ds_tab);
 #endif
 #else
@@ -674,6 +686,7 @@ struct comb_launch_args {
   const uint32_t* msg_idx; // votes form (null: one message per signature)
   uint32_t n_msg;
   const uint64_t* wk;      // votes form, 85-byte envelopes: per-envelope block-2 schedule (null: hash in full)
+  uint32_t* r_copy = nullptr;  // one-lane mode: [N][8] copy of R for the finish (R read from host memory)
   bool latency_mode;
   int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
   hipStream_t st;
@@ -707,15 +720,15 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
     if (a.msg_len == PBFT_ENVELOPE_LEN && N >= PBFT_CHAIN_MIN_N)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st,
                          a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,
-                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
     else if (a.msg_len == PBFT_ENVELOPE_LEN)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
                          a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
-                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
+                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
     else
       hipLaunchKernelGGL((comb_kernel<-1, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R, a.S, a.K,
                          a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,
-                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk);
+                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
   }
   return hipGetLastError();
 }
@@ -734,8 +747,8 @@ hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int nega
                              uint32_t* d_keys_out = nullptr);
 
 // finish.hip: batch-inversion finish of the one-lane comb: fm (1, 2, 4, 8, 16) signatures per lane, lv = 0
-// (one inversion per lane) or 6 (one per wave, cross-lane product tree), w = waves per SIMD it is compiled for
-// (lv = 6: 1, or 2 for fm 2 / 4 / 8)
+// (one inversion per lane) or nonzero (cross-lane product tree of PBFT_FIN_LV levels: one inversion per 16-lane
+// row, or per wave), w = waves per SIMD it is compiled for (tree: 1, or 2 for fm 2 / 4 / 8)
 hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_stride, const uint32_t* xyz,
                          const uint8_t* flags, uint64_t N, uint64_t* bitmap, hipStream_t st);
 // sign.hip: RFC 8032 signing, len = 85 (envelope), 0 (public keys only) or -1 (any length)

@@ -12,4 +12,6 @@ grep -E "launch-stall" gpurun_out/probe_r04g.err | head -20; cat gpurun_out/prob
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u bench.py > gpurun_out/bench_r04g.json 2> gpurun_out/bench_r04g.err; rc=$?
 tail -c 300 gpurun_out/bench_r04g.err
-exit $rc
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 300 python -u tools/ab.py pbft_amd/libpbft_verify.so@3=20000 build/ab/libpbft_latrows.so@3=20000 --latency --sizes 4096,8192 --rounds 8 > gpurun_out/ab_latrows.txt 2>&1; rc=$?
+grep -v "^W2026" gpurun_out/ab_latrows.txt; exit $rc
