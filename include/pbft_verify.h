@@ -154,18 +154,25 @@ int pbft_verify_wait(pbft_ctx *ctx);
 int pbft_verify_votes_async(pbft_ctx *ctx, const uint8_t *R, const uint8_t *S, const uint16_t *key_idx,
                             const uint32_t *env_idx, const uint8_t *envelopes, uint32_t n_env, uint64_t N,
                             uint64_t *bitmap_out);
-/* Zero-copy votes form: pbft_verify_votes_stage returns the context's pinned host staging for a batch of N
- * signatures over n_env envelopes -- sig[N][64] (the 64-byte signature R || S as it travels), key_idx[N],
- * env_idx[N], envelopes[n_env][85]; valid until the next call on this context that uses the staging (another
- * stage, or any host-buffer submit: pageable inputs are copied there, and a bigger batch reallocates it; such a
- * call also voids the stage, so a later pbft_verify_votes_submit fails with PBFT_EINVAL) -- the caller fills it in place and
- * pbft_verify_votes_submit launches it asynchronously (DMA straight from the staging, the kernels read R and S
- * at a 64-byte stride).  This is what pbft_replica_flush_submit uses. */
+/* Staged votes form: pbft_verify_votes_stage returns the context's pinned host staging for a batch of N
+ * signatures over n_env envelopes, laid out as N rows of PBFT_VOTES_ROW_BYTES (72) bytes -- the 64-byte
+ * signature R || S as it travels, key_idx (u16) at byte 64, two zero bytes, env_idx (u32) at byte 68 -- then
+ * envelopes[n_env][85].  sig, key_idx and env_idx point at row 0's fields (row i's at + i * row_stride bytes), so
+ * one DMA per chunk moves everything a chunk's kernels read (three per chunk with separate columns: the two
+ * small copies and their gaps cost 23 % of the copy engine's time, profiles/r04/votes_copies.txt).  Valid until the
+ * next call on this context that uses the staging (another stage, or any host-buffer submit: pageable inputs are
+ * copied there, and a bigger batch reallocates it; such a call also voids the stage, so a later
+ * pbft_verify_votes_submit fails with PBFT_EINVAL) -- the caller fills it in place and pbft_verify_votes_submit
+ * launches it asynchronously.  This is what pbft_replica_flush_submit uses. */
+#define PBFT_VOTES_ROW_BYTES 72
+#define PBFT_VOTES_ROW_KEY 64
+#define PBFT_VOTES_ROW_ENV 68
 typedef struct {
-  uint8_t *sig;
-  uint16_t *key_idx;
-  uint32_t *env_idx;
-  uint8_t *envelopes;
+  uint8_t *sig;        /* row i: sig + i * row_stride, 64 bytes */
+  uint16_t *key_idx;   /* row i: (uint8_t *)key_idx + i * row_stride */
+  uint32_t *env_idx;   /* row i: (uint8_t *)env_idx + i * row_stride */
+  uint8_t *envelopes;  /* [n_env][85], contiguous */
+  uint32_t row_stride; /* PBFT_VOTES_ROW_BYTES */
 } pbft_votes_staging;
 int pbft_verify_votes_stage(pbft_ctx *ctx, uint64_t N, uint32_t n_env, pbft_votes_staging *out);
 int pbft_verify_votes_submit(pbft_ctx *ctx, uint64_t N, uint32_t n_env, uint64_t *bitmap_out);
@@ -268,10 +275,10 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *                                 or 2 (widths 1, 2, 4, 8; width 1 prefetched); any other value = by batch size
  *   PBFT_OPT_KERNEL_TIMING        1 (default): two HIP events bracket every launch for pbft_last_kernel_ms; 0: none
  *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers)
- *   PBFT_OPT_VOTES_ZERO_COPY      1 (default; env PBFT_VOTES_ZERO_COPY): votes rows that sit in the context's
- *                                 pinned staging (pbft_verify_votes_stage / _submit_begin, the replica's flush,
- *                                 pageable inputs copied there) are read by the kernels in place over PCIe; 0:
- *                                 copied to HBM chunk by chunk first */
+ *   PBFT_OPT_VOTES_ZERO_COPY      1: votes rows that sit in the context's pinned staging (pbft_verify_votes_stage
+ *                                 / _submit_begin, the replica's flush, pageable inputs copied there) are read by
+ *                                 the kernels in place over PCIe; 0 (default; env PBFT_VOTES_ZERO_COPY): copied
+ *                                 to HBM chunk by chunk first (faster on MI355X: DESIGN.md section 5) */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3

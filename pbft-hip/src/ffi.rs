@@ -21,13 +21,20 @@ pub struct pbft_multi {
 }
 
 /// Pinned host staging of one votes-form batch (pbft_verify_votes_stage): filled in place, then submitted.
+/// Rows of `row_stride` (PBFT_VOTES_ROW_BYTES = 72) bytes: row i's signature at `sig + i * row_stride`, its key
+/// index and envelope index at the same offset from `key_idx` / `env_idx` (as bytes).
 #[repr(C)]
 pub struct pbft_votes_staging {
     pub sig: *mut u8,
     pub key_idx: *mut u16,
     pub env_idx: *mut u32,
     pub envelopes: *mut u8,
+    pub row_stride: u32,
 }
+
+pub const PBFT_VOTES_ROW_BYTES: usize = 72;
+pub const PBFT_VOTES_ROW_KEY: usize = 64;
+pub const PBFT_VOTES_ROW_ENV: usize = 68;
 
 pub const PBFT_OK: c_int = 0;
 pub const PBFT_EINVAL: c_int = -1;

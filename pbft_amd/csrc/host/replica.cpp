@@ -375,6 +375,21 @@ static void record_done(pbft_replica* r, uint64_t seq) {
   }
   r->done[seq] = seq;
 }
+// record_done for every seq in [lo, hi] at once (the GC's committed prefix: one interval update, not one per seq)
+static void record_done_range(pbft_replica* r, uint64_t lo, uint64_t hi) {
+  auto it = r->done.upper_bound(lo);  // first interval starting after lo
+  std::map<uint64_t, uint64_t>::iterator cur;
+  if (it != r->done.begin() && std::prev(it)->second + 1 >= lo) {
+    cur = std::prev(it);  // [a, b] with b + 1 >= lo: extend it
+    if (cur->second < hi) cur->second = hi;
+  } else {
+    cur = r->done.emplace_hint(it, lo, hi);
+  }
+  // absorb the intervals that now touch or overlap
+  for (auto nx = std::next(cur); nx != r->done.end() && nx->first <= cur->second + 1; nx = r->done.erase(nx))
+    if (nx->second > cur->second) cur->second = nx->second;
+}
+
 static bool is_done(const pbft_replica* r, uint64_t view, uint64_t seq) {
   if (view != r->current_view) return false;
   auto it = r->done.upper_bound(seq);
@@ -384,16 +399,18 @@ static bool is_done(const pbft_replica* r, uint64_t view, uint64_t seq) {
 
 static void gc(pbft_replica* r) {
   r->last_w = nullptr;  // windows may go away
-  // committed prefix: h advances over consecutive committed windows of the current view
-  for (;;) {
-    auto it = r->windows.find({r->current_view, r->h + 1});
-    if (it == r->windows.end() || !it->second.committed_reported) break;
-    record_done(r, r->h + 1);
-    r->dirty.erase(it->first);
-    drop_window(r, it);
+  // committed prefix: h advances over consecutive committed windows of the current view (one ordered walk:
+  // they are neighbours in the map)
+  const uint64_t h0 = r->h;
+  for (auto it = r->windows.lower_bound({r->current_view, r->h + 1});
+       it != r->windows.end() && it->first.first == r->current_view && it->first.second == r->h + 1 &&
+       it->second.committed_reported;) {
+    if (!r->dirty.empty()) r->dirty.erase(it->first);
+    it = drop_window(r, it);
     ++r->h;
     ++r->stats.windows_gc;
   }
+  if (r->h > h0) record_done_range(r, h0 + 1, r->h);
   // anything at or below h (stable checkpoint, or stale views); the in-flight rows of an erased window are
   // skipped when the batch completes
   for (auto it = r->windows.begin(); it != r->windows.end();) {
@@ -635,22 +652,36 @@ static void finish_batch(pbft_replica* r) {
   r->erased_in_flight = false;
 }
 
-// Copy the candidates of segments [s0, s1) into the batch (pinned staging or the overrides' buffers).
-static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX) {
+// Copy the candidates of segments [s0, s1) into the batch: the GPU context's staged votes rows (rs =
+// PBFT_VOTES_ROW_BYTES: signature, key index and envelope index side by side, include/pbft_verify.h) or the
+// overrides' columns (rs = 0: SIG [N][64], K [N], IDX [N]).
+static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, size_t rs) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
     Phase& p = g.w->ph[g.kind];
-    memcpy(SIG + 64 * g.row0, p.sig.data(), 64 * (size_t)g.count);
-    memcpy(K + g.row0, p.who.data(), 2 * (size_t)g.count);
-    if (p.digs.size() == 1) {
-      std::fill(IDX + g.row0, IDX + g.row0 + g.count, g.env0);
+    const bool one = p.digs.size() == 1;
+    if (rs) {
+      uint8_t* row = SIG + rs * g.row0;
+      for (uint32_t i = 0; i < g.count; ++i, row += rs) {
+        memcpy(row, &p.sig[64 * (size_t)i], 64);
+        const uint64_t meta = (uint64_t)p.who[i] | (uint64_t)(g.env0 + (one ? 0 : p.dix[i])) << 32;
+        memcpy(row + PBFT_VOTES_ROW_KEY, &meta, 8);  // key_idx, two zero bytes, env_idx
+      }
     } else {
-      for (uint32_t i = 0; i < g.count; ++i) IDX[g.row0 + i] = g.env0 + p.dix[i];
+      memcpy(SIG + 64 * g.row0, p.sig.data(), 64 * (size_t)g.count);
+      memcpy(K + g.row0, p.who.data(), 2 * (size_t)g.count);
+      if (one) {
+        std::fill(IDX + g.row0, IDX + g.row0 + g.count, g.env0);
+      } else {
+        for (uint32_t i = 0; i < g.count; ++i) IDX[g.row0 + i] = g.env0 + p.dix[i];
+      }
     }
     memset(p.st.data(), V_IN_FLIGHT, g.count);
     p.n_pending = 0;
   }
 }
+static_assert(PBFT_VOTES_ROW_ENV == PBFT_VOTES_ROW_KEY + 4 && PBFT_VOTES_ROW_BYTES == PBFT_VOTES_ROW_KEY + 8,
+              "fill_rows writes key_idx, pad and env_idx as one 8-byte word");
 static void fill_envs(pbft_replica* r, size_t s0, size_t s1, uint8_t* ENV) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
@@ -660,16 +691,17 @@ static void fill_envs(pbft_replica* r, size_t s0, size_t s1, uint8_t* ENV) {
                     p.digs[j].data());
   }
 }
-static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV) {
+static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV,
+                      size_t rs) {
   fill_envs(r, s0, s1, ENV);
-  fill_rows(r, s0, s1, SIG, K, IDX);
+  fill_rows(r, s0, s1, SIG, K, IDX, rs);
 }
 
 
 // GPU path of a large batch: envelopes, then the rows in steps (the library's votes chunks) on T threads while this thread launches
 // each step as soon as it is filled (pbft_verify_votes_submit_rows): the fill overlaps the copies and kernels.
 static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K, uint32_t* IDX, uint8_t* ENV,
-                           uint32_t E) {
+                           uint32_t E, size_t rs) {
   const size_t G = r->segs.size();
   const uint64_t N = r->rows;
   // one fill step per chunk of the library's votes schedule (PBFT_VOTES_CHUNK_END, include/pbft_verify.h)
@@ -697,7 +729,7 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
           const uint64_t lo = r->segs[a].row0, hi = b < G ? r->segs[b].row0 : N;
           const size_t x = t == 0 ? a : std::max(a, first_at(lo + (hi - lo) * t / T));
           const size_t y = t + 1 == T ? b : std::min(b, first_at(lo + (hi - lo) * (t + 1) / T));
-          if (y > x) fill_rows(r, x, y, SIG, K, IDX);
+          if (y > x) fill_rows(r, x, y, SIG, K, IDX, rs);
         }
         done[k].fetch_add(1, std::memory_order_release);
       }
@@ -1042,6 +1074,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   uint8_t *SIG, *ENV;
   uint16_t* K;
   uint32_t* IDX;
+  size_t rs = 0;  // staged rows' stride (0: the overrides' columns)
   if (r->verify_fn || r->vsub) {
     r->hSig.resize(64 * N); r->hK.resize(N); r->hI.resize(N);
     r->hE.assign(PBFT_ENVELOPE_BYTES * (size_t)E + 16, 0);
@@ -1052,6 +1085,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     RTRACE(r, "stage", rc);
     if (rc) { r->segs.clear(); return rc; }
     SIG = st.sig; K = st.key_idx; IDX = st.env_idx; ENV = st.envelopes;
+    rs = st.row_stride;
   }
   const size_t G = r->segs.size();
   r->touched.assign(G, 0);
@@ -1059,14 +1093,14 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   const unsigned hw = std::thread::hardware_concurrency();
   const size_t T = N >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), G) : 1;
   if (T > 1 && !r->verify_fn && !r->vsub) {
-    rc = fill_and_launch(r, T, SIG, K, IDX, ENV, E);
+    rc = fill_and_launch(r, T, SIG, K, IDX, ENV, E, rs);
     r->in_flight_via = 0;
     if (rc) { revert_segs(r); return rc; }
     r->in_flight = true;
     return PBFT_OK;
   }
   if (T <= 1) {
-    fill_segs(r, 0, G, SIG, K, IDX, ENV);
+    fill_segs(r, 0, G, SIG, K, IDX, ENV, rs);
   } else {
     std::vector<size_t> cut(T + 1, G);
     cut[0] = 0;
@@ -1077,7 +1111,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
       cut[t + 1] = s1;
     }
     WorkerPool::get().run(T, [&](size_t t) {
-      if (cut[t + 1] > cut[t]) fill_segs(r, cut[t], cut[t + 1], SIG, K, IDX, ENV);
+      if (cut[t + 1] > cut[t]) fill_segs(r, cut[t], cut[t + 1], SIG, K, IDX, ENV, rs);
     });
   }
   // 3. launch

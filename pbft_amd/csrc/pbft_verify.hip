@@ -123,12 +123,13 @@ static void keyset_release(keyset* k) {
   }
 }
 
-// Votes rows in the context's pinned staging (the replica's flush, pbft_verify_votes_stage, pageable votes inputs)
-// are read by the comb kernel straight from host memory over PCIe instead of being copied to HBM first: the reads
-// overlap the arithmetic wave by wave instead of chunk by chunk (env PBFT_VOTES_ZERO_COPY, option
-// PBFT_OPT_VOTES_ZERO_COPY).
+// 1: votes rows in the context's pinned staging (the replica's flush, pbft_verify_votes_stage, pageable votes
+// inputs) are read by the comb kernel straight from host memory over PCIe instead of being copied to HBM first
+// (env PBFT_VOTES_ZERO_COPY, option PBFT_OPT_VOTES_ZERO_COPY).  Measured slower, so off by default: a 2^20 staged
+// round 2.69 ms against 1.97 ms with chunked copies (profiles/r04/zc_probe.json) -- every wave generation waits
+// for its rows at its start, so PCIe and the arithmetic take turns instead of overlapping.
 #ifndef PBFT_VOTES_ZERO_COPY
-#define PBFT_VOTES_ZERO_COPY 1
+#define PBFT_VOTES_ZERO_COPY 0
 #endif
 
 struct pbft_ctx {
@@ -257,14 +258,15 @@ static bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// Columnar pinned layout of a votes batch (pbft_verify_votes_stage) / a per-signature batch.
+// Pinned layout of a staged votes batch (pbft_verify_votes_stage): n rows of PBFT_VOTES_ROW_BYTES, then the
+// envelopes.
+static constexpr uint32_t ROW = PBFT_VOTES_ROW_BYTES;
+static_assert(PBFT_VOTES_ROW_BYTES % 8 == 0 && PBFT_VOTES_ROW_KEY == 64 && PBFT_VOTES_ROW_ENV % 4 == 0 &&
+                  PBFT_VOTES_ROW_ENV + 4 <= PBFT_VOTES_ROW_BYTES, "votes row layout");
 struct host_votes_layout {
-  size_t offS, offK, offI, offE, bytes;
+  size_t offE, bytes;
   host_votes_layout(uint64_t n, uint32_t n_env) {
-    offS = 32 * n;
-    offK = 64 * n;
-    offI = (offK + 2 * n + 15) & ~(size_t)15;
-    offE = (offI + 4 * n + 255) & ~(size_t)255;
+    offE = (ROW * (size_t)n + 255) & ~(size_t)255;
     bytes = offE + (size_t)PBFT_ENVELOPE_LEN * n_env + 64;  // + read slack of the envelope loads
   }
 };
@@ -378,7 +380,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
                          uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
                          const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr,
-                         bool r_host = false) {
+                         bool r_host = false, uint32_t mi_stride = 1) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
@@ -401,7 +403,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.xyz = (uint32_t*)hw;
   a.flags = hw + 120 * N;  // within the half's 121 W bytes
   a.eidx = (uint32_t*)(c->d_work + eidx_offset(W));
-  a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
+  a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.mi_stride = mi_stride; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
   if (r_host && !latency_mode) a.r_copy = (uint32_t*)(c->d_work + rcopy_offset(W, c->work_two));
@@ -553,13 +555,16 @@ static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, h
 // signature (70 B instead of 151 B over PCIe) + the batch's table of distinct 85-byte envelopes.
 // Device chunk layout: R | S (rs_stride 32), or the signatures as 64-byte R || S rows (rs_stride 64, the
 // staging of pbft_verify_votes_stage), then key_idx and env_idx.
+// One chunk's device staging: R | S | key_idx | env_idx columns (caller columns), or the chunk's rows as staged
+// (PBFT_VOTES_ROW_BYTES each, one copy).
 struct votes_layout {
   size_t offS, offK, offI, bytes;
   explicit votes_layout(uint64_t n) {
     offS = 32 * n;
     offK = 64 * n;
     offI = (offK + 2 * n + 15) & ~(size_t)15;
-    bytes = (offI + 4 * n + 255) & ~(size_t)255;
+    const size_t cols = (offI + 4 * n + 255) & ~(size_t)255, rows = (ROW * (size_t)n + 255) & ~(size_t)255;
+    bytes = cols > rows ? cols : rows;
   }
 };
 
@@ -571,7 +576,8 @@ static const uint8_t* zc_dev(const pbft_ctx* c, const void* p, size_t bytes) {
   return c->h_stage_dev + (q - c->h_stage);
 }
 
-// rs_stride 32: R and S are separate [N][32] host columns; 64: R = the [N][64] signature rows, S = R + 32.
+// rs_stride 32: R and S are separate [N][32] host columns (key_idx, env_idx columns too); PBFT_VOTES_ROW_BYTES: R
+// = the staged rows (S = R + 32, key_idx at + 64, env_idx at + 68 of each row).
 // votes_begin copies the envelope table and launches its schedule; votes_launch then launches every whole chunk
 // inside rows [0, rows) (all the rest once rows >= N): the kernels of chunk c run on the context stream after
 // its copies (copy stream), overlapping the copies of chunk c+1.
@@ -618,15 +624,17 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     const uint64_t lo = c->v_next;
     const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
     const int b = (int)(c->v_chunk & 1);
+    const bool rows_form = rs_stride == ROW;
     const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
-    const uint8_t* zS = rs_stride == 64 ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
-    const uint8_t* zK = zc_dev(c, K + lo, 2 * n);
-    const uint8_t* zI = zc_dev(c, IDX + lo, 4 * n);
+    const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
+    const uint8_t* zK = rows_form ? zR + PBFT_VOTES_ROW_KEY : zc_dev(c, K + lo, 2 * n);
+    const uint8_t* zI = rows_form ? zR + PBFT_VOTES_ROW_ENV : zc_dev(c, IDX + lo, 4 * n);
+    const uint32_t ks = rows_form ? ROW : 2, mis = rows_form ? ROW / 4 : 1;
     if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
       int rc = 0;
       LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
-                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
-                                       (const uint32_t*)zI, c->v_env, c->v_wk, true));
+                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, ks, nullptr,
+                                       (const uint32_t*)zI, c->v_env, c->v_wk, true, mis));
       if (rc) return rc;
       if (c->v_readback) {
         LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, c->stream)));
@@ -638,21 +646,24 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     }
     uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
     if (c->v_chunk >= 2) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
-    if (rs_stride == 64) {
-      LT("h2d_sig", HIP_TRY(hipMemcpyAsync(base, R + 64 * lo, 64 * n, hipMemcpyHostToDevice, c->cstream)));
+    if (rows_form) {  // the chunk's rows: one copy
+      LT("h2d_rows", HIP_TRY(hipMemcpyAsync(base, R + (size_t)ROW * lo, (size_t)ROW * n, hipMemcpyHostToDevice,
+                                            c->cstream)));
     } else {
       HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
       HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+      LT("h2d_key", HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream)));
+      LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
     }
-    LT("h2d_key", HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream)));
-    LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
     LT("rec_copied", HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream)));
     LT("wait_copied", HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0)));
     int rc = 0;
-    LT("kernels", rc = launch_verify(c, base, rs_stride == 64 ? base + 32 : base + L.offS,
-                                     (const uint16_t*)(base + L.offK), c->d_stage, PBFT_ENVELOPE_LEN,
-                                     PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, 2, nullptr,
-                                     (const uint32_t*)(base + L.offI), c->v_env, c->v_wk));
+    LT("kernels", rc = launch_verify(c, base, base + (rows_form ? 32 : L.offS),
+                                     (const uint16_t*)(base + (rows_form ? PBFT_VOTES_ROW_KEY : L.offK)), c->d_stage,
+                                     PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream,
+                                     rs_stride, ks, nullptr,
+                                     (const uint32_t*)(base + (rows_form ? PBFT_VOTES_ROW_ENV : L.offI)), c->v_env,
+                                     c->v_wk, false, mis));
     if (rc) return rc;
     LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream)));
     if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
@@ -1079,10 +1090,11 @@ int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_
   int rc = ensure_host_stage(c, L.bytes);
   if (rc) return rc;
   uint8_t* h = c->h_stage;
-  out->sig = h;  // [N][64]: R || S rows over the R and S columns of the layout
-  out->key_idx = (uint16_t*)(h + L.offK);
-  out->env_idx = (uint32_t*)(h + L.offI);
+  out->sig = h;
+  out->key_idx = (uint16_t*)(h + PBFT_VOTES_ROW_KEY);
+  out->env_idx = (uint32_t*)(h + PBFT_VOTES_ROW_ENV);
   out->envelopes = h + L.offE;
+  out->row_stride = ROW;
   c->staged = true;
   c->staged_n = N;
   c->staged_env = n_env;
@@ -1101,8 +1113,8 @@ int pbft_verify_votes_submit(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* 
   HIP_TRY(hipSetDevice(c->device));
   const host_votes_layout L(N, n_env);
   uint8_t* h = c->h_stage;
-  return votes_submit_from(c, h, h + 32, (const uint16_t*)(h + L.offK), (const uint32_t*)(h + L.offI), h + L.offE,
-                           n_env, N, out, 64);
+  return votes_submit_from(c, h, h + 32, (const uint16_t*)(h + PBFT_VOTES_ROW_KEY),
+                           (const uint32_t*)(h + PBFT_VOTES_ROW_ENV), h + L.offE, n_env, N, out, ROW);
 }
 
 // Progressive form: the caller fills the staging front to back and launches as it goes.
@@ -1129,9 +1141,9 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   if (!c->in_flight || !c->v_open) return set_err(PBFT_EINVAL, "no progressive votes batch open");
   HIP_TRY(hipSetDevice(c->device));
   const uint64_t N = c->v_n;
-  const host_votes_layout L(N, c->v_env);
   uint8_t* h = c->h_stage;
-  int rc = votes_launch(c, h, h + 32, (const uint16_t*)(h + L.offK), (const uint32_t*)(h + L.offI), 64, rows);
+  int rc = votes_launch(c, h, h + 32, (const uint16_t*)(h + PBFT_VOTES_ROW_KEY), (const uint32_t*)(h + PBFT_VOTES_ROW_ENV),
+                        ROW, rows);
   if (rc == PBFT_OK && !c->v_open)
     rc = hipEventRecord(c->ev_done, c->stream) == hipSuccess ? PBFT_OK : set_err(PBFT_EHIP, "event record");
   if (rc) {  // the batch is lost: drain what was launched, the context stays usable
@@ -1184,11 +1196,13 @@ int pbft_verify_votes_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   int rc = pbft_verify_votes_stage(c, N, n_env, &st);
   if (rc) return rc;
   for (uint64_t i = 0; i < N; ++i) {
-    memcpy(st.sig + 64 * i, R + 32 * i, 32);
-    memcpy(st.sig + 64 * i + 32, S + 32 * i, 32);
+    uint8_t* row = st.sig + (size_t)ROW * i;
+    memcpy(row, R + 32 * i, 32);
+    memcpy(row + 32, S + 32 * i, 32);
+    const uint32_t kp = K[i];  // key_idx, two zero bytes
+    memcpy(row + PBFT_VOTES_ROW_KEY, &kp, 4);
+    memcpy(row + PBFT_VOTES_ROW_ENV, I + i, 4);
   }
-  memcpy(st.key_idx, K, 2 * N);
-  memcpy(st.env_idx, I, 4 * N);
   memcpy(st.envelopes, E, (size_t)PBFT_ENVELOPE_LEN * n_env);
   return pbft_verify_votes_submit(c, N, n_env, out);
 }

@@ -228,7 +228,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
-    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg,
+    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
     const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy) {
   using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     // the signed message: row ii, or the envelope table row msg_idx[ii] (votes form; out of range -> bit 0)
     uint64_t mrow = ii;
     if (msg_idx) {
-      mrow = msg_idx[ii];
+      mrow = msg_idx[(size_t)mi_stride * ii];
       kok = kok && mrow < n_msg;
       if (mrow >= n_msg) mrow = 0;
     }
@@ -450,7 +450,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Lpad,
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint64_t* __restrict__ bitmap,
-    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg,
+    const uint8_t** __restrict__ eaddr, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
     const uint64_t* __restrict__ wk) {
   static_assert(SPLIT == 4 || SPLIT == 8, "2 or 3 combine rounds");
   static_assert(!PBFT_LAT_DECOMP || SPLIT == 4, "the decompression-wave variant pairs 4 lanes per signature");
@@ -522,7 +522,7 @@ __global__ void __launch_bounds__(LAT_BLOCK, 1) comb_latency_kernel(
     }
     uint64_t mrow = ii;
     if (msg_idx) {
-      mrow = msg_idx[ii];
+      mrow = msg_idx[(size_t)mi_stride * ii];
       kok = kok && mrow < n_msg;
       if (mrow >= n_msg) mrow = 0;
     }
@@ -684,6 +684,7 @@ struct comb_launch_args {
   uint32_t* eidx;          // entry-index workspace (latency mode: 64-bit entry addresses)
   uint64_t* bitmap;        // latency mode writes the bitmap itself
   const uint32_t* msg_idx; // votes form (null: one message per signature)
+  uint32_t mi_stride = 1;  // msg_idx[mi_stride * i] (the votes rows layout: PBFT_VOTES_ROW_BYTES / 4)
   uint32_t n_msg;
   const uint64_t* wk;      // votes form, 85-byte envelopes: per-envelope block-2 schedule (null: hash in full)
   uint32_t* r_copy = nullptr;  // one-lane mode: [N][8] copy of R for the finish (R read from host memory)
@@ -705,7 +706,7 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
 #define PBFT_LAUNCH_LAT(LEN_, SPL_)                                                                               \
   hipLaunchKernelGGL((comb_latency_kernel<LEN_, PLA, SPL_>), dim3((unsigned)sblocks), dim3(LAT_BLOCK), LAT_LDS, a.st, \
                      a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Lpad, a.tabB, a.tabA,   \
-                     a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg, a.wk)
+                     a.keys, a.key_ok, a.n_keys, a.bitmap, (const uint8_t**)a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk)
     if (a.msg_len == PBFT_ENVELOPE_LEN) {
       if (split == 8 && !PBFT_LAT_DECOMP) PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 8 - 4 * PBFT_LAT_DECOMP);
       else PBFT_LAUNCH_LAT(PBFT_ENVELOPE_LEN, 4);
@@ -720,15 +721,15 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
     if (a.msg_len == PBFT_ENVELOPE_LEN && N >= PBFT_CHAIN_MIN_N)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st,
                          a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,
-                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy);
     else if (a.msg_len == PBFT_ENVELOPE_LEN)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
                          a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
-                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
+                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy);
     else
       hipLaunchKernelGGL((comb_kernel<-1, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R, a.S, a.K,
                          a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,
-                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.wk, a.r_copy);
+                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy);
   }
   return hipGetLastError();
 }

@@ -66,7 +66,7 @@ class KeyStats(ctypes.Structure):
 class VotesStaging(ctypes.Structure):
     """pbft_votes_staging (include/pbft_verify.h)."""
     _fields_ = [("sig", ctypes.c_void_p), ("key_idx", ctypes.c_void_p), ("env_idx", ctypes.c_void_p),
-                ("envelopes", ctypes.c_void_p)]
+                ("envelopes", ctypes.c_void_p), ("row_stride", ctypes.c_uint32)]
 
 
 def bitmap_to_bool(bitmap: np.ndarray, n: int) -> np.ndarray:
@@ -249,7 +249,8 @@ class GpuBatchVerifier:
 
     def stage_votes(self, n: int, n_env: int) -> dict:
         """pbft_verify_votes_stage: numpy views of the context's pinned staging for an (n, n_env) votes batch
-        (sig rows R || S, key_idx, env_idx, envelopes), to be filled in place and launched by submit_staged.
+        (72-byte rows: sig R || S, key_idx, env_idx as strided views of them; envelopes), to be filled in place and
+        launched by submit_staged.
         The views are valid only until the next call on this context that uses the staging (another stage_votes,
         or any host-buffer submit / verify): do not touch them afterwards."""
         st = VotesStaging()
@@ -261,8 +262,13 @@ class GpuBatchVerifier:
                 return np.zeros(shape, dtype)
             buf = (ctypes.c_uint8 * (count * np.dtype(dtype).itemsize)).from_address(ptr)
             return np.frombuffer(buf, dtype=dtype).reshape(shape)
-        return {"sig": view(st.sig, np.uint8, (n, 64)), "key_idx": view(st.key_idx, np.uint16, (n,)),
-                "env_idx": view(st.env_idx, np.uint32, (n,)), "envelopes": view(st.envelopes, np.uint8, (n_env, 85))}
+        # the rows (PBFT_VOTES_ROW_BYTES each: signature, key_idx at 64, env_idx at 68) as one byte array, the
+        # three fields as strided views of it
+        rs = int(st.row_stride)
+        rows = view(st.sig, np.uint8, (n, rs))
+        return {"sig": rows[:, :64], "key_idx": rows[:, 64:66].view(np.uint16).reshape(n),
+                "env_idx": rows[:, 68:72].view(np.uint32).reshape(n), "rows": rows,
+                "envelopes": view(st.envelopes, np.uint8, (n_env, 85))}
 
     def submit_staged(self, n: int, n_env: int) -> int:
         out = np.zeros((n + 63) // 64, dtype=np.uint64)

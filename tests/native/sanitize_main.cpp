@@ -54,9 +54,9 @@ int pbft_verify_update_keys(pbft_ctx*, const uint32_t*, const uint8_t*, uint32_t
 // its rows were filled is caught, and one chunk of the library's schedule (PBFT_VOTES_CHUNK_END) "completing" per poll.  A row verifies iff its
 // signature's first byte is not 0xEE (no curve arithmetic: the point is the host's threads and bookkeeping).
 struct FakeGpu {
-  std::vector<uint8_t> sig, env;
-  std::vector<uint16_t> K;
-  std::vector<uint32_t> I;
+  std::vector<uint8_t> rows, env;  // staged rows of PBFT_VOTES_ROW_BYTES (include/pbft_verify.h), envelopes
+  uint16_t key(uint64_t i) const { uint16_t k; memcpy(&k, &rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY], 2); return k; }
+  uint32_t idx(uint64_t i) const { uint32_t x; memcpy(&x, &rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_ENV], 4); return x; }
   uint64_t N = 0, launched = 0, done = 0;
   uint32_t n_env = 0, n_keys = 0;
   uint64_t* out = nullptr;
@@ -69,11 +69,12 @@ int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_
   FakeGpu* g = (FakeGpu*)c;
   if (!g) return PBFT_ENODEV;
   CHECK(!g->in_flight);
-  g->sig.assign(64 * N, 0);
-  g->K.assign(N, 0xFFFF);
-  g->I.assign(N, 0);
+  g->rows.assign((size_t)PBFT_VOTES_ROW_BYTES * N, 0);
+  for (uint64_t i = 0; i < N; ++i) memset(&g->rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY], 0xFF, 2);
   g->env.assign((size_t)PBFT_ENVELOPE_BYTES * n_env, 0);
-  st->sig = g->sig.data(); st->key_idx = g->K.data(); st->env_idx = g->I.data(); st->envelopes = g->env.data();
+  uint8_t* h = g->rows.data();
+  st->sig = h; st->key_idx = (uint16_t*)(h + PBFT_VOTES_ROW_KEY); st->env_idx = (uint32_t*)(h + PBFT_VOTES_ROW_ENV);
+  st->envelopes = g->env.data(); st->row_stride = PBFT_VOTES_ROW_BYTES;
   g->N = N; g->n_env = n_env; g->staged = true;
   return 0;
 }
@@ -91,7 +92,7 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   uint64_t upto = g->launched;  // every whole chunk of the library's schedule inside [0, rows)
   while (upto < g->N && PBFT_VOTES_CHUNK_END(upto, g->N) <= (rows >= g->N ? g->N : rows))
     upto = PBFT_VOTES_CHUNK_END(upto, g->N);
-  for (uint64_t i = g->launched; i < upto; ++i) CHECK(g->K[i] != 0xFFFF && g->I[i] < g->n_env);  // filled
+  for (uint64_t i = g->launched; i < upto; ++i) CHECK(g->key(i) != 0xFFFF && g->idx(i) < g->n_env);  // filled
   if (upto > g->launched) { g->launched = upto; ++g->chunk_launches; }
   if (g->launched == g->N) g->open = false;
   return 0;
@@ -103,7 +104,7 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
     const uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
     for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
     for (uint64_t i = g->done; i < hi; ++i)
-      if (g->sig[64 * i] != 0xEE && g->K[i] < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
+      if (g->rows[(size_t)PBFT_VOTES_ROW_BYTES * i] != 0xEE && g->key(i) < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
     g->done = hi;
   }
   *rows_done = g->done;

@@ -657,6 +657,39 @@ def test_progressive_votes_submit(gv, coracle):
     assert (bitmap_to_bool(gv.verify_votes(R, S, K, ei, env), len(R)) == exp).all()
 
 
+def test_votes_zero_copy_equals_copied(gv, coracle):
+    """PBFT_OPT_VOTES_ZERO_COPY (r04, off by default: slower): votes rows in the context's pinned staging are read
+    by the kernels in place over PCIe (the comb leaves an HBM copy of R for the finish) instead of being copied to
+    HBM chunk by chunk.  On
+    the staged path (pbft_verify_votes_stage / _submit) and the pageable path (copied into the staging first), at
+    a multi-chunk size, one chunk, and latency-mode sizes (that kernel reads R at the end too), both settings give
+    the oracle's bits."""
+    from pbft_amd import bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=53)   # 65,536 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(53)
+    R, S, K, M, _ = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R, S, K, M, 85)
+    env, inv = np.unique(M, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    big = (1 << 18) + 3 * (1 << 16) + 77                                  # chunks 2^16, 2^17, 2^18, rest
+    reps = big // len(R) + 1
+    RR, SS, KK, II, EE = (np.concatenate([a] * reps)[:big] for a in (R, S, K, ei, exp))
+    try:
+        for zc in (1, 0):
+            gv.set_option(gv.OPT_VOTES_ZERO_COPY, zc)
+            for n in (big, 1 << 16, 4096, 777):
+                st = gv.stage_votes(n, len(env))
+                st["sig"][:, :32], st["sig"][:, 32:] = RR[:n], SS[:n]
+                st["key_idx"][:], st["env_idx"][:], st["envelopes"][:] = KK[:n], II[:n], env
+                got = bitmap_to_bool(gv.wait(gv.submit_staged(n, len(env))), n)
+                assert (got == EE[:n]).all(), ("staged", zc, n, np.nonzero(got != EE[:n])[0][:8])
+                got = bitmap_to_bool(gv.verify_votes(RR[:n], SS[:n], KK[:n], II[:n], env), n)
+                assert (got == EE[:n]).all(), ("pageable", zc, n)
+    finally:
+        gv.set_option(gv.OPT_VOTES_ZERO_COPY, 0)
+
+
 def test_multi_gpu_rccl_allgather_one_rank(gv, coracle):
     """pbft_multi_create / pbft_verify_batch_device_multi on the one GPU of this box: a
     1-rank RCCL communicator, the shard verified into its slice of the padded rank-major bitmap, then

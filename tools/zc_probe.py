@@ -3,7 +3,7 @@
 2^20-vote round staged in the context's pinned staging (pbft_verify_votes_stage), then submit + wait timed
 (the GPU pipeline alone: the fill is done before the clock starts), and the pageable pbft_verify_votes call
 (copy into the staging + the same pipeline).  Every bitmap is checked against the corrupted positions.
-usage: python tools/zc_probe.py [rounds]"""
+usage: python tools/zc_probe.py [rounds] [settings, default 1,0]"""
 import json
 import os
 import sys
@@ -20,6 +20,7 @@ def main():
     from pbft_amd import GpuBatchVerifier, bitmap_to_bool
     torch.cuda.set_device(0)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    settings = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,0").split(",")]
     seeds = bench.key_seeds(bench.N_REPLICAS)
     msg, key_idx = bench.envelopes(1, bench.SEQS, bench.N_REPLICAS)
     v = GpuBatchVerifier(0)
@@ -31,9 +32,9 @@ def main():
     env, inv = np.unique(msg, axis=0, return_inverse=True)
     inv = inv.reshape(-1).astype(np.uint32)
     n, ne = len(msg), len(env)
-    res = {0: {"staged": [], "pageable": []}, 1: {"staged": [], "pageable": []}}
+    res = {zc: {"staged": [], "pageable": []} for zc in settings}
     for r in range(rounds + 1):
-        for zc in (1, 0):
+        for zc in settings:
             v.set_option(v.OPT_VOTES_ZERO_COPY, zc)
             st = v.stage_votes(n, ne)
             st["sig"][:, :32] = R
@@ -53,7 +54,7 @@ def main():
                 res[zc]["staged"].append(dt)
                 res[zc]["pageable"].append(dp)
     out = {}
-    for zc in (1, 0):
+    for zc in settings:
         for k, x in res[zc].items():
             x = np.array(x)
             out[f"zc{zc}_{k}_ms"] = {"median": float(np.median(x)), "min": float(x.min()), "max": float(x.max()),
