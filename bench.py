@@ -142,7 +142,7 @@ def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_prof.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
-    for rel in ("r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
+    for rel in ("r04/pmc_comb", "r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
         p = os.path.join(ROOT, "profiles", rel, "derived.json")
         try:
             d = json.load(open(p))

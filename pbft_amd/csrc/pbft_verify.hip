@@ -132,6 +132,13 @@ static void keyset_release(keyset* k) {
 #define PBFT_VOTES_ZERO_COPY 0
 #endif
 
+// device staging buffers of the votes chunks (chunk c uses buffer c % VOTES_BUFS; its copy waits for the kernels
+// of chunk c - VOTES_BUFS)
+static constexpr int VOTES_BUFS = 4;
+#ifndef PBFT_VOTES_TWO_STREAMS
+#define PBFT_VOTES_TWO_STREAMS 1
+#endif
+
 struct pbft_ctx {
   int device = -1;
   hipStream_t stream = nullptr;
@@ -175,9 +182,19 @@ struct pbft_ctx {
   hipEvent_t ev_comb = nullptr, ev_fin[2] = {nullptr, nullptr};
   bool fin_pending[2] = {false, false};
   int half = 0;
-  // host-buffer pipeline: H2D of chunk c+1 (copy stream) overlaps the kernels of chunk c
+  // host-buffer pipeline: H2D of chunk c+1 (copy stream) overlaps the kernels of chunk c; VOTES_BUFS device
+  // staging buffers (the per-signature form uses 2)
   hipStream_t cstream = nullptr;
-  hipEvent_t ev_copied[2] = {nullptr, nullptr}, ev_consumed[2] = {nullptr, nullptr};
+  hipEvent_t ev_copied[VOTES_BUFS] = {}, ev_consumed[VOTES_BUFS] = {};
+  // votes chunks alternate between the context stream and stream2, each with its own workspace, so that the
+  // kernels of consecutive chunks may overlap (PBFT_VOTES_TWO_STREAMS)
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_env = nullptr, ev_s2 = nullptr;
+  uint8_t* d_work2 = nullptr;
+  size_t work2_cap = 0;
+  uint64_t work2_n = 0;
+  bool v_two = false;
+  bool two_streams = PBFT_VOTES_TWO_STREAMS;  // env PBFT_VOTES_TWO_STREAMS
   bool in_flight = false;
   uint64_t* async_out = nullptr;
   uint64_t* h_bitmap = nullptr;      // pinned, fine-grained
@@ -374,27 +391,49 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   return PBFT_OK;
 }
 
+// The second workspace (votes chunks on stream2): one half, same layout.
+static int ensure_work2(pbft_ctx* c, uint64_t N) {
+  if (N <= c->work2_n) return PBFT_OK;
+  const uint64_t W = N;
+  const size_t need = rcopy_offset(W, false) + 32 * (size_t)W + 256;
+  if (c->d_work2) {
+    HIP_TRY(hipStreamSynchronize(c->stream2));
+    HIP_TRY(hipFree(c->d_work2));
+  }
+  c->d_work2 = nullptr;
+  c->work2_cap = 0;
+  c->work2_n = 0;
+  if (hipMalloc(&c->d_work2, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
+  c->work2_cap = need;
+  c->work2_n = W;
+  return PBFT_OK;
+}
+
 // fst != null: pipelined form -- the finish runs on fst after an event, on one of two
-// workspace halves, so the next launch's comb (on st) overlaps it.
+// workspace halves, so the next launch's comb (on st) overlaps it.  slot 1: the second workspace (votes chunks
+// on stream2; no timing events, never pipelined).
 static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, const uint16_t* dK, const uint8_t* dM,
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
                          uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
                          const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr,
-                         bool r_host = false, uint32_t mi_stride = 1) {
+                         bool r_host = false, uint32_t mi_stride = 1, int slot = 0) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
-  int rc = ensure_work(c, N, fst != nullptr);
+  int rc = slot ? ensure_work2(c, N) : ensure_work(c, N, fst != nullptr);
   if (rc) return rc;
+  uint8_t* const wbase = slot ? c->d_work2 : c->d_work;
+  const bool wtwo = slot ? false : c->work_two;
+  const bool timing = c->timing && slot == 0;
   int h = 0;
   if (fst) {
     h = c->half;
     c->half ^= 1;
   }
-  if (c->fin_pending[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));  // a pipelined finish still reading half h
-  if (c->timing) LT("rec_ev0", HIP_TRY(hipEventRecord(c->ev0, st)));
-  const uint64_t W = c->work_n;  // layout (>= N)
-  uint8_t* hw = c->d_work + (h ? half1_offset(W) : 0);
+  if (slot == 0 && c->fin_pending[h]) HIP_TRY(hipStreamWaitEvent(st, c->ev_fin[h], 0));  // a pipelined finish still reading half h
+  if (timing) LT("rec_ev0", HIP_TRY(hipEventRecord(c->ev0, st)));
+  const uint64_t W = slot ? c->work2_n : c->work_n;  // layout (>= N)
+  uint8_t* hw = wbase + (h ? half1_offset(W) : 0);
   const bool latency_mode = N < c->split_below;
   comb_launch_args a;
   a.R = dR; a.S = dS; a.K = (const uint8_t*)dK; a.rs_stride = rs_stride; a.k_stride = k_stride;
@@ -402,11 +441,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.tabB = c->d_tabB; a.tabA = c->d_tabA; a.keys = c->d_keys; a.key_ok = c->d_key_ok; a.n_keys = c->n_keys;
   a.xyz = (uint32_t*)hw;
   a.flags = hw + 120 * N;  // within the half's 121 W bytes
-  a.eidx = (uint32_t*)(c->d_work + eidx_offset(W));
+  a.eidx = (uint32_t*)(wbase + eidx_offset(W));
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.mi_stride = mi_stride; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
-  if (r_host && !latency_mode) a.r_copy = (uint32_t*)(c->d_work + rcopy_offset(W, c->work_two));
+  if (r_host && !latency_mode) a.r_copy = (uint32_t*)(wbase + rcopy_offset(W, wtwo));
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
   LT("comb", HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
@@ -415,7 +454,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
                                            : launch_comb_small(a)));
   HIP_TRY(hipGetLastError());
   if (fst) {
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
+    if (timing) HIP_TRY(hipEventRecord(c->ev1, st));  // pipelined form: last_kernel_ms = the comb (or latency) kernel
     HIP_TRY(hipEventRecord(c->ev_comb, st));
     HIP_TRY(hipStreamWaitEvent(fst, c->ev_comb, 0));
     st = fst;
@@ -440,7 +479,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     c->fin_pending[h] = true;
     return PBFT_OK;
   }
-  if (c->timing) LT("rec_ev1", HIP_TRY(hipEventRecord(c->ev1, st)));
+  if (timing) LT("rec_ev1", HIP_TRY(hipEventRecord(c->ev1, st)));
   return PBFT_OK;
 }
 
@@ -586,8 +625,16 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
   const uint64_t ch = N < VOTES_CHUNK ? N : VOTES_CHUNK;
   const votes_layout L(ch);
-  int rc = ensure_stage(c, env_bytes + (N > VOTES_CHUNK ? 2 : 1) * L.bytes, words);
+  int rc = ensure_stage(c, env_bytes + (N > VOTES_CHUNK ? VOTES_BUFS : 1) * L.bytes, words);
   if (rc) return rc;
+  // more than one chunk: odd chunks' kernels on stream2 (their own workspace), so consecutive chunks' kernels may
+  // overlap -- the small first chunks and the last big one leave most of the GPU idle on one stream
+  const bool two = c->two_streams && N > PBFT_VOTES_FIRST_ROWS;
+  if (two && !c->stream2) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_env, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming));
+  }
   if (readback) {
     uint64_t chunks = 0;
     for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ++chunks;
@@ -604,6 +651,11 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[0], 0));
   rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &c->v_wk);
   if (rc) return rc;
+  if (two) {  // stream2's chunks read the envelope table and its schedule too
+    HIP_TRY(hipEventRecord(c->ev_env, c->stream));
+    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_env, 0));
+  }
+  c->v_two = two;
   c->v_n = N;
   c->v_next = 0;
   c->v_chunk = 0;
@@ -623,7 +675,9 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
   while (c->v_next < N && (rows >= N || PBFT_VOTES_CHUNK_END(c->v_next, N) <= rows)) {
     const uint64_t lo = c->v_next;
     const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
-    const int b = (int)(c->v_chunk & 1);
+    const int b = (int)(c->v_chunk % VOTES_BUFS);
+    const int slot = c->v_two ? (int)(c->v_chunk & 1) : 0;
+    hipStream_t st = slot ? c->stream2 : c->stream;
     const bool rows_form = rs_stride == ROW;
     const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
     const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
@@ -633,19 +687,19 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
       int rc = 0;
       LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
-                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream, rs_stride, ks, nullptr,
-                                       (const uint32_t*)zI, c->v_env, c->v_wk, true, mis));
+                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st, rs_stride, ks, nullptr,
+                                       (const uint32_t*)zI, c->v_env, c->v_wk, true, mis, slot));
       if (rc) return rc;
       if (c->v_readback) {
-        LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, c->stream)));
-        LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream)));
+        LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
+        LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
       }
       c->v_next += n;
       ++c->v_chunk;
       continue;
     }
     uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
-    if (c->v_chunk >= 2) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
+    if (c->v_chunk >= VOTES_BUFS) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
     if (rows_form) {  // the chunk's rows: one copy
       LT("h2d_rows", HIP_TRY(hipMemcpyAsync(base, R + (size_t)ROW * lo, (size_t)ROW * n, hipMemcpyHostToDevice,
                                             c->cstream)));
@@ -656,24 +710,30 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
       LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
     }
     LT("rec_copied", HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream)));
-    LT("wait_copied", HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[b], 0)));
+    LT("wait_copied", HIP_TRY(hipStreamWaitEvent(st, c->ev_copied[b], 0)));
     int rc = 0;
     LT("kernels", rc = launch_verify(c, base, base + (rows_form ? 32 : L.offS),
                                      (const uint16_t*)(base + (rows_form ? PBFT_VOTES_ROW_KEY : L.offK)), c->d_stage,
-                                     PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, c->stream,
+                                     PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st,
                                      rs_stride, ks, nullptr,
                                      (const uint32_t*)(base + (rows_form ? PBFT_VOTES_ROW_ENV : L.offI)), c->v_env,
-                                     c->v_wk, false, mis));
+                                     c->v_wk, false, mis, slot));
     if (rc) return rc;
-    LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], c->stream)));
+    LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], st)));
     if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
-      LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, c->stream)));
-      LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], c->stream)));
+      LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
+      LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
     }
     c->v_next += n;
     ++c->v_chunk;
   }
-  if (c->v_next >= N) c->v_open = false;
+  if (c->v_next >= N) {
+    c->v_open = false;
+    if (c->v_two) {  // the context stream (ev_done, the final bitmap export) follows stream2's last chunk too
+      HIP_TRY(hipEventRecord(c->ev_s2, c->stream2));
+      HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+    }
+  }
   return PBFT_OK;
 }
 
@@ -759,22 +819,22 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
   if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
+  if (const char* e = getenv("PBFT_VOTES_TWO_STREAMS")) c->two_streams = strtol(e, nullptr, 10) != 0;
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
   HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_comb, hipEventDisableTiming));
-  for (int b = 0; b < 2; ++b) {
-    HIP_TRY(hipEventCreateWithFlags(&c->ev_fin[b], hipEventDisableTiming));
+  for (int b = 0; b < 2; ++b) HIP_TRY(hipEventCreateWithFlags(&c->ev_fin[b], hipEventDisableTiming));
+  for (int b = 0; b < VOTES_BUFS; ++b) {
     HIP_TRY(hipEventCreateWithFlags(&c->ev_copied[b], hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&c->ev_consumed[b], hipEventDisableTiming));
   }
   int rc = acquire_base_table(device, c->stream, &c->d_tabB);
   if (rc) {
     (void)hipEventDestroy(c->ev0); (void)hipEventDestroy(c->ev1); (void)hipEventDestroy(c->ev_done);
-    for (int b = 0; b < 2; ++b) {
-      (void)hipEventDestroy(c->ev_copied[b]); (void)hipEventDestroy(c->ev_consumed[b]); (void)hipEventDestroy(c->ev_fin[b]);
-    }
+    for (int b = 0; b < 2; ++b) (void)hipEventDestroy(c->ev_fin[b]);
+    for (int b = 0; b < VOTES_BUFS; ++b) { (void)hipEventDestroy(c->ev_copied[b]); (void)hipEventDestroy(c->ev_consumed[b]); }
     (void)hipEventDestroy(c->ev_comb);
     (void)hipStreamDestroy(c->cstream);
     (void)hipStreamDestroy(c->stream);
@@ -800,10 +860,16 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   if (c->ev_done) (void)hipEventDestroy(c->ev_done);
   for (int b = 0; b < 2; ++b) {
     if (c->fin_pending[b]) (void)hipEventSynchronize(c->ev_fin[b]);
-    if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
-    if (c->ev_consumed[b]) (void)hipEventDestroy(c->ev_consumed[b]);
     if (c->ev_fin[b]) (void)hipEventDestroy(c->ev_fin[b]);
   }
+  for (int b = 0; b < VOTES_BUFS; ++b) {
+    if (c->ev_copied[b]) (void)hipEventDestroy(c->ev_copied[b]);
+    if (c->ev_consumed[b]) (void)hipEventDestroy(c->ev_consumed[b]);
+  }
+  if (c->stream2) { (void)hipStreamSynchronize(c->stream2); (void)hipStreamDestroy(c->stream2); }
+  if (c->ev_env) (void)hipEventDestroy(c->ev_env);
+  if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
+  (void)hipFree(c->d_work2);
   if (c->ev_comb) (void)hipEventDestroy(c->ev_comb);
   for (hipEvent_t e : c->ev_rows) (void)hipEventDestroy(e);
   if (c->cstream) { (void)hipStreamSynchronize(c->cstream); (void)hipStreamDestroy(c->cstream); }
@@ -985,6 +1051,7 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->lat_split = parent->lat_split;
   c->timing = parent->timing;
   c->zero_copy = parent->zero_copy;
+  c->two_streams = parent->two_streams;
   c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
@@ -1148,6 +1215,7 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
     rc = hipEventRecord(c->ev_done, c->stream) == hipSuccess ? PBFT_OK : set_err(PBFT_EHIP, "event record");
   if (rc) {  // the batch is lost: drain what was launched, the context stays usable
     (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     (void)hipStreamSynchronize(c->cstream);
     c->in_flight = false;
     c->v_open = false;
