@@ -35,7 +35,7 @@ def agg(name):
     return {k: sum(v) / len(v) for k, v in vals.items()}
 
 
-out = {"launch": f"comb_kernel<85> PB={pb} PA={pa} + finish_kernel, one 2^20-signature round", "sigs_per_launch": n}
+out = {"launch": f"comb_kernel<85> PB={pb} PA={pa} + finish_kernel, one {n}-signature launch", "sigs_per_launch": n}
 tot = 0.0
 for k in ("comb_kernel", "finish_kernel"):
     m = agg(k)
