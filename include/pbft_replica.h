@@ -122,8 +122,8 @@ typedef int (*pbft_batch_verify_fn)(void *user, const uint8_t *R, const uint8_t 
                                     uint64_t *bitmap_out);
 
 /* Optional asynchronous votes-form verifier (tests without a GPU, other backends): submit receives the
- * batch in the layout of pbft_verify_votes_stage -- sig[N][64] (R || S), key_idx[N], env_idx[N] and
- * envelopes[n_env][85]; envelopes[env_idx[i]] is signature i's message; buffers owned by the replica, valid
+ * batch as columns -- sig[N][64] (R || S), key_idx[N], env_idx[N] and envelopes[n_env][85] (not the 72-byte
+ * rows of pbft_verify_votes_stage); envelopes[env_idx[i]] is signature i's message; buffers owned by the replica, valid
  * until poll reports completion -- and returns 0 or a negative code; poll returns 1 once bitmap_out is
  * written, 0 while running, < 0 on failure. */
 typedef int (*pbft_votes_submit_fn)(void *user, const uint8_t *sig, const uint16_t *key_idx, const uint32_t *env_idx,
