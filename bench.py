@@ -725,19 +725,32 @@ def main():
     torch.cuda.synchronize()
     check_round()
 
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events on the launch stream: pipelined, a pair around every step's comb kernel (its finish runs on
+    # fin_stream); sequential, ONE pair around the whole timed region -- a pair per step adds two timestamp packets
+    # between the launches (the finish -> next comb gap grew from ~11 to ~20 us, profiles/r04/shard/), so the
+    # launch pair's average is the region's time / K (the ~11-us gap between launches included)
+    # (N > 1: per step as well, so that the all-gather on the same stream stays outside the kernels' time)
+    per_step = pipelined or ws > 1
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps if per_step else 1)]
     if ws > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    if not per_step:
+        evs[0][0].record(stream)
     for k in range(args.steps):
-        step(evs[k])
+        step(evs[k] if per_step else None)
+    if not per_step:
+        evs[0][1].record(stream)
     torch.cuda.synchronize()
     if ws > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    kern_ms = [a.elapsed_time(b) for a, b in evs]
-    kern_avg = float(np.mean(kern_ms))  # pipelined: the comb kernel (finish on fin_stream); sequential: the pair
+    if per_step:
+        kern_avg = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # pipelined: the comb kernel
+    else:
+        kern_avg = evs[0][0].elapsed_time(evs[0][1]) / args.steps  # the comb + finish pair
     if ws > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -33,7 +33,7 @@ the form r01 timed: that, not the VALU, was the gap to MI355X_MICROARCH.md's rat
 import re
 
 FIN_M = 8            # finish signatures per lane at >= 2^19 signatures (pbft_verify.hip PBFT_FIN_FM_BIG)
-FIN_TREE_LEVELS = 6
+FIN_TREE_LEVELS = 4  # finish.hip PBFT_FIN_LV: the product tree spans a 16-lane row (r04; 6 = the wave before)
 VALU_MAD_PEAK_PER_S = 31.19e12   # measured, profiles/r03/valu_clock.txt
 MAD_CYCLES_PER_WAVE_INSTR = 4.53  # per SIMD, at the measured clock
 MAD_CLOCK_HZ = 2.157e9            # in-kernel clock during that measurement
@@ -61,10 +61,11 @@ def products_comb(pb: int, pa: int) -> int:
 
 
 def products_per_verify(pb: int, pa: int) -> int:
-    """comb_kernel + finish_kernel<8, 6, 2>: 3 batch-inversion muls and 2 affine muls per signature, the product
-    tree's 12 muls per lane over FIN_M signatures, one wave inversion per 64 FIN_M signatures."""
+    """comb_kernel + finish_kernel<8, 4, 2>: 3 batch-inversion muls and 2 affine muls per signature, the product
+    tree's 2 x FIN_TREE_LEVELS muls per lane over FIN_M signatures, one row-uniform inversion per
+    2^FIN_TREE_LEVELS x FIN_M signatures."""
     return (products_comb(pb, pa) + 5 * 100 + 2 * FIN_TREE_LEVELS * 100 // FIN_M
-            + INV_PRODUCTS // (64 * FIN_M))
+            + INV_PRODUCTS // ((1 << FIN_TREE_LEVELS) * FIN_M))
 
 
 def gather_bytes_per_verify(pb: int, pa: int) -> int:
