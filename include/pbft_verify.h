@@ -188,16 +188,23 @@ int pbft_verify_votes_submit_begin(pbft_ctx *ctx, uint64_t N, uint32_t n_env, ui
 /* Chunk schedule of the votes forms from host buffers (each chunk: its H2D on the copy stream, its kernels, and in
  * the progressive form its bitmap words back): a batch of at most PBFT_VOTES_CHUNK_ROWS rows is one chunk; a larger
  * one starts with a PBFT_VOTES_FIRST_ROWS-row chunk and a 2 x PBFT_VOTES_FIRST_ROWS-row one, so that the first copy
- * starts after a small part of the rows is filled, then PBFT_VOTES_CHUNK_ROWS-row chunks.  The chunk starting at
- * row lo of an n-row batch ends at PBFT_VOTES_CHUNK_END(lo, n). */
+ * starts after a small part of the rows is filled, then PBFT_VOTES_CHUNK_ROWS-row chunks, and it ends with a
+ * ~2 x PBFT_VOTES_FIRST_ROWS-row and a ~PBFT_VOTES_FIRST_ROWS-row chunk, so that little compute is left once the
+ * last copy lands (the copies are the bound; r04: profiles/r04/votes_copies.txt).  Every chunk but the last is a
+ * multiple of 64 rows.  The chunk starting at row lo of an n-row batch ends at PBFT_VOTES_CHUNK_END(lo, n). */
 #define PBFT_VOTES_CHUNK_ROWS (1u << 18)
 #define PBFT_VOTES_FIRST_ROWS (1u << 16)
-#define PBFT_VOTES_CHUNK_SIZE_AT(lo) \
-  ((lo) == 0 ? PBFT_VOTES_FIRST_ROWS : (lo) == PBFT_VOTES_FIRST_ROWS ? 2 * PBFT_VOTES_FIRST_ROWS : PBFT_VOTES_CHUNK_ROWS)
-#define PBFT_VOTES_CHUNK_END(lo, n)                                                            \
-  ((uint64_t)(n) <= PBFT_VOTES_CHUNK_ROWS                                   ? (uint64_t)(n)  \
-   : (uint64_t)(lo) + PBFT_VOTES_CHUNK_SIZE_AT(lo) < (uint64_t)(n) ? (uint64_t)(lo) + PBFT_VOTES_CHUNK_SIZE_AT(lo) \
-                                                                   : (uint64_t)(n))
+static inline uint64_t pbft_votes_chunk_end(uint64_t lo, uint64_t n) {
+  const uint64_t F = PBFT_VOTES_FIRST_ROWS, C = PBFT_VOTES_CHUNK_ROWS, r = n - lo;
+  if (n <= C || lo >= n) return n;
+  if (lo == 0) return F;
+  if (lo == F) return 3 * F < n ? 3 * F : n;
+  if (r > C + 3 * F) return lo + C;                      /* at least 3F rows stay */
+  if (r > 4 * F) return lo + ((r - 3 * F) & ~(uint64_t)63); /* 2F + F stay */
+  if (r > 2 * F) return lo + ((r - F) & ~(uint64_t)63);     /* F stays */
+  return n;
+}
+#define PBFT_VOTES_CHUNK_END(lo, n) pbft_votes_chunk_end((uint64_t)(lo), (uint64_t)(n))
 int pbft_verify_votes_submit_rows(pbft_ctx *ctx, uint64_t rows);
 int pbft_verify_poll_rows(pbft_ctx *ctx, uint64_t *rows_done);
 

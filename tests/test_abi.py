@@ -18,6 +18,10 @@ def declared_functions():
     for h in HEADERS:
         src = re.sub(r"/\*.*?\*/", "", open(h).read(), flags=re.S)
         src = re.sub(r"typedef[^;]*;", "", src)  # function-pointer typedefs are not exports
+        # header-only helpers (static inline, e.g. pbft_votes_chunk_end) are not exports either; nor are the calls
+        # inside their bodies or inside macros
+        src = re.sub(r"static inline[^{]*\{.*?\n\}", "", src, flags=re.S)
+        src = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", src)
         names |= set(re.findall(r"\b(pbft_[a-z0-9_]+)\s*\(", src))
     return sorted(names)
 

@@ -16,6 +16,8 @@ def _header_decls():
             continue
         src = re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", h)).read(), flags=re.S)
         src = re.sub(r"typedef[^;]*;", "", src)
+        src = re.sub(r"static inline[^{]*\{.*?\n\}", "", src, flags=re.S)  # header-only helpers: not exports
+        src = re.sub(r"#define[^\n]*(\\\n[^\n]*)*", "", src)
         for m in re.finditer(r"\b(pbft_[a-z0-9_]+)\s*\(([^;{]*?)\)\s*;", src, flags=re.S):
             args = m.group(2).strip()
             out[m.group(1)] = 0 if args in ("", "void") else args.count(",") + 1

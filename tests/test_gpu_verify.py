@@ -606,8 +606,9 @@ def test_progressive_votes_submit(gv, coracle):
     """pbft_verify_votes_submit_begin / _rows + pbft_verify_poll_rows (what pbft_replica_flush_submit and
     _flush_poll use): the staging is launched chunk by chunk as it is filled, each chunk's bitmap words come back
     on their own; until the last rows are submitted the batch reads "running" and a blocking wait is refused.
-    2^19 + 3 rows = chunks [0, 2^16), [2^16, 3 * 2^16), [3 * 2^16, 7 * 2^16), [7 * 2^16, 2^19 + 3) (the schedule of
-    include/pbft_verify.h PBFT_VOTES_CHUNK_END); every prefix reported done equals the oracle."""
+    2^19 + 3 rows = chunks [0, 2^16), [2^16, 3 * 2^16), [3 * 2^16, 5 * 2^16), [5 * 2^16, 7 * 2^16),
+    [7 * 2^16, 2^19 + 3) (the schedule of include/pbft_verify.h PBFT_VOTES_CHUNK_END: two small chunks at either
+    end); every prefix reported done equals the oracle."""
     import ctypes
     from pbft_amd import PbftError, bitmap_to_bool
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=47)   # 65,536 signatures
@@ -629,7 +630,7 @@ def test_progressive_votes_submit(gv, coracle):
     h = 1 << 18
     st["sig"][:h, :32], st["sig"][:h, 32:], st["key_idx"][:h], st["env_idx"][:h] = RR[:h], SS[:h], KK[:h], II[:h]
     assert L.pbft_verify_votes_submit_begin(ctx, N, len(env), out.ctypes.data) == 0
-    ends = [1 << 16, 3 << 16, 7 << 16, N]
+    ends = [1 << 16, 3 << 16, 5 << 16, 7 << 16, N]
     assert L.pbft_verify_votes_submit_rows(ctx, 1000) == 0                # no whole chunk yet
     assert L.pbft_verify_votes_submit_rows(ctx, h + 5) == 0               # chunks 0 and 1 (the filled rows' whole chunks)
     assert L.pbft_verify_poll(ctx) == 0
