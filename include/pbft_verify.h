@@ -179,7 +179,7 @@ int pbft_verify_votes_submit(pbft_ctx *ctx, uint64_t N, uint32_t n_env, uint64_t
 /* Progressive form of pbft_verify_votes_submit, so that filling the staging, the GPU and applying the results
  * overlap: after pbft_verify_votes_stage and with the envelopes filled, _submit_begin launches the envelope
  * table; the caller then fills the signature rows front to back and calls _submit_rows(rows) whenever rows
- * [0, rows) are filled -- every whole 2^18-row chunk inside is copied and launched -- and finally
+ * [0, rows) are filled -- every whole chunk of the schedule below inside is copied and launched -- and finally
  * _submit_rows(N).  pbft_verify_poll_rows returns like pbft_verify_poll and sets *rows_done: the bitmap words of
  * rows [0, rows_done) are already in bitmap_out (each chunk's words come back as soon as its kernels finish).
  * pbft_replica_flush_submit / _flush_poll use this.  Until _submit_rows(N) pbft_verify_poll reports "running"
