@@ -194,6 +194,7 @@ struct pbft_ctx {
   size_t work2_cap = 0;
   uint64_t work2_n = 0;
   bool v_two = false;
+  bool v_s2_ready = false;  // stream2 has waited for this batch's envelope table and schedule (ev_env)
   bool two_streams = PBFT_VOTES_TWO_STREAMS;  // env PBFT_VOTES_TWO_STREAMS
   bool in_flight = false;
   uint64_t* async_out = nullptr;
@@ -237,6 +238,13 @@ __global__ void export_words_kernel(const uint64_t* __restrict__ src, uint64_t* 
   __threadfence_system();
 }
 static hipError_t export_words(pbft_ctx* c, uint64_t lo, uint64_t n, hipStream_t st);
+// 16-byte words from host memory the kernels can address (the mapped staging) to device memory: one launch on the
+// consuming stream instead of a copy-stream hipMemcpyAsync + event + cross-stream wait (~0.14 ms of host time per
+// votes batch, PBFT_LAUNCH_TRACE=30)
+__global__ void import16_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[i];
+}
 
 // Pinned host staging (grow-only: hipHostMalloc costs milliseconds).  Never while a batch is in flight.
 // Every user of the staging calls this first: whatever pbft_verify_votes_stage handed out is void from here on
@@ -347,17 +355,25 @@ static inline size_t eidx_bytes(uint64_t N) {
 }
 // PBFT_LAUNCH_TRACE=1: every HIP call of a votes chunk launch that blocks the host for more than 0.3 ms is reported
 // on stderr (the replica's flush timeline showed 6-7 ms stalls inside pbft_verify_votes_submit_rows)
-static bool launch_trace() {
-  static const bool on = getenv("PBFT_LAUNCH_TRACE") != nullptr;
-  return on;
+// (PBFT_LAUNCH_TRACE=<n> with n > 1: report calls longer than n microseconds instead)
+static double launch_trace_ms() {
+  static const double ms = [] {
+    const char* e = getenv("PBFT_LAUNCH_TRACE");
+    if (!e) return -1.0;
+    const double v = strtod(e, nullptr);
+    return v > 1 ? v / 1000.0 : 0.3;
+  }();
+  return ms;
 }
+static bool launch_trace() { return launch_trace_ms() >= 0; }
 #define LT(name, ...)                                                                                              \
   do {                                                                                                             \
     const auto lt_t0 = std::chrono::steady_clock::now();                                                           \
     __VA_ARGS__;                                                                                                   \
     if (launch_trace()) {                                                                                          \
       const double lt_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - lt_t0).count(); \
-      if (lt_ms > 0.3) fprintf(stderr, "launch-stall %s chunk %u: %.3f ms\n", name, (unsigned)c->v_chunk, lt_ms);  \
+      if (lt_ms > launch_trace_ms())                                                                            \
+        fprintf(stderr, "launch-stall %s chunk %u: %.3f ms\n", name, (unsigned)c->v_chunk, lt_ms);             \
     }                                                                                                              \
   } while (0)
 
@@ -591,9 +607,8 @@ static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, h
 }
 
 // Votes form (include/pbft_verify.h pbft_verify_votes): R, S, key_idx and a 4-byte envelope index per
-// signature (70 B instead of 151 B over PCIe) + the batch's table of distinct 85-byte envelopes.
-// Device chunk layout: R | S (rs_stride 32), or the signatures as 64-byte R || S rows (rs_stride 64, the
-// staging of pbft_verify_votes_stage), then key_idx and env_idx.
+// signature (70 B instead of 151 B over PCIe; 72 B as staged rows) + the batch's table of distinct 85-byte
+// envelopes.
 // One chunk's device staging: R | S | key_idx | env_idx columns (caller columns), or the chunk's rows as staged
 // (PBFT_VOTES_ROW_BYTES each, one copy).
 struct votes_layout {
@@ -612,6 +627,13 @@ struct votes_layout {
 static const uint8_t* zc_dev(const pbft_ctx* c, const void* p, size_t bytes) {
   const uint8_t* q = (const uint8_t*)p;
   if (!c->zero_copy || !c->h_stage_dev || q < c->h_stage || q + bytes > c->h_stage + c->h_stage_cap) return nullptr;
+  return c->h_stage_dev + (q - c->h_stage);
+}
+
+// The kernels' address of [p, p + bytes) in the context's mapped staging, else null (whatever the zero-copy option).
+static const uint8_t* zc_map(const pbft_ctx* c, const void* p, size_t bytes) {
+  const uint8_t* q = (const uint8_t*)p;
+  if (!c->h_stage_dev || q < c->h_stage || q + bytes > c->h_stage + c->h_stage_cap) return nullptr;
   return c->h_stage_dev + (q - c->h_stage);
 }
 
@@ -644,17 +666,25 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
       c->ev_rows.push_back(e);
     }
   }
-  HIP_TRY(hipMemcpyAsync(c->d_stage, ENV, (size_t)PBFT_ENVELOPE_LEN * n_env, hipMemcpyHostToDevice, c->cstream));
-  // the envelopes' block-2 schedule on the context stream once the table has landed (ev_copied[0] is
-  // re-recorded by chunk 0)
-  HIP_TRY(hipEventRecord(c->ev_copied[0], c->cstream));
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[0], 0));
-  rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &c->v_wk);
-  if (rc) return rc;
-  if (two) {  // stream2's chunks read the envelope table and its schedule too
-    HIP_TRY(hipEventRecord(c->ev_env, c->stream));
-    HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_env, 0));
+  const size_t env_len = (size_t)PBFT_ENVELOPE_LEN * n_env;
+  const uint8_t* zenv = zc_map(c, ENV, env_len + 15);
+  if (zenv && ((uintptr_t)zenv & 15) == 0) {  // the table sits in the mapped staging: copied by a kernel
+    const uint64_t n16 = (env_len + 15) / 16;
+    hipLaunchKernelGGL(import16_kernel, dim3((unsigned)((n16 + 255) / 256)), dim3(256), 0, c->stream,
+                       (const uint4*)zenv, (uint4*)c->d_stage, n16);
+    LT("import_env", HIP_TRY(hipGetLastError()));
+  } else {
+    LT("h2d_env", HIP_TRY(hipMemcpyAsync(c->d_stage, ENV, env_len, hipMemcpyHostToDevice, c->cstream)));
+    // the envelopes' block-2 schedule on the context stream once the table has landed (ev_copied[0] is
+    // re-recorded by chunk 0)
+    LT("rec_env", HIP_TRY(hipEventRecord(c->ev_copied[0], c->cstream)));
+    LT("wait_env", HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_copied[0], 0)));
   }
+  LT("env_sched", rc = prepare_env_sched(c, c->d_stage, n_env, c->stream, &c->v_wk));
+  if (rc) return rc;
+  // stream2's chunks read the envelope table and its schedule too (it waits at its first chunk: votes_launch)
+  if (two) HIP_TRY(hipEventRecord(c->ev_env, c->stream));
+  c->v_s2_ready = false;
   c->v_two = two;
   c->v_n = N;
   c->v_next = 0;
@@ -678,6 +708,10 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
     const int b = (int)(c->v_chunk % VOTES_BUFS);
     const int slot = c->v_two ? (int)(c->v_chunk & 1) : 0;
     hipStream_t st = slot ? c->stream2 : c->stream;
+    if (slot && !c->v_s2_ready) {
+      LT("wait_env2", HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_env, 0)));
+      c->v_s2_ready = true;
+    }
     const bool rows_form = rs_stride == ROW;
     const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
     const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
