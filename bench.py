@@ -536,6 +536,65 @@ def config2_leg(v, torch, dev, stream, cpu: bool, iters: int = 200):
         c.close()
 
 
+L_ORDER = 2**252 + 27742317777372353535851937790883648493  # the group order L (RFC 8032)
+
+
+def adversarial_round(R, S, frac: float, seed: int):
+    """config #3's adversarial share: a seeded `frac` of the signatures made invalid in three ways, a third each --
+    one bit of s flipped, s replaced by s + L (non-canonical: verify_strict rejects s >= L), one bit of R flipped.
+    Returns the corrupted copies and the expected bits."""
+    rng = np.random.default_rng(seed)
+    idx = np.sort(rng.choice(len(S), size=max(3, int(len(S) * frac)), replace=False))
+    R, S = R.copy(), S.copy()
+    a, b, c = np.array_split(idx, 3)
+    S[a, rng.integers(0, 31, len(a))] ^= np.uint8(4)
+    for i in b:
+        S[i] = np.frombuffer((int.from_bytes(S[i].tobytes(), "little") + L_ORDER).to_bytes(32, "little"), np.uint8)
+    R[c, rng.integers(0, 31, len(c))] ^= np.uint8(2)
+    expect = np.ones(len(R), bool)
+    expect[idx] = False
+    return R, S, expect
+
+
+def config3_leg(v, torch, dev, stream, cpu: bool, iters: int = 100):
+    """BASELINE configs[2]: n = 64 replicas (f = 21), one 2^16-signature round batch (512 seqs x {Prepare, Commit} x
+    64) with 1 % adversarial signatures (flipped s, non-canonical s + L, flipped R), one GPU: device-resident p50 and
+    throughput, the bitmap checked, and the CPU baselines on the same batch."""
+    from pbft_amd import bitmap_to_bool
+    c = v.clone()
+    try:
+        seeds = key_seeds(64, 0x5EED0000 + 3)
+        msg, key_idx = envelopes(1, 512, 64)
+        R0, S0, pub = c.sign(seeds, key_idx, msg, ENVELOPE)
+        R, S, expect = adversarial_round(R0, S0, 0.01, 0x5EED0000 + 3)
+        assert c.set_keys(pub).all()
+        d = to_device(torch, dev, R, S, key_idx, msg)
+        lat = []
+        for it in range(iters + 5):
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            c.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                            ENVELOPE, len(R), d["B"].data_ptr(), stream.cuda_stream)
+            torch.cuda.synchronize()
+            if it >= 5:
+                lat.append((time.perf_counter() - t) * 1e3)
+        got = bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), len(R))
+        assert (got == expect).all(), "config #3 bitmap differs from the expected bits"
+        out = {"sigs": len(R), "replicas": 64, "adversarial": int((~expect).sum()),
+               "device_p50_ms": float(np.median(lat)), "device_verifies_per_s": len(R) / (np.median(lat) * 1e-3)}
+        if cpu:
+            cores = host_cores()
+            for name, lib, fn in (("cpu_port", "liboracle.so", "oracle_verify_batch"),
+                                  ("cpu_openssl", "libossl_baseline.so", "ossl_verify_batch")):
+                L = _cpu_lib(lib, fn)
+                if L is not None:
+                    rate, n, dt = cpu_rate(getattr(L, fn), pub, R, S, key_idx, msg, 2.0, cores, expect)
+                    out[name] = {"verifies_per_s": rate, "round_ms": len(R) / rate * 1e3, "cores": cores}
+        return out
+    finally:
+        c.close()
+
+
 def c_abi_multi_round(verifiers, R, S, key_idx, msg, expect, torch, steps: int, warmup: int = 2):
     """the round sharded over G GPUs of THIS process through the C ABI's single-process form
     (include/pbft_verify.h pbft_multi_create -> ncclCommInitAll over the contexts' devices;
@@ -854,6 +913,7 @@ def main():
         extras["e2e_votes_2^20"] = e2e_votes_round(v, R, S, key_idx, msg, expect, torch)
         extras["votes_device_2^20"] = votes_device_round(v, d, msg, expect, stream, torch, dev)
         extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
+        extras["config3"] = config3_leg(v, torch, dev, stream, cpu=not args.no_cpu)
         extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect)
         extras["shuffled_2^20"] = shuffled_leg(v, d, n, stream, torch, dev, expect)
         # the C ABI's single-process multi-GPU form on this process's one GPU (a 1-rank RCCL communicator): its
