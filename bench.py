@@ -409,7 +409,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             "push_many_ms": med["push_ms"], "flush_ms": med["flush_ms"],
             "flush_verifies_per_s": n / (med["flush_ms"] * 1e-3),
             "flush_submit_ms": med["submit_ms"], "apply_ms": med["apply_ms"],
-            "gpu_wait_ms": med["flush_ms"] - med["submit_ms"] - med["apply_ms"],
+            "gpu_wait_ms": max(0.0, med["flush_ms"] - med["submit_ms"] - med["apply_ms"]),  # (medians of separate series)
             "polls_while_running": int(med["polls"]), "sigs": n + n_seq, "rounds": rounds,
             "path": "one long-lived pbft_replica: push_many (2^20 votes; + 2048 PrePrepares via on_pre_prepare, "
                     "untimed) -> flush_submit (votes form filled into pinned staging by worker threads, each 2^18-row "

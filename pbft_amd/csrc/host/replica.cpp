@@ -230,6 +230,7 @@ class WorkerPool {
 // Flush timeline (PBFT_REPLICA_TRACE=1): host timestamps of the submit / fill / launch / land / apply steps of one
 // batch, printed to stderr when the batch completes (tools/replica_probe.py reads them).
 static const bool g_trace = getenv("PBFT_REPLICA_TRACE") != nullptr;
+static const bool g_push_trace = getenv("PBFT_PUSH_TRACE") != nullptr;
 struct TraceEv {
   const char* what;
   uint64_t ns, arg;
@@ -1020,6 +1021,12 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       q += c.queued;
     }
     RTRACE(r, "push_done", q);
+    if (g_push_trace && r->trace.size() >= 4) {  // PBFT_PUSH_TRACE (with PBFT_REPLICA_TRACE): pass times of this call
+      const size_t e = r->trace.size();
+      fprintf(stderr, "push-trace: checks %.3f windows %.3f rows %.3f ms\n", (r->trace[e - 3].ns - r->trace[e - 4].ns) / 1e6,
+              (r->trace[e - 2].ns - r->trace[e - 3].ns) / 1e6, (r->trace[e - 1].ns - r->trace[e - 2].ns) / 1e6);
+      r->trace.clear();
+    }
   }
   if (queued) *queued = q;
   return n_ok < N ? PBFT_EINVAL : PBFT_OK;
