@@ -32,6 +32,9 @@
 #include <mutex>
 #include <thread>
 #include <unistd.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -51,8 +54,66 @@ enum : uint8_t { V_PENDING = 0, V_IN_FLIGHT = 1 };
 // signatures are copied into the verifier's staging with one memcpy per phase.  Per signer: the candidate
 // count (flood bound) and the accepted digest (HashMap<PeerId, _>::insert, src/state.rs:49-67: the last
 // accepted vote of a signer wins).  Phase 0 of a window holds its PrePrepare candidates (signer = primary).
+// Growable byte buffer whose appends leave the new bytes uninitialised (std::vector would zero them first: a
+// second write of every signature byte before push_many's streaming stores).
+class ByteBuf {
+ public:
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  uint8_t* data() { return p_.get(); }
+  const uint8_t* data() const { return p_.get(); }
+  uint8_t& operator[](size_t i) { return p_[i]; }
+  const uint8_t& operator[](size_t i) const { return p_[i]; }
+  void reserve(size_t c) {
+    if (c > cap_) grow_to(c);
+  }
+  uint8_t* append(size_t k) {  // k more bytes at the end, uninitialised
+    if (n_ + k > cap_) grow_to(std::max(2 * cap_, n_ + k));
+    uint8_t* q = p_.get() + n_;
+    n_ += k;
+    return q;
+  }
+  void erase_front(size_t k) {
+    if (k >= n_) { n_ = 0; return; }
+    memmove(p_.get(), p_.get() + k, n_ - k);
+    n_ -= k;
+  }
+  void clear() { n_ = 0; }
+
+ private:
+  void grow_to(size_t c) {
+    std::unique_ptr<uint8_t[]> q(new uint8_t[c]);  // (default-initialised: no zeroing)
+    if (n_) memcpy(q.get(), p_.get(), n_);
+    p_ = std::move(q);
+    cap_ = c;
+  }
+  std::unique_ptr<uint8_t[]> p_;
+  size_t n_ = 0, cap_ = 0;
+};
+
+// PBFT_STREAM_STORES=0: plain stores for the candidates' signatures (push) and the staged rows (flush fill); by
+// default both are streaming (non-temporal) stores -- no read-for-ownership of lines that are only written here
+// and read much later (r04 A/B on MI355X boxes: the flush's fill 1.1 -> 0.6 ms less of the calling thread's time).
+static const bool g_stream_stores = !(getenv("PBFT_STREAM_STORES") && atoi(getenv("PBFT_STREAM_STORES")) == 0);
+
+// 64 bytes from src to dst (8-byte aligned) with streaming stores where available
+static inline void copy64_nt(uint8_t* dst, const uint8_t* src) {
+#if defined(__x86_64__)
+  long long v[8];
+  memcpy(v, src, 64);  // (src may be unaligned: a caller's row)
+  for (int q = 0; q < 8; ++q) _mm_stream_si64((long long*)dst + q, v[q]);
+#else
+  memcpy(dst, src, 64);
+#endif
+}
+static inline void stream_fence() {
+#if defined(__x86_64__)
+  _mm_sfence();
+#endif
+}
+
 struct Phase {
-  std::vector<uint8_t> sig;   // [k][64] R || S
+  ByteBuf sig;                // [k][64] R || S
   std::vector<uint16_t> who;  // signer
   std::vector<uint32_t> dix;  // index into digs
   std::vector<uint8_t> st;    // V_PENDING / V_IN_FLIGHT
@@ -76,13 +137,14 @@ struct Phase {
       if (memcmp(digs[j].data(), d, 64) == 0) return (int64_t)j;
     return -1;
   }
-  void append(const uint8_t* d, int64_t j, uint32_t signer, const uint8_t* sg) {
+  void append(const uint8_t* d, int64_t j, uint32_t signer, const uint8_t* sg, bool nt = false) {
     if (j < 0) {
       digs.emplace_back();
       memcpy(digs.back().data(), d, 64);
       j = (int64_t)digs.size() - 1;
     }
-    sig.insert(sig.end(), sg, sg + 64);
+    if (nt) copy64_nt(sig.append(64), sg);
+    else memcpy(sig.append(64), sg, 64);
     who.push_back((uint16_t)signer);
     dix.push_back((uint32_t)j);
     st.push_back(V_PENDING);
@@ -94,7 +156,7 @@ struct Phase {
       sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
       return;
     }
-    sig.erase(sig.begin(), sig.begin() + 64 * k);
+    sig.erase_front(64 * k);
     who.erase(who.begin(), who.begin() + k);
     dix.erase(dix.begin(), dix.begin() + k);
     st.erase(st.begin(), st.begin() + k);
@@ -231,6 +293,7 @@ class WorkerPool {
 // batch, printed to stderr when the batch completes (tools/replica_probe.py reads them).
 static const bool g_trace = getenv("PBFT_REPLICA_TRACE") != nullptr;
 static const bool g_push_trace = getenv("PBFT_PUSH_TRACE") != nullptr;
+
 struct TraceEv {
   const char* what;
   uint64_t ns, arg;
@@ -663,6 +726,19 @@ static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
     const bool one = p.digs.size() == 1;
     if (rs) {
       uint8_t* row = SIG + rs * g.row0;
+#if defined(__x86_64__)
+      if (g_stream_stores) {  // streaming stores: no read-for-ownership of the staging lines (the DMA reads them next)
+        for (uint32_t i = 0; i < g.count; ++i, row += rs) {
+          const long long* src = (const long long*)&p.sig[64 * (size_t)i];
+          long long* dst = (long long*)row;
+          for (int q = 0; q < 8; ++q) _mm_stream_si64(dst + q, src[q]);
+          _mm_stream_si64(dst + 8, (long long)((uint64_t)p.who[i] | (uint64_t)(g.env0 + (one ? 0 : p.dix[i])) << 32));
+        }
+        memset(p.st.data(), V_IN_FLIGHT, g.count);
+        p.n_pending = 0;
+        continue;
+      }
+#endif
       for (uint32_t i = 0; i < g.count; ++i, row += rs) {
         memcpy(row, &p.sig[64 * (size_t)i], 64);
         const uint64_t meta = (uint64_t)p.who[i] | (uint64_t)(g.env0 + (one ? 0 : p.dix[i])) << 32;
@@ -683,6 +759,11 @@ static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
 }
 static_assert(PBFT_VOTES_ROW_ENV == PBFT_VOTES_ROW_KEY + 4 && PBFT_VOTES_ROW_BYTES == PBFT_VOTES_ROW_KEY + 8,
               "fill_rows writes key_idx, pad and env_idx as one 8-byte word");
+static void fill_fence() {
+#if defined(__x86_64__)
+  if (g_stream_stores) _mm_sfence();
+#endif
+}
 static void fill_envs(pbft_replica* r, size_t s0, size_t s1, uint8_t* ENV) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
@@ -696,6 +777,7 @@ static void fill_segs(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
                       size_t rs) {
   fill_envs(r, s0, s1, ENV);
   fill_rows(r, s0, s1, SIG, K, IDX, rs);
+  fill_fence();
 }
 
 
@@ -732,6 +814,7 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
           const size_t y = t + 1 == T ? b : std::min(b, first_at(lo + (hi - lo) * (t + 1) / T));
           if (y > x) fill_rows(r, x, y, SIG, K, IDX, rs);
         }
+        fill_fence();  // (streaming stores are weakly ordered: visible before the chunk is launched)
         done[k].fetch_add(1, std::memory_order_release);
       }
   });
@@ -890,7 +973,7 @@ struct PushCounts {
 
 // The part of a push that touches one window (State::insert_* candidates, src/state.rs:49-67): 1 queued, 0 dropped.
 static int push_into(const pbft_replica* r, Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer,
-                     const uint8_t* sig, PushCounts& st) {
+                     const uint8_t* sig, PushCounts& st, bool nt = false) {
   if (w.committed_reported) { ++st.duplicates; return 0; }  // late vote for a decided round
   Phase& p = w.ph[kind];
   p.init(r->n);
@@ -914,7 +997,7 @@ static int push_into(const pbft_replica* r, Window& w, uint8_t kind, const uint8
     const size_t c = r->n < 1024 ? r->n : 1024;
     p.sig.reserve(64 * c); p.who.reserve(c); p.dix.reserve(c); p.st.reserve(c);
   }
-  p.append(digest, j, signer, sig);
+  p.append(digest, j, signer, sig, nt);
   ++p.cnt[signer];
   ++st.queued;
   return 1;
@@ -1013,8 +1096,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       for (const Run& u : runs) {
         if (u.owner != t) continue;
         for (uint64_t i = u.lo; i < u.hi; ++i)
-          if (!bad[i]) push_into(r, *u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c);
+          if (!bad[i]) push_into(r, *u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, g_stream_stores);
       }
+      if (g_stream_stores) stream_fence();  // (streaming stores are weakly ordered: drained before the join)
     });
     for (const PushCounts& c : cnt) {
       add_counts(r, c);
