@@ -285,7 +285,12 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *   PBFT_OPT_VOTES_ZERO_COPY      1: votes rows that sit in the context's pinned staging (pbft_verify_votes_stage
  *                                 / _submit_begin, the replica's flush, pageable inputs copied there) are read by
  *                                 the kernels in place over PCIe; 0 (default; env PBFT_VOTES_ZERO_COPY): copied
- *                                 to HBM chunk by chunk first (faster on MI355X: DESIGN.md section 5) */
+ *                                 to HBM chunk by chunk first (faster on MI355X: DESIGN.md section 5)
+ *   PBFT_OPT_COMB_PAIR            1: one-lane batches run the comb with two waves per 64 signatures (a hashing
+ *                                 wave and a base-point wave, joined by one extended addition); 0: one wave per
+ *                                 64 signatures; any other value = by batch size (pairs up to 98,304 signatures,
+ *                                 where one wave per 64 signatures leaves SIMDs short of waves; env
+ *                                 PBFT_COMB_PAIR) */
 #define PBFT_OPT_SPLIT_BELOW 1
 #define PBFT_OPT_FINISH_WIDTH 2
 #define PBFT_OPT_KEY_TABLE_BUDGET_MB 3
@@ -294,6 +299,7 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 #define PBFT_OPT_KERNEL_TIMING 7
 #define PBFT_OPT_FINISH_WAVES 8
 #define PBFT_OPT_VOTES_ZERO_COPY 9
+#define PBFT_OPT_COMB_PAIR 10
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

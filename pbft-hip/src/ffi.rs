@@ -52,6 +52,7 @@ pub const PBFT_OPT_LAT_SPLIT: c_int = 5;
 pub const PBFT_OPT_KERNEL_TIMING: c_int = 7;
 pub const PBFT_OPT_FINISH_WAVES: c_int = 8;
 pub const PBFT_OPT_VOTES_ZERO_COPY: c_int = 9;
+pub const PBFT_OPT_COMB_PAIR: c_int = 10;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
 pub const PBFT_KIND_PREPARE: u8 = 1;

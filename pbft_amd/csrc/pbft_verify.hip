@@ -155,6 +155,7 @@ struct pbft_ctx {
   int fin_tree = -1;                   // finish cross-lane tree (0: none; 4 / 6: the compiled tree; -1 = by batch size)
   int fin_waves = 0;                   // product-tree finish compiled for 1 or 2 waves per SIMD (0 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
+  int comb_pair = -1;                  // comb_pair_kernel: 1 on, 0 off, -1 by batch size (PBFT_OPT_COMB_PAIR)
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   pbft_key_stats kstats{};             // the last pbft_verify_set_keys / _update_keys (pbft_verify_key_stats)
@@ -459,6 +460,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.flags = hw + 120 * N;  // within the half's 121 W bytes
   a.eidx = (uint32_t*)(wbase + eidx_offset(W));
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.mi_stride = mi_stride; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
+  a.pair = c->comb_pair;
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
   if (r_host && !latency_mode) a.r_copy = (uint32_t*)(wbase + rcopy_offset(W, wtwo));
@@ -854,6 +856,10 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
   if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
   if (const char* e = getenv("PBFT_VOTES_TWO_STREAMS")) c->two_streams = strtol(e, nullptr, 10) != 0;
+  if (const char* e = getenv("PBFT_COMB_PAIR")) {
+    const long v = strtol(e, nullptr, 10);
+    c->comb_pair = (v == 0 || v == 1) ? (int)v : -1;
+  }
   HIP_TRY(hipEventCreate(&c->ev0));
   HIP_TRY(hipEventCreate(&c->ev1));
   HIP_TRY(hipEventCreateWithFlags(&c->ev_done, hipEventDisableTiming));
@@ -1677,6 +1683,7 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
     case PBFT_OPT_VOTES_ZERO_COPY: c->zero_copy = value != 0; return PBFT_OK;
+    case PBFT_OPT_COMB_PAIR: c->comb_pair = value <= 1 ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");

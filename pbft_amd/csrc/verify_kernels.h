@@ -357,6 +357,255 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   }
 }
 
+// ---- pair mode: two waves per 64 signatures (mid-size batches) -----------------
+// Below ~2^18 signatures comb_kernel has fewer than 4 waves per SIMD in one generation (2^17: 2,048 waves, 2 per
+// SIMD; 2^16: 1 per SIMD), so the VALU idles in every stall another wave would fill (VALUBusy 72.7 % at 2^17
+// against 92 % at 2^20).  comb_pair_kernel splits each signature's sum over two waves of one block:
+//  * role 0 (the hashing wave): R, A, M -> k = SHA-512(R || A || M) mod L, the entry indices of all PA key-table
+//    positions (eidx rows PB..PB+PA-1) and their signs (LDS), then the sum of key positions 0..A0-1;
+//  * role 1: s -> the PB base-point positions, then key positions A0..PA-1 once role 0 has published them
+//    (one block barrier, placed so that it precedes the first read of a key-position index);
+//  * role 1 leaves its extended point in LDS (its own entry buffer + the pair's 2 KB), a second barrier, and
+//    role 0 adds it (one 8-multiplication extended addition, complete) and writes X, Y, Z for finish_kernel.
+// A0 balances the two waves' VALU (SHA-512 + reduction ~ 6 mixed additions).  Twice the waves for the same work
+// plus one addition per signature; the same R' = [s]B - [k]A, so the finish and the bitmap are unchanged.
+// Measured (profiles/r04/pair/): 2^15 signatures -29 %, 2^16 -8 %, 2^17 even (VALUBusy 72.7 -> 76 %: the waves
+// of one generation start and stall together, and the combining addition adds ~4 % VALU), 2^18 +2 %; so by batch
+// size up to PBFT_PAIR_MAX_N.  Both roles run one copy of the step loop: with a loop per role the instruction
+// footprint of SHA-512 + two loops made the kernel 5 % slower at 2^17.
+#ifndef PBFT_PAIR_MIN_N
+#define PBFT_PAIR_MIN_N 0u  // (below the latency kernel's threshold no batch reaches the one-lane kernels)
+#endif
+#ifndef PBFT_PAIR_MAX_N
+#define PBFT_PAIR_MAX_N (3u << 15)  // by batch size: faster up to 2^16 (-29 % at 2^15, -8 % at 2^16), even at 2^17
+                                    // (profiles/r04/pair/)
+#endif
+static constexpr uint32_t PAIR_SIGS = BLOCK / 2;     // signatures per block
+static constexpr uint32_t PAIR_XLDS = 8 * 64 * 4;     // per pair: limbs 32..39 of the exchanged point / sign words
+static constexpr size_t PAIR_LDS = (BLOCK / 64) * COMB_LDS_PER_WAVE + (BLOCK / 128) * PAIR_XLDS;
+#ifndef PBFT_PAIR_A0_ADJ
+#define PBFT_PAIR_A0_ADJ 0  // key positions of role 0: (PB + PA - 6) / 2 + this
+#endif
+#ifndef PBFT_PAIR_BAR
+#define PBFT_PAIR_BAR 0  // role 1's step at which it waits for role 0's indices (0: PB - 2, the latest possible)
+#endif
+#ifndef PBFT_PAIR_FLIP
+#define PBFT_PAIR_FLIP 0  // 1: the wave -> role map flips with the parity of blockIdx (roles mixed over SIMDs)
+#endif
+template <class PLA>
+struct pair_split {
+  static constexpr int PB = PLB::P, PA = PLA::P;
+  static constexpr int A0r = (PB + PA - 6) / 2 + PBFT_PAIR_A0_ADJ;
+  static constexpr int BAR = PBFT_PAIR_BAR ? PBFT_PAIR_BAR : PB - 2;
+  static constexpr int A0 = A0r < 1 ? 1 : A0r > PA - 1 ? PA - 1 : A0r;  // key positions of role 0
+  static constexpr int N1 = PB + PA - A0;                                  // steps of role 1
+  static_assert(BAR >= 1 && BAR <= PB - 2 && N1 <= 32, "role 1 waits before its first key-position index read; "
+                "its sign mask is 32 bits");
+};
+__device__ __forceinline__ void lds_write32(uint32_t addr, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *(__attribute__((address_space(3))) uint32_t*)(uintptr_t)addr = v;
+#else
+  (void)addr; (void)v;
+#endif
+}
+__device__ __forceinline__ uint32_t lds_read32(uint32_t addr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return *(__attribute__((address_space(3))) const uint32_t*)(uintptr_t)addr;
+#else
+  (void)addr;
+  return 0;
+#endif
+}
+
+template <int LEN, class PLA>
+__global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_pair_kernel(
+    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
+    uint32_t rs_stride, uint32_t k_stride,
+    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
+    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
+    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
+    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
+    const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy) {
+  using SP = pair_split<PLA>;
+  constexpr int PB = SP::PB, PA = SP::PA, A0 = SP::A0, N1 = SP::N1;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t flip = PBFT_PAIR_FLIP ? (uint32_t)__builtin_popcount(blockIdx.x) & 1u : 0u;
+  const uint32_t pair = wave >> 1, role = (wave & 1) ^ flip;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+  const uint32_t ebuf = lds0 + wave * COMB_LDS_PER_WAVE;
+  const uint32_t pbuf = lds0 + (2 * pair + (1 ^ flip)) * COMB_LDS_PER_WAVE;        // role 1's point, limbs 0..31
+  const uint32_t xbuf = lds0 + (BLOCK / 64) * COMB_LDS_PER_WAVE + pair * PAIR_XLDS;  // limbs 32..39; sign words
+  const uint64_t i = (uint64_t)blockIdx.x * PAIR_SIGS + pair * 64 + lane;  // < Npad
+  const bool live = i < N;
+  const uint64_t ii = live ? i : 0;
+  const uint8_t* tB = (const uint8_t*)tabB;
+  const uint8_t* tA = (const uint8_t*)tabA;
+  const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);
+  uint32_t* const erow = eidx + i;  // step row r at erow[r * Npad]
+  ge P;
+  uint32_t sgn = 0;  // bit t: digit of this role's step t is negative
+  bool s_ok = false;  // role 1
+  if (role == 0) {
+    bool kok;
+    {
+      uint32_t r[8], a[8];
+      load32(r, R + (size_t)rs_stride * ii);
+      if (r_copy && live) {
+        uint4* rc = (uint4*)(r_copy + 8 * i);
+        rc[0] = uint4{r[0], r[1], r[2], r[3]};
+        rc[1] = uint4{r[4], r[5], r[6], r[7]};
+      }
+      uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
+      kok = ki < n_keys;
+      if (!kok) ki = 0;
+      kok = kok && key_ok[ki];
+      {
+        const uint4* kp = (const uint4*)(keys + 8 * ki);
+        const uint4 k0 = kp[0], k1 = kp[1];
+        a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
+      }
+      uint64_t mrow = ii;
+      if (msg_idx) {
+        mrow = msg_idx[(size_t)mi_stride * ii];
+        kok = kok && mrow < n_msg;
+        if (mrow >= n_msg) mrow = 0;
+      }
+      uint32_t h[16], k[8];
+      sha512_k<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len, wk, mrow);
+      sc_reduce512(k, h);
+      const uint32_t keybase = ki * PLA::ENTRIES;
+      digits dk;
+      dk.init(k);
+      static_for<PA>([&](auto pc) {
+        constexpr int pos = decltype(pc)::value;
+        const int d = dk.template take_pos<PLA, pos>();
+        sgn |= (d < 0 ? 1u : 0u) << pos;
+        erow[(size_t)(PB + pos) * Npad] = keybase + PLA::offset(pos) + (uint32_t)(d < 0 ? -d : d);
+      });
+    }
+    // key positions A0.. and the key's usability for role 1
+    lds_write32(xbuf + 4u * lane, (sgn >> A0) | (kok ? 0x80000000u : 0u));
+    __syncthreads();  // (1) role 1 may read key-position indices from here on
+  } else {
+    uint32_t s[8];
+    load32(s, S + (size_t)rs_stride * ii);
+    s_ok = sc_lt_L(s);
+    sc_clamp_rejected(s, s_ok);
+    digits ds;
+    ds.init(s);
+    static_for<PB>([&](auto pc) {
+      constexpr int pos = decltype(pc)::value;
+      const int d = ds.template take_pos<PLB, pos>();
+      sgn |= (d < 0 ? 1u : 0u) << pos;
+      erow[(size_t)pos * Npad] = PLB::offset(pos) + (uint32_t)(d < 0 ? -d : d);
+    });
+  }
+  // Both roles run the SAME step loop (one copy of its ~9 KB of code in the instruction cache while the other
+  // role hashes).  Step t of a role: table tB for t < nb, else tA; eidx row t + (t < nb ? 0 : roff).
+  //   role 0: nb = 0,  roff = PB       (key positions 0 .. A0-1), NS = A0
+  //   role 1: nb = PB, roff = A0       (base-point positions, then key positions A0 .. PA-1), NS = N1
+  // role 1 meets barrier (1) at step bar, before its first read of a key-position index.
+  const int nb = role ? PB : 0, roff = role ? A0 : PB, NS = role ? N1 : A0, bar = role ? SP::BAR : -1;
+  auto tab = [&](int t) { return t < nb ? tB : tA; };
+  auto row = [&](int t) { return (size_t)(t < nb ? t : t + roff) * Npad; };
+  dma_entry_lines(tab(0), erow[row(0)], lane, ebuf);
+  uint32_t nidx = NS > 1 ? erow[row(1)] : 0u;
+  {
+    fe qa, qb, k;
+    const bool neg = sgn & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (NS > 1) dma_entry_lines(tab(1), nidx, lane, ebuf);
+    if (NS > 2) nidx = erow[row(2)];
+    ge_from_ab(P, qa, qb, k, neg);
+  }
+  for (int t = 1; t < NS; ++t) {
+    if (t == bar) {
+      __syncthreads();  // (1): the key positions' indices and signs are published
+      const uint32_t w = lds_read32(xbuf + 4u * lane);
+      sgn |= (w & 0x7fffffffu) << PB;
+      if (live) flags[i] = (s_ok && (w >> 31)) ? 1 : 0;
+    }
+    fe qa, qb, k;
+    const bool neg = (sgn >> t) & 1u;
+    lds_entry_signed(rd0, neg, qa, qb, k);
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    if (t + 1 < NS) dma_entry_lines(tab(t + 1), nidx, lane, ebuf);
+    if (t + 2 < NS) nidx = erow[row(t + 2)];
+    ge_madd_ab<true, true>(P, P, qa, qb, k, neg);
+#pragma unroll
+    for (int q = 0; q < 10; ++q) asm("" : "+v"(P.X.v[q]), "+v"(P.Y.v[q]), "+v"(P.Z.v[q]), "+v"(P.T.v[q]));
+  }
+  if (role) {
+    // the point to role 0: limb-major (conflict-free), X Y Z T[0..1] in this wave's entry buffer (its last entry
+    // has been read: LDS operations of one wave complete in order), T[2..9] in the pair's area (its sign words
+    // were read at barrier 1)
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const uint32_t o = 4u * (64u * q + lane);
+      lds_write32(pbuf + o, P.X.v[q]);
+      lds_write32(pbuf + 64u * 4u * 10u + o, P.Y.v[q]);
+      lds_write32(pbuf + 64u * 4u * 20u + o, P.Z.v[q]);
+      if (q < 2) lds_write32(pbuf + 64u * 4u * 30u + o, P.T.v[q]);
+      else lds_write32(xbuf + 4u * (64u * (q - 2) + lane), P.T.v[q]);
+    }
+    __syncthreads();  // (2)
+    return;
+  }
+  __syncthreads();  // (2) role 1's point is in LDS
+  // R' = P + Q (ge_add's arithmetic without T3; Q's coordinates read from LDS as they are needed)
+  auto lds_fe = [&](fe& f, int c) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      const int l = 10 * c + q;
+      f.v[q] = l < 32 ? lds_read32(pbuf + 4u * (64u * l + lane)) : lds_read32(xbuf + 4u * (64u * (l - 32) + lane));
+    }
+  };
+  auto mul1 = [](fe& h, const fe& f, const fe& g) {
+    fe* const ho[1] = {&h};
+    const fe* const fo[1] = {&f};
+    const fe* const go[1] = {&g};
+    fe_mul_chain<1>(ho, fo, go);
+  };
+  fe a, b, c, t, u, w;
+  lds_fe(u, 1);
+  lds_fe(w, 0);
+  fe_sub(t, P.Y, P.X); fe_carry(t);
+  fe_sub(a, u, w); fe_carry(a);
+  mul1(a, t, a);                        // A = (Y1 - X1)(Y2 - X2)
+  fe_add(t, P.Y, P.X);
+  fe_add(b, u, w);
+  mul1(b, t, b);                        // B = (Y1 + X1)(Y2 + X2)
+  lds_fe(u, 3);
+  mul1(c, P.T, u);
+  fe_const_2d(w);
+  mul1(c, c, w);                        // C = 2d T1 T2
+  lds_fe(u, 2);
+  mul1(t, P.Z, u);
+  fe_add(t, t, t);                      // D = 2 Z1 Z2
+  fe e, f, g, h;
+  fe_sub(e, b, a); fe_sub(f, t, c); fe_add(g, t, c); fe_add(h, b, a);
+  fe_carry(e); fe_carry(f); fe_carry(g); fe_carry(h);
+  fe X3, Y3, Z3;
+  {
+    fe* const ho[3] = {&X3, &Y3, &Z3};
+    const fe* const fo[3] = {&e, &g, &f};
+    const fe* const go[3] = {&f, &h, &g};
+    fe_mul_chain<3>(ho, fo, go);
+  }
+  if (live) {
+#pragma unroll
+    for (int q = 0; q < 10; ++q) {
+      xyz[(size_t)q * N + i] = X3.v[q];
+      xyz[(size_t)(10 + q) * N + i] = Y3.v[q];
+      xyz[(size_t)(20 + q) * N + i] = Z3.v[q];
+    }
+  }
+}
+
 // ---- latency mode: small batches --------------------------------------------
 // For small batches (BASELINE config #5: 4096-signature rounds) one lane per
 // signature leaves most SIMDs idle, and the round's latency is one lane's
@@ -690,6 +939,7 @@ struct comb_launch_args {
   uint32_t* r_copy = nullptr;  // one-lane mode: [N][8] copy of R for the finish (R read from host memory)
   bool latency_mode;
   int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
+  int pair = -1;           // one-lane mode: comb_pair_kernel 1 / comb_kernel 0 / by batch size -1
   hipStream_t st;
 };
 
@@ -718,7 +968,17 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
   } else {
     const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
     const size_t lds = (BLOCK / 64) * COMB_LDS_PER_WAVE;
-    if (a.msg_len == PBFT_ENVELOPE_LEN && N >= PBFT_CHAIN_MIN_N)
+    const bool pair = a.pair >= 0 ? a.pair > 0 : (N >= PBFT_PAIR_MIN_N && N <= PBFT_PAIR_MAX_N);
+    if (pair) {
+      const uint64_t pblocks = (N + PAIR_SIGS - 1) / PAIR_SIGS;
+#define PBFT_LAUNCH_PAIR(LEN_)                                                                                     \
+  hipLaunchKernelGGL((comb_pair_kernel<LEN_, PLA>), dim3((unsigned)pblocks), dim3(BLOCK), PAIR_LDS, a.st, a.R, a.S, \
+                     a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,    \
+                     a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy)
+      if (a.msg_len == PBFT_ENVELOPE_LEN) PBFT_LAUNCH_PAIR(PBFT_ENVELOPE_LEN);
+      else PBFT_LAUNCH_PAIR(-1);
+#undef PBFT_LAUNCH_PAIR
+    } else if (a.msg_len == PBFT_ENVELOPE_LEN && N >= PBFT_CHAIN_MIN_N)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st,
                          a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,
                          a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy);

@@ -293,6 +293,7 @@ class GpuBatchVerifier:
     OPT_KERNEL_TIMING = 7
     OPT_FINISH_WAVES = 8
     OPT_VOTES_ZERO_COPY = 9
+    OPT_COMB_PAIR = 10
 
     def set_option(self, option: int, value: int) -> None:
         """pbft_verify_set_option: latency-mode threshold, finish width, key-table budget (include/pbft_verify.h)."""

@@ -174,6 +174,40 @@ def test_config3_round_with_adversarial(gv, coracle):
     assert not got[idx].any() and got.sum() == len(R) - len(idx)
 
 
+def test_comb_pair_matches_oracle(gv, coracle):
+    """PBFT_OPT_COMB_PAIR (r04): the comb with two waves per 64 signatures (a hashing wave and a base-point wave
+    joined by one extended addition) gives the oracle's bits, forced on and off and by batch size, above its
+    automatic range (140,800 and the 131k shard), inside it with ragged tails, and for a non-envelope message
+    length."""
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 1100, tag=5)        # 140,800 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(5)
+    R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
+    assert not exp[idx].any()
+    try:
+        for n in (len(R2), 131072, 65536 + 63, 20000 + 1):
+            for mode in (1, 0, 2):
+                gv.set_option(gv.OPT_COMB_PAIR, mode)
+                got, bm = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
+                assert (got == exp[:n]).all(), (n, mode, np.nonzero(got != exp[:n])[0][:10])
+                if n % 64:
+                    assert int(bm[-1]) >> (n % 64) == 0
+        # a message length other than the 85-byte envelope (the generic SHA-512 path of the hashing wave)
+        n, ml = 40000, 111
+        m = rng.integers(0, 256, size=(n, ml), dtype=np.uint8)
+        ki = rng.integers(0, 64, size=n).astype(np.uint16)
+        Rm, Sm, _ = gv.sign(seeds, ki, m, ml)
+        Sm[::501, 5] ^= 4
+        e2 = oracle_bits(coracle, pub, Rm, Sm, ki, m, ml)
+        for mode in (1, 0):
+            gv.set_option(gv.OPT_COMB_PAIR, mode)
+            got, _ = verify(gv, Rm, Sm, ki, m, ml)
+            assert (got == e2).all() and not got[::501].any(), mode
+    finally:
+        gv.set_option(gv.OPT_COMB_PAIR, 2)
+
+
 def test_config4_full_size_properties(gv, coracle):
     """2^20 signatures (BASELINE configs[3] round): size-independent properties + oracle checksum."""
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 256, 2048, tag=4)
