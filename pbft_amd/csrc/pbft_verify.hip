@@ -39,6 +39,9 @@ using namespace pbft;
 #ifndef PBFT_FIN_FM_SMALL
 #define PBFT_FIN_FM_SMALL 2  // finish signatures per lane for N <= PBFT_FIN_SMALL_UPTO
 #endif
+#ifndef PBFT_FIN_TINY_UPTO
+#define PBFT_FIN_TINY_UPTO (1u << 16)  // one signature per finish lane up to here (r04: 2^16 0.1097 -> 0.1064 ms,
+#endif                                 // 2^17 +3 %: profiles/r04/ab_fin_shard.txt)
 #ifndef PBFT_FIN_FM_MID
 #define PBFT_FIN_FM_MID 4  // ... for PBFT_FIN_SMALL_UPTO < N < 2^19
 #endif
@@ -480,7 +483,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
     // signatures per finish lane, product tree and waves per SIMD by batch size (PBFT_FIN_* above)
     const bool big = N >= ((uint64_t)1 << 19);
-    int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID : PBFT_FIN_FM_SMALL;
+    int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID
+                                   : N > PBFT_FIN_TINY_UPTO  ? PBFT_FIN_FM_SMALL : 1;
     // cross-lane product tree (one variable-time inversion per 16-lane row since r04, per wave before) where few
     // signatures share a lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
     // (profiles/r02_ab_log.md); lv is a flag here, finish.hip compiles the tree depth (PBFT_FIN_LV)
