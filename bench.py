@@ -569,19 +569,33 @@ def config3_leg(v, torch, dev, stream, cpu: bool, iters: int = 100):
         R, S, expect = adversarial_round(R0, S0, 0.01, 0x5EED0000 + 3)
         assert c.set_keys(pub).all()
         d = to_device(torch, dev, R, S, key_idx, msg)
-        lat = []
-        for it in range(iters + 5):
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            c.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
-                            ENVELOPE, len(R), d["B"].data_ptr(), stream.cuda_stream)
-            torch.cuda.synchronize()
-            if it >= 5:
-                lat.append((time.perf_counter() - t) * 1e3)
-        got = bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), len(R))
-        assert (got == expect).all(), "config #3 bitmap differs from the expected bits"
+
+        def p50():
+            lat = []
+            d["B"].zero_()
+            for it in range(iters + 5):
+                torch.cuda.synchronize()
+                t = time.perf_counter()
+                c.verify_device(d["R"].data_ptr(), d["S"].data_ptr(), d["K"].data_ptr(), d["M"].data_ptr(), ENVELOPE,
+                                ENVELOPE, len(R), d["B"].data_ptr(), stream.cuda_stream)
+                torch.cuda.synchronize()
+                if it >= 5:
+                    lat.append((time.perf_counter() - t) * 1e3)
+            got = bitmap_to_bool(d["B"].cpu().numpy().view(np.uint64), len(R))
+            assert (got == expect).all(), "config #3 bitmap differs from the expected bits"
+            return float(np.median(lat))
+        m = p50()
         out = {"sigs": len(R), "replicas": 64, "adversarial": int((~expect).sum()),
-               "device_p50_ms": float(np.median(lat)), "device_verifies_per_s": len(R) / (np.median(lat) * 1e-3)}
+               "device_p50_ms": m, "device_verifies_per_s": len(R) / (m * 1e-3),
+               "comb": "comb_pair_kernel (two waves per 64 signatures, by batch size)"}
+        # the single-wave comb on the same batch (PBFT_OPT_COMB_PAIR = 0), for the pair comb's gain (bitmap checked)
+        try:
+            c.set_option(c.OPT_COMB_PAIR, 0)
+            out["device_p50_ms_single_wave_comb"] = p50()
+        except Exception as e:  # a diagnostic beside the measured line; its failure is reported, not fatal
+            out["single_wave_comb_error"] = repr(e)
+        finally:
+            c.set_option(c.OPT_COMB_PAIR, 2)
         if cpu:
             cores = host_cores()
             for name, lib, fn in (("cpu_port", "liboracle.so", "oracle_verify_batch"),
