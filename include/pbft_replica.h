@@ -144,7 +144,10 @@ int pbft_replica_create(pbft_ctx *ctx, uint32_t n, uint32_t self_id, const uint8
  * src/behavior.rs:45-61, fed by mDNS discovery src/network_behaviour_composer.rs:24-33): its PeerId now maps to
  * replica idx[i] (pbft_replica_peer_index) and, with a GPU context, only its comb tables are rebuilt
  * (pbft_verify_update_keys; key_ok as there).  Votes already accepted under the old key stay; candidates still
- * pending are verified under the new key.  PBFT_EBUSY while a batch is in flight. */
+ * pending are verified under the new key.  PBFT_EBUSY while a batch is in flight.  PBFT_EINVAL if two new keys
+ * are equal or a new key is held by a slot that is not being replaced (one of the two would be unreachable by
+ * PeerId).  The GPU key set belongs to the context (and its clones): a context serves ONE replica -- another
+ * replica on it would verify against the new key while its PeerId map keeps the old one. */
 int pbft_replica_update_keys(pbft_replica *r, const uint32_t *idx, const uint8_t *A, uint32_t m, uint8_t *key_ok);
 int pbft_replica_destroy(pbft_replica *r);
 int pbft_replica_set_verifier(pbft_replica *r, pbft_batch_verify_fn fn, void *user);

@@ -74,7 +74,10 @@ int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *k
  * with a placeholder key, key_ok 0, and filled here when its peer appears).
  * key_ok (optional, m bytes) as for set_keys.  The set is updated in place for
  * every context sharing it (pbft_verify_ctx_clone): no batch may be in flight
- * on any of them (the call synchronises the device first). */
+ * on any of them (the call synchronises the device first).  On failure: if
+ * nothing was written yet (scratch allocation, key upload) the set is
+ * unchanged; otherwise the m slots' key_ok is cleared in the shared set (every
+ * context holding it rejects signatures under them; the other keys work). */
 int pbft_verify_update_keys(pbft_ctx *ctx, const uint32_t *idx, const uint8_t *A, uint32_t m, uint8_t *key_ok);
 
 /* Phases of the last pbft_verify_set_keys / pbft_verify_update_keys on this
@@ -274,7 +277,8 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *                                 (0 = env PBFT_KEY_TABLE_BUDGET_MB or 70 % of the free HBM); selects the key
  *                                 comb plan
  *   PBFT_OPT_FINISH_TREE          cross-lane levels of the finish's batch inversion: 0 (one inversion per lane)
- *                                 or 4 / 6 (the compiled product tree: one inversion per 16-lane row); any
+ *                                 or 4 (the compiled product tree: one inversion per 16-lane row; 6, the per-wave
+ *                                 tree, is a build-time A/B and returns PBFT_EINVAL); any
  *                                 other value = by batch size
  *   PBFT_OPT_LAT_SPLIT            lanes per signature of the latency-mode kernel: 4 or 8; any other value = by
  *                                 batch size (8 up to 8,192 signatures, else 4)
@@ -300,6 +304,14 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 #define PBFT_OPT_FINISH_WAVES 8
 #define PBFT_OPT_VOTES_ZERO_COPY 9
 #define PBFT_OPT_COMB_PAIR 10
+/* Testing: the next pbft_verify_update_keys on this context fails at a chosen point -- 1: before anything is written
+ * (as if its scratch allocation failed: the key set is unchanged), 2: after the updated keys' tables were written
+ * (their key_ok is cleared in the shared key set, so every context holding it rejects them); 0: off. */
+#define PBFT_OPT_FAULT_INJECT 11
+/* 1 (default; env PBFT_COMB_SPREAD): a one-lane comb launch of fewer than 4 blocks per CU (e.g. the 131k shard of
+ * an 8-GPU round) asks for enough LDS that no CU takes more than its even share of the blocks; 0: the kernels'
+ * own LDS (the dispatcher then packs up to 4 blocks on some CUs). */
+#define PBFT_OPT_COMB_SPREAD 12
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

@@ -53,6 +53,8 @@ pub const PBFT_OPT_KERNEL_TIMING: c_int = 7;
 pub const PBFT_OPT_FINISH_WAVES: c_int = 8;
 pub const PBFT_OPT_VOTES_ZERO_COPY: c_int = 9;
 pub const PBFT_OPT_COMB_PAIR: c_int = 10;
+pub const PBFT_OPT_FAULT_INJECT: c_int = 11;
+pub const PBFT_OPT_COMB_SPREAD: c_int = 12;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
 pub const PBFT_KIND_PREPARE: u8 = 1;

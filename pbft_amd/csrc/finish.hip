@@ -65,10 +65,6 @@ extern "C" int pbft_debug_fin_stamps(uint64_t* out, uint32_t waves) {
 #define FIN_STAMP(k)
 #endif
 
-#ifndef PBFT_FIN_LV
-#define PBFT_FIN_LV 4  // product-tree levels: 4 = one inversion per 16-lane row (fe_invert_wave<true>), 6 = one per wave
-                       // (r04 A/B, profiles/r04/ab_fin_lv4.txt: 131k shard -1.8 %, 2^20 -0.4 %)
-#endif
 static_assert(PBFT_FIN_LV == 4 || PBFT_FIN_LV == 6, "");
 #ifndef PBFT_FIN_DPP
 #define PBFT_FIN_DPP 0  // 1: product-tree partners by DPP / ds_swizzle instead of ds_bpermute (r04 A/B: no difference)

@@ -859,10 +859,18 @@ int pbft_replica_create(pbft_ctx* ctx, uint32_t n, uint32_t self_id, const uint8
 int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t* A, uint32_t m, uint8_t* key_ok) {
   if (!r || (m && (!idx || !A))) return PBFT_EINVAL;
   if (r->in_flight) return PBFT_EBUSY;
+  auto replaced = [&](uint32_t slot) {
+    for (uint32_t j = 0; j < m; ++j)
+      if (idx[j] == slot) return true;
+    return false;
+  };
   for (uint32_t i = 0; i < m; ++i) {
     if (idx[i] >= r->n) return PBFT_EINVAL;
     for (uint32_t j = 0; j < i; ++j)
-      if (idx[j] == idx[i]) return PBFT_EINVAL;
+      if (idx[j] == idx[i] || memcmp(A + 32 * (size_t)j, A + 32 * (size_t)i, 32) == 0) return PBFT_EINVAL;
+    // a new key another (kept) slot already holds: one of the two would be unreachable by PeerId
+    auto it = r->key_index.find(key_str(A + 32 * (size_t)i));
+    if (it != r->key_index.end() && it->second != idx[i] && !replaced(it->second)) return PBFT_EINVAL;
   }
   if (r->ctx && m) {
     const int rc = pbft_verify_update_keys(r->ctx, idx, A, m, key_ok);
@@ -870,12 +878,22 @@ int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t
   } else if (key_ok) {
     memset(key_ok, 1, m);  // (no GPU context: the installed verifier override judges the keys)
   }
+  // the old keys' entries: dropped, or handed to a kept slot with the same key (replicas created with duplicates)
+  for (uint32_t i = 0; i < m; ++i) {
+    const std::string old = key_str(&r->keys[32 * (size_t)idx[i]]);
+    auto it = r->key_index.find(old);
+    if (it == r->key_index.end() || it->second != idx[i]) continue;
+    r->key_index.erase(it);
+    for (uint32_t j = 0; j < r->n; ++j)
+      if (!replaced(j) && key_str(&r->keys[32 * (size_t)j]) == old) {
+        r->key_index.emplace(old, j);
+        break;
+      }
+  }
   for (uint32_t i = 0; i < m; ++i) {
     uint8_t* k = &r->keys[32 * (size_t)idx[i]];
-    auto it = r->key_index.find(key_str(k));
-    if (it != r->key_index.end() && it->second == idx[i]) r->key_index.erase(it);
     memcpy(k, A + 32 * (size_t)i, 32);
-    r->key_index.emplace(key_str(k), idx[i]);  // (a key another replica already has keeps its first index)
+    r->key_index[key_str(k)] = idx[i];
   }
   return PBFT_OK;
 }

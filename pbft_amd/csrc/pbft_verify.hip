@@ -9,6 +9,7 @@
 //   batch  SoA: R[N][32], S[N][32], key_idx[N] u16, msg[N][stride]
 //   bitmap ceil(N/64) u64 words, one per wavefront (ballot)
 #include <dlfcn.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>  // types only: librccl.so.1 is dlopen'ed by pbft_multi_create
 #include <stdio.h>
@@ -159,9 +160,12 @@ struct pbft_ctx {
   int fin_waves = 0;                   // product-tree finish compiled for 1 or 2 waves per SIMD (0 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   int comb_pair = -1;                  // comb_pair_kernel: 1 on, 0 off, -1 by batch size (PBFT_OPT_COMB_PAIR)
+  int comb_spread = 1;                 // even block placement of one-generation comb launches (PBFT_OPT_COMB_SPREAD)
+  int cus = 0;                         // compute units of the device
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   pbft_key_stats kstats{};             // the last pbft_verify_set_keys / _update_keys (pbft_verify_key_stats)
+  int fault_inject = 0;                // PBFT_OPT_FAULT_INJECT (tests): fail the next pbft_verify_update_keys
   void adopt(keyset* k) {
     keyset_release(ks);
     ks = k;
@@ -285,6 +289,77 @@ static bool host_pinned(const void* p) {
     return false;
   }
   return a.type == hipMemoryTypeHost;
+}
+// The address kernels read pinned host memory p at, or null (pageable, or no device mapping).
+static const uint8_t* host_dev(const void* p) {
+  if (!p) return nullptr;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  if (a.type != hipMemoryTypeHost || !a.devicePointer || !a.hostPointer) return nullptr;
+  return (const uint8_t*)a.devicePointer + ((const uint8_t*)p - (const uint8_t*)a.hostPointer);
+}
+
+// Host-buffer batches up to one chunk: R, S, key_idx and the messages reach the device staging through ONE kernel
+// that reads the pinned host memory over PCIe (16 B per lane, line-contiguous per wave), instead of four
+// hipMemcpyAsync.  VERDICT r04 item 2: config #5's back-to-back leg had one 7.5-9.4 ms maximum in every bench line;
+// PBFT_LAUNCH_TRACE put it inside hipMemcpyAsync H2D of a 4k batch's columns (profiles/r05/stall_probe.txt: the
+// calling thread blocked 7-30 ms in h2d_R / h2d_M while a kernel launch never did), the same signature as the D2H
+// stalls r04 removed from the votes path.  PBFT_HOST_IMPORT=0 restores the copies (A/B).
+struct import_segs {
+  const uint8_t* src[4];
+  uint64_t dst_off[4];   // 16-B aligned offsets into the destination
+  uint64_t len[4];       // bytes
+  uint64_t first[5];     // first 16-B piece of each segment; first[4] = total pieces
+};
+__global__ void __launch_bounds__(256) import_segs_kernel(import_segs s, uint8_t* __restrict__ dst) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= s.first[4]) return;
+  const int k = c >= s.first[2] ? (c >= s.first[3] ? 3 : 2) : (c >= s.first[1] ? 1 : 0);
+  const uint64_t o = (c - s.first[k]) * 16;
+  const uint8_t* src = s.src[k] + o;
+  uint8_t* d = dst + s.dst_off[k] + o;
+  const uint64_t rem = s.len[k] - o;
+  if (rem >= 16 && ((uintptr_t)src & 15) == 0) {
+    *(uint4*)d = *(const uint4*)src;
+  } else if (rem >= 16 && ((uintptr_t)src & 3) == 0) {
+    const uint32_t* q = (const uint32_t*)src;
+    *(uint4*)d = uint4{q[0], q[1], q[2], q[3]};
+  } else {
+    const int m = rem < 16 ? (int)rem : 16;
+    for (int b = 0; b < m; ++b) d[b] = src[b];
+  }
+}
+static bool host_import_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("PBFT_HOST_IMPORT");
+    return !e || strtol(e, nullptr, 10) != 0;
+  }();
+  return on;
+}
+// Launch the import of up to 4 host segments (device-readable addresses) into dst; false if a source has no device
+// mapping (the caller then copies).
+static bool launch_import(const uint8_t* const* src_host, const uint64_t* dst_off, const uint64_t* len, int n,
+                          uint8_t* dst, hipStream_t st) {
+  if (!host_import_enabled()) return false;
+  import_segs s{};
+  uint64_t pieces = 0;
+  for (int k = 0; k < 4; ++k) {
+    s.first[k] = pieces;
+    if (k < n && len[k]) {
+      s.src[k] = host_dev(src_host[k]);
+      if (!s.src[k]) return false;
+      s.dst_off[k] = dst_off[k];
+      s.len[k] = len[k];
+      pieces += (len[k] + 15) / 16;
+    }
+  }
+  s.first[4] = pieces;
+  if (pieces == 0) return true;
+  hipLaunchKernelGGL(import_segs_kernel, dim3((unsigned)((pieces + 255) / 256)), dim3(256), 0, st, s, dst);
+  return true;
 }
 
 // Pinned layout of a staged votes batch (pbft_verify_votes_stage): n rows of PBFT_VOTES_ROW_BYTES, then the
@@ -464,6 +539,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.eidx = (uint32_t*)(wbase + eidx_offset(W));
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.mi_stride = mi_stride; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   a.pair = c->comb_pair;
+  a.cus = c->cus;
+  a.spread = c->comb_spread;
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
   if (r_host && !latency_mode) a.r_copy = (uint32_t*)(wbase + rcopy_offset(W, wtwo));
@@ -488,7 +565,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     // cross-lane product tree (one variable-time inversion per 16-lane row since r04, per wave before) where few
     // signatures share a lane: 131k 0.2106 -> 0.2061 ms at fm 4, 0.2467 -> 0.2160 at fm 1; no gain at fm 16
     // (profiles/r02_ab_log.md); lv is a flag here, finish.hip compiles the tree depth (PBFT_FIN_LV)
-    int lv = fm <= PBFT_FIN_TREE_MAX_FM ? 6 : 0;
+    int lv = fm <= PBFT_FIN_TREE_MAX_FM ? PBFT_FIN_LV : 0;
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
     const int fw = c->fin_waves ? c->fin_waves : (big ? PBFT_FIN_W_BIG : 1);
@@ -550,11 +627,21 @@ static int stage_and_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
     const stage_layout L(N, msg_stride);
     int rc = ensure_stage(c, L.bytes, words);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(c->d_stage, R, 32 * N, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_stage + L.offS, S, 32 * N, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_stage + L.offK, K, 2 * N, hipMemcpyHostToDevice, c->stream));
-    if ((size_t)msg_stride * N)
-      HIP_TRY(hipMemcpyAsync(c->d_stage + L.offM, M, (size_t)msg_stride * N, hipMemcpyHostToDevice, c->stream));
+    const uint8_t* src[4] = {R, S, (const uint8_t*)K, M};
+    const uint64_t off[4] = {0, L.offS, L.offK, L.offM};
+    const uint64_t len[4] = {32 * N, 32 * N, 2 * N, (uint64_t)msg_stride * N};
+    bool imported = false;
+    LT("import", imported = launch_import(src, off, len, 4, c->d_stage, c->stream));
+    if (imported) {
+      HIP_TRY(hipGetLastError());
+    } else {
+      LT("h2d_R", HIP_TRY(hipMemcpyAsync(c->d_stage, R, 32 * N, hipMemcpyHostToDevice, c->stream)));
+      LT("h2d_S", HIP_TRY(hipMemcpyAsync(c->d_stage + L.offS, S, 32 * N, hipMemcpyHostToDevice, c->stream)));
+      LT("h2d_K", HIP_TRY(hipMemcpyAsync(c->d_stage + L.offK, K, 2 * N, hipMemcpyHostToDevice, c->stream)));
+      if ((size_t)msg_stride * N)
+        LT("h2d_M", HIP_TRY(hipMemcpyAsync(c->d_stage + L.offM, M, (size_t)msg_stride * N, hipMemcpyHostToDevice,
+                                           c->stream)));
+    }
     return launch_verify(c, c->d_stage, c->d_stage + L.offS, (const uint16_t*)(c->d_stage + L.offK),
                          c->d_stage + L.offM, msg_len, msg_stride, N, c->d_bitmap, c->stream);
   }
@@ -856,6 +943,8 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   pbft_ctx* c = new pbft_ctx();
   c->device = device;
+  c->cus = prop.multiProcessorCount;
+  if (const char* e = getenv("PBFT_COMB_SPREAD")) c->comb_spread = strtol(e, nullptr, 10) != 0;
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
   if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
@@ -1021,6 +1110,14 @@ int pbft_verify_set_keys(pbft_ctx* c, const uint8_t* A, uint32_t n, uint8_t* key
 
 // Replace m keys of the installed set in place (the reference admits peers one at a time,
 // src/behavior.rs:45-61 add_peer via src/network_behaviour_composer.rs:24-33): only their tables are rebuilt.
+// The key set is shared by every clone of this context, so is the update.  Failure handling: a failure
+// before any table is written (scratch allocation, key upload) changes nothing; one after the build kernels were
+// launched clears key_ok of the updated slots in the SHARED key set -- every context that holds it then rejects
+// those keys (their tables may be half-written) instead of verifying against them, the other keys keep working.
+__global__ void clear_key_ok_kernel(uint8_t* key_ok, const uint32_t* slots, uint32_t m) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) key_ok[slots[i]] = 0;
+}
 int pbft_verify_update_keys(pbft_ctx* c, const uint32_t* idx, const uint8_t* A, uint32_t m, uint8_t* key_ok) {
   if (!c || (m && (!idx || !A))) return set_err(PBFT_EINVAL, "null argument");
   if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
@@ -1034,22 +1131,25 @@ int pbft_verify_update_keys(pbft_ctx* c, const uint32_t* idx, const uint8_t* A, 
   pbft_key_stats ks{};
   ks.reused = 1;
   if (m == 0) { c->kstats = ks; return PBFT_OK; }
+  const int inject = c->fault_inject;
+  c->fault_inject = 0;
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipDeviceSynchronize());  // no launch (this context's, a clone's, a device form's) reads the old tables
   keyset* k = c->ks;
   uint8_t* d_tmp = nullptr;  // [m] slots (u32) then [m][32] encodings
   const size_t off_enc = ((size_t)4 * m + 255) & ~(size_t)255;
-  if (hipMalloc(&d_tmp, off_enc + 32 * (size_t)m) != hipSuccess) {
+  if (inject == 1 || hipMalloc(&d_tmp, off_enc + 32 * (size_t)m) != hipSuccess) {
     (void)hipGetLastError();
-    return set_err(PBFT_ENOMEM, "update staging alloc");
+    return set_err(PBFT_ENOMEM, "update staging alloc");  // nothing written: the key set is unchanged
   }
-  int rc = PBFT_OK;
+  int rc = PBFT_OK, wrote = 0;
   if (hipMemcpyAsync(d_tmp, idx, 4 * (size_t)m, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(d_tmp + off_enc, A, 32 * (size_t)m, hipMemcpyHostToDevice, c->stream) != hipSuccess)
     rc = set_err(PBFT_EHIP, "key upload");
   if (!rc && build_comb_tables(k->pa, (const uint32_t*)(d_tmp + off_enc), m, 1, k->d_tabA, k->d_key_ok, c->stream,
-                               (const uint32_t*)d_tmp, k->d_keys) != hipSuccess)
-    rc = set_err(PBFT_EHIP, "key table build");
+                               (const uint32_t*)d_tmp, k->d_keys, &wrote) != hipSuccess)
+    rc = set_err(PBFT_EHIP, wrote ? "key table build" : "key table build scratch alloc");
+  if (!rc && inject == 2) rc = set_err(PBFT_EHIP, "key table build (injected fault)");
   std::vector<uint8_t> ok_all;
   if (!rc && key_ok) {
     ok_all.resize(k->n);
@@ -1057,11 +1157,19 @@ int pbft_verify_update_keys(pbft_ctx* c, const uint32_t* idx, const uint8_t* A, 
       rc = set_err(PBFT_EHIP, "key_ok download");
   }
   if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "key table build");
-  (void)hipFree(d_tmp);
-  if (rc) {
-    c->adopt(nullptr);  // tables of the updated slots may be half-written
-    return rc;
+  if (rc && (wrote || inject == 2)) {
+    // the updated slots' tables may be half-written: reject them everywhere the key set is used
+    const std::string why = g_last_error;
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(clear_key_ok_kernel, dim3((m + 255) / 256), dim3(256), 0, c->stream, k->d_key_ok,
+                       (const uint32_t*)d_tmp, m);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+      c->adopt(nullptr);  // could not even mark them: drop the key set from this context rather than trust it
+    g_last_error = why;
   }
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(d_tmp);
+  if (rc) return rc;
   if (key_ok)
     for (uint32_t i = 0; i < m; ++i) key_ok[i] = ok_all[idx[i]];
   ks.keys_built = m;
@@ -1096,6 +1204,8 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->timing = parent->timing;
   c->zero_copy = parent->zero_copy;
   c->two_streams = parent->two_streams;
+  c->comb_pair = parent->comb_pair;
+  c->comb_spread = parent->comb_spread;
   c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
@@ -1116,7 +1226,9 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
   if (N == 0) return PBFT_OK;
   HIP_TRY(hipSetDevice(c->device));
-  if (!(host_pinned(R) && host_pinned(S) && host_pinned(K) && host_pinned(M))) {
+  bool pinned = false;
+  LT("pinned_query", pinned = host_pinned(R) && host_pinned(S) && host_pinned(K) && host_pinned(M));
+  if (!pinned) {
     // pageable: copy into the pinned staging first, so the DMA below is asynchronous (a pageable
     // hipMemcpyAsync stages through the runtime's buffers and returns only when the copy is done)
     const host_batch_layout L(N, msg_stride);
@@ -1132,13 +1244,32 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
   int rc = stage_and_launch(c, R, S, K, M, msg_len, msg_stride, N);
   if (rc) return rc;
   const uint64_t words = (N + 63) / 64;
-  HIP_TRY(export_words(c, 0, words, c->stream));
-  HIP_TRY(hipEventRecord(c->ev_done, c->stream));
+  LT("export_bitmap", HIP_TRY(export_words(c, 0, words, c->stream)));
+  LT("rec_done", HIP_TRY(hipEventRecord(c->ev_done, c->stream)));
   c->in_flight = true;
   c->v_readback = false;
   c->async_out = out;
   c->async_words = words;
   return PBFT_OK;
+}
+
+// Wait for an event by polling hipEventQuery instead of hipEventSynchronize.  VERDICT r04 item 2: with the H2D
+// copies of a 4k host batch replaced by the import kernel, the back-to-back leg's stall moved into
+// hipEventSynchronize (10.8 ms once in 5 one-second reps, profiles/r05/stall_probe.txt): the runtime's blocking
+// wait (spin briefly, then sleep on the completion interrupt) sometimes wakes milliseconds late.  A serving
+// thread that waits for its batch is latency-critical, so it polls (yielding the core between polls) -- the same
+// thing the replica's flush_poll and the bench's poll loops do.  PBFT_SPIN_WAIT=0 restores hipEventSynchronize.
+static hipError_t wait_event(hipEvent_t e) {
+  static const bool spin = [] {
+    const char* v = getenv("PBFT_SPIN_WAIT");
+    return !v || strtol(v, nullptr, 10) != 0;
+  }();
+  if (!spin) return hipEventSynchronize(e);
+  for (uint32_t k = 0;; ++k) {
+    const hipError_t q = hipEventQuery(e);
+    if (q != hipErrorNotReady) return q;
+    if ((k & 63) == 63) sched_yield();
+  }
 }
 
 static int finish_async(pbft_ctx* c) {
@@ -1155,7 +1286,8 @@ int pbft_verify_poll(pbft_ctx* c) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight) return 1;
   if (c->v_open) return 0;  // progressive batch: not every chunk launched yet
-  hipError_t e = hipEventQuery(c->ev_done);
+  hipError_t e;
+  LT("poll_query", e = hipEventQuery(c->ev_done));
   if (e == hipErrorNotReady) return 0;
   if (e != hipSuccess) {
     c->in_flight = false;  // the batch is lost; the context stays usable for the next submit
@@ -1169,7 +1301,8 @@ int pbft_verify_wait(pbft_ctx* c) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight) return PBFT_OK;
   if (c->v_open) return set_err(PBFT_EBUSY, "progressive votes batch not fully submitted");
-  const hipError_t e = hipEventSynchronize(c->ev_done);
+  hipError_t e;
+  LT("wait_sync", e = wait_event(c->ev_done));
   if (e != hipSuccess) {
     c->in_flight = false;
     HIP_TRY(e);
@@ -1251,7 +1384,6 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (!c->in_flight || !c->v_open) return set_err(PBFT_EINVAL, "no progressive votes batch open");
   HIP_TRY(hipSetDevice(c->device));
-  const uint64_t N = c->v_n;
   uint8_t* h = c->h_stage;
   int rc = votes_launch(c, h, h + 32, (const uint16_t*)(h + PBFT_VOTES_ROW_KEY), (const uint32_t*)(h + PBFT_VOTES_ROW_ENV),
                         ROW, rows);
@@ -1682,13 +1814,22 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
         return set_err(PBFT_EINVAL, "finish width");
       c->fin_m = (int)value;
       return PBFT_OK;
-    case PBFT_OPT_FINISH_TREE: c->fin_tree = (value == 0 || value == 4 || value == 6) ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_FINISH_TREE:
+      // the one compiled tree depth (PBFT_FIN_LV) or none; the other depth is a build-time A/B (-DPBFT_FIN_LV)
+      if ((value == 4 || value == 6) && value != PBFT_FIN_LV) return set_err(PBFT_EINVAL, "finish tree depth not compiled");
+      c->fin_tree = (value == 0 || value == PBFT_FIN_LV) ? (int)value : -1;
+      return PBFT_OK;
     case PBFT_OPT_FINISH_WAVES: c->fin_waves = (value == 1 || value == 2) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
     case PBFT_OPT_VOTES_ZERO_COPY: c->zero_copy = value != 0; return PBFT_OK;
     case PBFT_OPT_COMB_PAIR: c->comb_pair = value <= 1 ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
+    case PBFT_OPT_COMB_SPREAD: c->comb_spread = value != 0; return PBFT_OK;
+    case PBFT_OPT_FAULT_INJECT:
+      if (value > 2) return set_err(PBFT_EINVAL, "fault injection point");
+      c->fault_inject = (int)value;
+      return PBFT_OK;
   }
   return set_err(PBFT_EINVAL, "unknown option");
 }

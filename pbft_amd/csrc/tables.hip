@@ -117,33 +117,42 @@ __global__ void __launch_bounds__(BLOCK) comb_entry_kernel(const ge* __restrict_
 
 template <class PL>
 static hipError_t build_tables(const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables, uint8_t* d_key_ok,
-                               hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out) {
+                               hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out, int* wrote) {
+  // scratch first: a failed allocation returns before anything the caller's key set holds is touched
   ge* d_bases = nullptr;
   uint8_t* d_dec = nullptr;
-  PBFT_HIP_RET(hipMalloc(&d_bases, sizeof(ge) * (size_t)PL::P * n));
-  PBFT_HIP_RET(hipMalloc(&d_dec, n));
-  const uint64_t t1 = (uint64_t)PL::P * n;
-  hipLaunchKernelGGL(comb_base_kernel<PL>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc, n,
-                     negate, d_bases, d_dec, d_key_ok, d_slot, d_keys_out);
-  PBFT_HIP_RET(hipGetLastError());
-  const uint64_t t2 = (uint64_t)plan_runs_total<PL>() * n;
-  hipLaunchKernelGGL(comb_entry_kernel<PL>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_bases,
-                     d_dec, n, d_tables, d_slot);
-  PBFT_HIP_RET(hipGetLastError());
-  PBFT_HIP_RET(hipStreamSynchronize(st));
-  PBFT_HIP_RET(hipFree(d_bases));
-  PBFT_HIP_RET(hipFree(d_dec));
-  return hipSuccess;
+  hipError_t e = hipMalloc(&d_bases, sizeof(ge) * (size_t)PL::P * n);
+  if (e == hipSuccess) e = hipMalloc(&d_dec, n);
+  if (e == hipSuccess) {
+    if (wrote) *wrote = 1;
+    const uint64_t t1 = (uint64_t)PL::P * n;
+    hipLaunchKernelGGL(comb_base_kernel<PL>, dim3((unsigned)((t1 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st, d_enc,
+                       n, negate, d_bases, d_dec, d_key_ok, d_slot, d_keys_out);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
+    const uint64_t t2 = (uint64_t)plan_runs_total<PL>() * n;
+    hipLaunchKernelGGL(comb_entry_kernel<PL>, dim3((unsigned)((t2 + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, st,
+                       d_bases, d_dec, n, d_tables, d_slot);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  else (void)hipStreamSynchronize(st);  // (nothing may still read the scratch when it is freed)
+  if (d_bases) (void)hipFree(d_bases);
+  if (d_dec) (void)hipFree(d_dec);
+  return e;
 }
 
 hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
-                             uint8_t* d_key_ok, hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out) {
+                             uint8_t* d_key_ok, hipStream_t st, const uint32_t* d_slot, uint32_t* d_keys_out,
+                             int* wrote) {
+  if (wrote) *wrote = 0;
   switch (pa) {
-    case 0: return build_tables<PLB>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
-    case PLA_HUGE::P: return build_tables<PLA_HUGE>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
-    case PLA_BIG::P: return build_tables<PLA_BIG>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
-    case PLA_MID::P: return build_tables<PLA_MID>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
-    case PLA_SMALL::P: return build_tables<PLA_SMALL>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out);
+    case 0: return build_tables<PLB>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out, wrote);
+    case PLA_HUGE::P: return build_tables<PLA_HUGE>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out, wrote);
+    case PLA_BIG::P: return build_tables<PLA_BIG>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out, wrote);
+    case PLA_MID::P: return build_tables<PLA_MID>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out, wrote);
+    case PLA_SMALL::P: return build_tables<PLA_SMALL>(d_enc, n, negate, d_tables, d_key_ok, st, d_slot, d_keys_out, wrote);
     default: return hipErrorInvalidValue;
   }
 }

@@ -86,6 +86,11 @@ __device__ __forceinline__ u32x4 lds_read16(uint32_t addr) {
 #ifndef FIN_M
 #define FIN_M 16
 #endif
+#ifndef PBFT_FIN_LV
+#define PBFT_FIN_LV 4  // finish product-tree levels (finish.hip): 4 = one inversion per 16-lane row
+                       // (fe_invert_wave<true>), 6 = one per wave (r04 A/B, profiles/r04/ab_fin_lv4.txt: 131k shard
+                       // -1.8 %, 2^20 -0.4 %); one depth is compiled, PBFT_OPT_FINISH_TREE selects it or none
+#endif
 #ifndef FIN_WAVES_PER_EU
 #define FIN_WAVES_PER_EU 1
 #endif
@@ -221,6 +226,22 @@ __device__ __forceinline__ void sha512_k(uint32_t h[16], const uint32_t r[8], co
   }
 }
 
+// Diagnostic build (PBFT_COMB_STAMPS=1, never the product): every wave of comb_kernel stamps its phases into
+// g_comb_stamp (a buffer no other code reads; read back by pbft_debug_comb_stamps in comb_pa13.hip, the 13-position
+// plan's translation unit).  Per wave: [0] s_memtime at start, [1] s_memrealtime at start, [2] s_memtime once the
+// hash, reduction and digit recoding are done, [3] shader cycles spent in the gathers' vmcnt(0) waits (summed over
+// the steps), [4] s_memtime at the end, [5] s_memrealtime at the end, [6] cycles in the steps' lgkmcnt(0) waits,
+// [7] the HW_ID register (SE / CU / SIMD of the wave).  VERDICT r04 item 3: attribute the 131k shard's stalls.
+#ifndef PBFT_COMB_STAMPS
+#define PBFT_COMB_STAMPS 0
+#endif
+#if PBFT_COMB_STAMPS
+#define COMB_STAMP_WAVES 16384
+static __device__ uint64_t g_comb_stamp[COMB_STAMP_WAVES][8];
+#define COMB_T() __builtin_amdgcn_s_memtime()
+#define COMB_RT() __builtin_amdgcn_s_memrealtime()
+#endif
+
 template <int LEN, class PLA, bool CHAIN = false>
 __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
@@ -241,6 +262,25 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   const uint64_t ii = live ? i : 0;  // dead lanes recompute lane 0 (no OOB reads)
   typename ST::mask_t sgn = 0;        // bit j: digit of step j is negative
   bool s_ok, kok;
+#if PBFT_COMB_STAMPS
+  const uint64_t st_t0 = COMB_T(), st_rt0 = COMB_RT();
+  uint64_t st_wait = 0, st_lgkm = 0, st_hash = 0;
+#define COMB_WAIT_VM()                                  \
+  do {                                                  \
+    const uint64_t a_ = COMB_T();                       \
+    __builtin_amdgcn_s_waitcnt(0x0F70);                 \
+    st_wait += COMB_T() - a_;                           \
+  } while (0)
+#define COMB_WAIT_LGKM()                                \
+  do {                                                  \
+    const uint64_t a_ = COMB_T();                       \
+    __builtin_amdgcn_s_waitcnt(0xC07F);                 \
+    st_lgkm += COMB_T() - a_;                           \
+  } while (0)
+#else
+#define COMB_WAIT_VM()
+#define COMB_WAIT_LGKM() __builtin_amdgcn_s_waitcnt(0xC07F)
+#endif
   {
     uint32_t r[8], s[8], a[8];
     load32(r, R + (size_t)rs_stride * ii);
@@ -298,6 +338,9 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
       eidx[(size_t)j * Npad + i] = e;
     });
   }
+#if PBFT_COMB_STAMPS
+  st_hash = COMB_T();
+#endif
   const uint8_t* tB = (const uint8_t*)tabB;
   const uint8_t* tA = (const uint8_t*)tabA;
   const uint32_t rd0 = ebuf + 128u * lane + 16u * (lane & 7);  // logical byte o of my entry at rd0 ^ o
@@ -309,8 +352,9 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     // step 0: P = +-T_B[0][s_0] directly (1 multiplication instead of a 7-multiplication addition)
     fe qa, qb, k;
     const bool neg = (uint32_t)sgn & 1u;
+    COMB_WAIT_VM();
     lds_entry_signed(rd0, neg, qa, qb, k);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): entry in VGPRs before the DMA reuses the buffer
+    COMB_WAIT_LGKM();  // lgkmcnt(0): entry in VGPRs before the DMA reuses the buffer
     dma_entry_lines(ST::is_a(1) ? tA : tB, nidx, lane, ebuf);
     nidx = eidx[2 * Npad + i];
     ge_from_ab(P, qa, qb, k, neg);
@@ -318,9 +362,10 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
   for (int j = 1; j < ST::N - 1; ++j) {
     fe qa, qb, k;
     const bool neg = (uint32_t)(sgn >> j) & 1u;
+    COMB_WAIT_VM();
     lds_entry_signed(rd0, neg, qa, qb, k);
     // the entry must be in VGPRs before the DMA overwrites the buffer (WAR on LDS)
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    COMB_WAIT_LGKM();  // lgkmcnt(0)
     dma_entry_lines(ST::is_a(j + 1) ? tA : tB, nidx, lane, ebuf);
     if (j + 2 < ST::N) nidx = eidx[(size_t)(j + 2) * Npad + i];
 #if PBFT_ABL_NOMADD  // ablation: gathers only, no group arithmetic
@@ -343,9 +388,24 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     // last step: R' needs X, Y, Z only (6 multiplications)
     fe qa, qb, k;
     const bool neg = (uint32_t)(sgn >> (ST::N - 1)) & 1u;
+    COMB_WAIT_VM();
     lds_entry_signed(rd0, neg, qa, qb, k);
     ge_madd_ab<false, CHAIN>(P, P, qa, qb, k, neg);
   }
+#if PBFT_COMB_STAMPS
+  {
+    const uint64_t t_end = COMB_T(), rt_end = COMB_RT();
+    const uint64_t gw = (uint64_t)blockIdx.x * (BLOCK / 64) + wave;
+    if (lane == 0 && gw < COMB_STAMP_WAVES) {
+      uint64_t* o = g_comb_stamp[gw];
+      o[0] = st_t0; o[1] = st_rt0; o[2] = st_hash; o[3] = st_wait; o[4] = t_end; o[5] = rt_end; o[6] = st_lgkm;
+      o[7] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |       // HW_ID (hwreg 4)
+             ((uint64_t)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);  // XCC_ID (hwreg 20)
+    }
+  }
+#endif
+#undef COMB_WAIT_VM
+#undef COMB_WAIT_LGKM
   if (live) {
 #pragma unroll
     for (int t = 0; t < 10; ++t) {
@@ -940,8 +1000,24 @@ struct comb_launch_args {
   bool latency_mode;
   int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
   int pair = -1;           // one-lane mode: comb_pair_kernel 1 / comb_kernel 0 / by batch size -1
+  int cus = 0;             // compute units of the device (0: unknown)
+  int spread = 1;          // one-lane mode: cap blocks per CU at the launch's share (comb_spread_lds)
   hipStream_t st;
 };
+
+// Even placement of a one-generation launch.  The 131k shard's comb launch is 512 blocks of 4
+// waves (128 VGPRs: up to 4 blocks per CU), i.e. 2 per CU if spread evenly -- but the stamped build showed the
+// waves ending anywhere between 94 and 148 us after a common start, live waves falling to 0.9 per SIMD over the
+// last quarter of the launch (profiles/r05/shard_waits.txt): the dispatcher packs up to 4 blocks onto some CUs
+// and leaves others short, and the launch lasts as long as its most crowded SIMD.  Requesting enough LDS that a CU
+// holds at most ceil(blocks / CUs) blocks forces the even placement.  Launches of >= 4 blocks per CU keep lds_min.
+static inline size_t comb_spread_lds(uint64_t blocks, int cus, size_t lds_min) {
+  if (cus <= 0 || blocks == 0) return lds_min;
+  const uint64_t per = (blocks + (uint64_t)cus - 1) / (uint64_t)cus;
+  // X with per * X <= 160 KB < (per + 1) * X: 1 -> 96 KB, 2 -> 72 KB, 3 -> 48 KB
+  const size_t want = per == 1 ? 96 * 1024 : per == 2 ? 72 * 1024 : per == 3 ? 48 * 1024 : 0;
+  return want > lds_min ? want : lds_min;
+}
 
 // Launch the comb (or, in latency mode, the 4-lanes-per-signature kernel) for
 // key plan PLA; LEN 85 (the signed envelope) is a specialised template.
@@ -967,12 +1043,14 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
 #undef PBFT_LAUNCH_LAT
   } else {
     const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
-    const size_t lds = (BLOCK / 64) * COMB_LDS_PER_WAVE;
     const bool pair = a.pair >= 0 ? a.pair > 0 : (N >= PBFT_PAIR_MIN_N && N <= PBFT_PAIR_MAX_N);
+    const size_t lds = a.spread ? comb_spread_lds(blocks, a.cus, (BLOCK / 64) * COMB_LDS_PER_WAVE)
+                                : (BLOCK / 64) * COMB_LDS_PER_WAVE;
     if (pair) {
       const uint64_t pblocks = (N + PAIR_SIGS - 1) / PAIR_SIGS;
+      const size_t plds = a.spread ? comb_spread_lds(pblocks, a.cus, PAIR_LDS) : PAIR_LDS;
 #define PBFT_LAUNCH_PAIR(LEN_)                                                                                     \
-  hipLaunchKernelGGL((comb_pair_kernel<LEN_, PLA>), dim3((unsigned)pblocks), dim3(BLOCK), PAIR_LDS, a.st, a.R, a.S, \
+  hipLaunchKernelGGL((comb_pair_kernel<LEN_, PLA>), dim3((unsigned)pblocks), dim3(BLOCK), plds, a.st, a.R, a.S,     \
                      a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,    \
                      a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy)
       if (a.msg_len == PBFT_ENVELOPE_LEN) PBFT_LAUNCH_PAIR(PBFT_ENVELOPE_LEN);
@@ -1002,10 +1080,12 @@ hipError_t launch_comb_small(const comb_launch_args& a);
 
 // tables.hip: comb tables of the base point (pa = 0, plan PLB) or of -A per key (pa = the key plan's positions).
 // d_slot (optional): key k goes to slot d_slot[k] of d_tables / d_key_ok / d_keys_out (partial rebuild);
-// d_keys_out (optional): the raw encodings, stored at their slots.
+// d_keys_out (optional): the raw encodings, stored at their slots.  *wrote (optional) is set to 1 once a kernel
+// that writes the tables / key_ok / keys_out has been launched: a failure with *wrote == 0 changed nothing (the
+// scratch is allocated before the first launch).
 hipError_t build_comb_tables(int pa, const uint32_t* d_enc, uint32_t n, int negate, uint32_t* d_tables,
                              uint8_t* d_key_ok, hipStream_t st, const uint32_t* d_slot = nullptr,
-                             uint32_t* d_keys_out = nullptr);
+                             uint32_t* d_keys_out = nullptr, int* wrote = nullptr);
 
 // finish.hip: batch-inversion finish of the one-lane comb: fm (1, 2, 4, 8, 16) signatures per lane, lv = 0
 // (one inversion per lane) or nonzero (cross-lane product tree of PBFT_FIN_LV levels: one inversion per 16-lane

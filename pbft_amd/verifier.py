@@ -294,6 +294,8 @@ class GpuBatchVerifier:
     OPT_FINISH_WAVES = 8
     OPT_VOTES_ZERO_COPY = 9
     OPT_COMB_PAIR = 10
+    OPT_FAULT_INJECT = 11
+    OPT_COMB_SPREAD = 12
 
     def set_option(self, option: int, value: int) -> None:
         """pbft_verify_set_option: latency-mode threshold, finish width, key-table budget (include/pbft_verify.h)."""

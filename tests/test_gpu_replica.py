@@ -164,14 +164,16 @@ def test_gpu_replica_2p20_round(gpu_cluster):
     ev = (Event * 8192)()
     ne = ctypes.c_uint32()
     polls = 0
+    evs = []   # every poll's events (a progressive batch may deliver some before it is done)
     while True:
         rc = L.pbft_replica_flush_poll(rep, ev, 8192, ctypes.byref(ne))
         assert rc >= 0
+        evs += [(e.seq, e.kind) for e in ev[: ne.value]]
         if rc == 1:
             break
         polls += 1
     t2 = time.perf_counter()
-    evs = [(e.seq, e.kind) for e in ev[: ne.value]]
+    assert [q for q, _ in evs] == sorted(q for q, _ in evs)   # (view, seq) order across the chunks
     assert {q for q, k in evs if k == EV_PREPARED} == set(range(1, seqs + 1)) - {7}
     assert {q for q, k in evs if k == EV_COMMITTED} == set(range(1, seqs + 1)) - {7, 9}
     from replica_sim import Stats

@@ -51,7 +51,7 @@ def oracle_bits(coracle, keys, R, S, key_idx, msg, msg_len):
     msg = np.ascontiguousarray(msg)
     rc = coracle.oracle_verify_batch(keys.ctypes.data, len(keys), R.ctypes.data, S.ctypes.data, key_idx.ctypes.data,
                                      msg.ctypes.data, msg_len, msg.shape[1], n, out.ctypes.data,
-                                     min(32, os.cpu_count() or 1))
+                                     min(16, os.cpu_count() or 1))  # the GPU box's CPU share
     assert rc == 0
     return out.astype(bool)
 
@@ -230,6 +230,87 @@ def test_config4_full_size_properties(gv, coracle):
     for n in (300_007, 65_536 + 63, 4096):
         got4, _ = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
         assert (got4 == got2[:n]).all(), n
+
+
+def test_config4_every_lane_vs_oracle(gv, coracle):
+    """the headline round (n = 256 keys, 2048 seqs x {Prepare, Commit} = 2^20 GPU-signed
+    envelopes) with every adversarial class at 0.5 %, a small-order key (slot 254) and a mixed-order key (slot 255,
+    with Python-built equation-valid and cofactored-only signatures) in the key set: EVERY lane of the SoA path,
+    the votes form (host columns and staged rows) and config #5's serving path (16 x 4096-signature batches
+    submitted concurrently over 4 cloned contexts, from one thread and from 4 threads) equals the C oracle
+    (oracle_verify_batch over all 2^20 lanes).  Slots certified: /root/reference/src/behavior.rs:159-195."""
+    import concurrent.futures as cf
+
+    import torch
+    import fullround as F
+    from pbft_amd import SigBatch, bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 256, 2048, tag=4)
+    n = len(R)
+    assert n == 1 << 20
+    pub2, a = F.install_special_keys(seeds, pub, small_slot=254, mixed_slot=255)
+    ok = gv.set_keys(pub2)
+    assert ok[:254].all() and not ok[254] and ok[255]
+    R1, S1, v_lanes, c_lanes = F.plant_mixed(R, S, key_idx, msg, 85, pub2, a, 255, n_valid=192, n_cofactored=96,
+                                             seed=4)
+    rng = np.random.default_rng(44)
+    R2, S2, K2, M2, idx = adversarial(rng, pub2, R1, S1, key_idx, msg, frac=0.005)
+    exp = oracle_bits(coracle, pub2, R2, S2, K2, M2, 85)
+    # the construction did what it says (checked on the oracle's bits)
+    untouched = np.ones(n, bool)
+    untouched[idx] = False
+    assert exp[np.setdiff1d(v_lanes, idx)].all() and not exp[c_lanes].any()
+    assert not exp[K2 == 254].any() and not exp[idx].any()
+    assert exp[untouched & (K2 < 254)].all()
+    assert 0.97 * n < exp.sum() < n
+
+    def check(got, what, sl=slice(None)):
+        bad = np.nonzero(got != exp[sl])[0]
+        assert len(bad) == 0, (what, len(bad), bad[:10])
+
+    got, bm = verify(gv, R2, S2, K2, M2, 85)
+    check(got, "soa")
+    # votes form: a table of the round's distinct envelopes (mutated messages are envelopes of their own)
+    env, inv = np.unique(M2, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    check(bitmap_to_bool(gv.verify_votes(R2, S2, K2, ei, env), n), "votes")
+    st = gv.stage_votes(n, len(env))
+    st["sig"][:, :32], st["sig"][:, 32:], st["key_idx"][:], st["env_idx"][:] = R2, S2, K2, ei
+    st["envelopes"][:] = env
+    check(bitmap_to_bool(gv.wait(gv.submit_staged(n, len(env))), n), "votes staged")
+    # config #5: 16 batches of 4096 over 4 clones, four in flight at once
+    offs = [int(o) // 64 * 64 for o in np.linspace(0, n - 4096, 16)]
+    clones = [gv.clone() for _ in range(4)]
+    try:
+        pin = lambda x: torch.from_numpy(np.ascontiguousarray(x)).pin_memory().numpy()  # noqa: E731
+        PR, PS, PK, PM = pin(R2), pin(S2), pin(K2), pin(M2)
+        for g in range(0, 16, 4):
+            tickets = []
+            for ci, o in enumerate(offs[g:g + 4]):
+                sl = slice(o, o + 4096)
+                tickets.append((ci, o, clones[ci].submit(SigBatch(PR[sl], PS[sl], PK[sl], PM[sl], 85))))
+            while tickets:
+                rest = []
+                for ci, o, t in tickets:
+                    out = clones[ci].poll(t)
+                    if out is None:
+                        rest.append((ci, o, t))
+                    else:
+                        check(bitmap_to_bool(out, 4096), ("stream", o), slice(o, o + 4096))
+                tickets = rest
+
+        def worker(ci):
+            res = []
+            for o in offs[ci::4]:
+                sl = slice(o, o + 4096)
+                res.append((o, bitmap_to_bool(clones[ci].verify(SigBatch(R2[sl], S2[sl], K2[sl], M2[sl], 85)), 4096)))
+            return res
+        with cf.ThreadPoolExecutor(4) as ex:
+            for fut in [ex.submit(worker, ci) for ci in range(4)]:
+                for o, got4 in fut.result():
+                    check(got4, ("threads", o), slice(o, o + 4096))
+    finally:
+        for c in clones:
+            c.close()
 
 
 def test_api_edges_and_async(gv, coracle, golden):
@@ -472,7 +553,7 @@ def test_config2_pipelined_window(gv, coracle):
     try:
         v1.set_keys(pub)
         n2 = len(R2) - 37
-        for lv, waves in ((0, 1), (6, 1), (6, 2)):  # (6, 2): the tree finish compiled for 2 waves per SIMD
+        for lv, waves in ((0, 1), (4, 1), (4, 2)):  # (4, 2): the tree finish compiled for 2 waves per SIMD
             v1.set_option(v1.OPT_FINISH_TREE, lv)
             v1.set_option(v1.OPT_FINISH_WAVES, waves)
             for fm in (1, 2, 4, 8, 16):
@@ -481,6 +562,8 @@ def test_config2_pipelined_window(gv, coracle):
                 assert (got1 == exp).all(), (fm, lv, waves)
                 got2, _ = verify(v1, R2[:n2], S2[:n2], K2[:n2], M2[:n2], 85)
                 assert (got2 == exp[:n2]).all(), (fm, lv, waves, n2)
+        with pytest.raises(Exception):               # the tree depth that is not compiled
+            v1.set_option(v1.OPT_FINISH_TREE, 6)
         with pytest.raises(Exception):
             v1.set_option(v1.OPT_FINISH_WIDTH, 3)
     finally:
@@ -828,3 +911,43 @@ def test_rekey_in_place_and_partial_update(gv, coracle):
         assert v2.set_keys(pub_new[:8]).all() and v2.key_stats()["reused"] == 1
     finally:
         v2.close()
+
+
+def test_update_keys_failure_keeps_shared_set_consistent(gv, coracle):
+    """pbft_verify_update_keys failing before anything is written (PBFT_OPT_FAULT_INJECT 1, as
+    if its scratch allocation failed) leaves the key set -- shared with a clone -- unchanged; failing after the
+    updated keys' tables were written (2) clears their key_ok in the shared set, so both contexts reject signatures
+    under those slots and keep verifying every other key; a later successful update restores the slots."""
+    from pbft_amd import PbftError
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 64, tag=61)      # 2,048 signatures
+    assert gv.set_keys(pub).all()
+    cl = gv.clone()
+    try:
+        slots = np.array([3, 9], np.uint32)
+        seeds_new = seeds.copy()
+        seeds_new[slots] = seeds_for(2, tag=62)
+        Rn, Sn, pub_new = gv.sign(seeds_new, key_idx, msg, 85)
+        hit = np.isin(key_idx, slots)
+        gv.set_option(gv.OPT_FAULT_INJECT, 1)
+        with pytest.raises(PbftError):
+            gv.update_keys(slots, pub_new[slots])
+        for v in (gv, cl):
+            got, _ = verify(v, R, S, key_idx, msg, 85)
+            assert got.all()                                              # unchanged, on both contexts
+        gv.set_option(gv.OPT_FAULT_INJECT, 2)
+        with pytest.raises(PbftError):
+            gv.update_keys(slots, pub_new[slots])
+        for v in (gv, cl):
+            got, _ = verify(v, R, S, key_idx, msg, 85)
+            assert not got[hit].any() and got[~hit].all()
+            got, _ = verify(v, Rn, Sn, key_idx, msg, 85)
+            assert not got[hit].any() and got[~hit].all()
+        assert gv.update_keys(slots, pub_new[slots]).all()                 # the injection was one-shot
+        for v in (gv, cl):
+            got, _ = verify(v, Rn, Sn, key_idx, msg, 85)
+            assert got.all()
+            assert (got == oracle_bits(coracle, pub_new, Rn, Sn, key_idx, msg, 85)).all()
+        with pytest.raises(PbftError):
+            gv.set_option(gv.OPT_FAULT_INJECT, 3)
+    finally:
+        cl.close()

@@ -217,3 +217,35 @@ def test_openssl_agrees_on_its_classes(golden):
             assert (rc == 1) == bool(b["expected"][i]), (ml, i, c)
             checked += 1
     assert checked > 300
+
+
+def test_fullround_special_key_construction(coracle):
+    """tests/fullround.py (the builder of the GPU full-round parity test): a small-order key slot and a mixed-order
+    key slot in the key set; Python-built equation-valid mixed-order signatures accept and cofactored-only ones
+    reject, in both restatements (the C oracle is the GPU test's checker at 2^20 lanes)."""
+    import fullround as F
+    seeds = np.stack([np.frombuffer(bytes([i + 1]) * 32, np.uint8) for i in range(4)])
+    pub = np.stack([np.frombuffer(E.public_key(s.tobytes()), np.uint8) for s in seeds])
+    pub2, a = F.install_special_keys(seeds, pub, small_slot=2, mixed_slot=3)
+    assert not E.key_ok(pub2[2].tobytes()) and E.key_ok(pub2[3].tobytes())
+    n = 24
+    key_idx = np.array([i % 4 for i in range(n)], np.uint16)
+    msg = np.stack([np.frombuffer(b"PBFT" + bytes([1]) + (1).to_bytes(8, "little") + i.to_bytes(8, "little")
+                                  + bytes(64), np.uint8) for i in range(n)])
+    sigs = [E.sign(seeds[k].tobytes(), msg[i].tobytes()) for i, k in enumerate(key_idx)]
+    R = np.stack([np.frombuffer(s[:32], np.uint8) for s in sigs])
+    S = np.stack([np.frombuffer(s[32:], np.uint8) for s in sigs])
+    R2, S2, v, c = F.plant_mixed(R, S, key_idx, msg, 85, pub2, a, 3, n_valid=3, n_cofactored=2, seed=7)
+    assert len(v) == 3 and len(c) == 2
+    exp = np.array([E.verify_strict(pub2[k].tobytes(), R2[i].tobytes() + S2[i].tobytes(), msg[i].tobytes())
+                    for i, k in enumerate(key_idx)])
+    out = np.zeros(n, np.uint8)
+    assert coracle.oracle_verify_batch(pub2.ctypes.data, 4, R2.ctypes.data, S2.ctypes.data, key_idx.ctypes.data,
+                                       np.ascontiguousarray(msg).ctypes.data, 85, 85, n, out.ctypes.data, 2) == 0
+    assert (out.astype(bool) == exp).all()
+    assert exp[v].all() and not exp[c].any()
+    assert not exp[key_idx == 2].any()                        # small-order key: everything rejects
+    planted = np.zeros(n, bool)
+    planted[v] = planted[c] = True
+    assert not exp[(key_idx == 3) & ~planted].any()           # signatures over the old key bytes reject under A'
+    assert exp[(key_idx < 2)].all()

@@ -372,3 +372,43 @@ def test_replica_update_keys_admits_a_new_identity():
     evs = c.flush(0)
     assert (1, 1, EV_PREPARED) in evs and c.stats(0)["rejected_sig"] == 0
     c.close()
+
+
+def test_replica_update_keys_refuses_unreachable_and_keeps_duplicates():
+    """a new key that a kept slot already holds is refused (one of the two slots would be unreachable by
+    PeerId), as are two equal new keys; swapping two slots' keys in one call is allowed; a replica set created with
+    a duplicated key keeps the duplicate's other slot mapped when one of them gets a new identity."""
+    import ctypes
+    from replica_sim import seeds as mkseeds
+    c = Cluster(4)
+    L = c.L
+
+    def pid_of(k):
+        p = ctypes.create_string_buffer(38)
+        L.pbft_peer_id_from_key(k, p)
+        return p.raw
+
+    def peer_index(r, k):
+        return L.pbft_replica_peer_index(r, pid_of(k), 38)
+
+    r0 = c.reps[0]
+    k = [c.keys[32 * i: 32 * i + 32] for i in range(4)]
+    one = lambda i: (ctypes.c_uint32 * 1)(i)  # noqa: E731
+    assert L.pbft_replica_update_keys(r0, one(3), k[1], 1, None) == -1             # slot 1 keeps that key
+    fresh = ctypes.create_string_buffer(32)
+    c.o.oracle_public_key(fresh, mkseeds(1, tag=98)[0])
+    assert L.pbft_replica_update_keys(r0, (ctypes.c_uint32 * 2)(2, 3), fresh.raw * 2, 2, None) == -1  # equal new keys
+    assert L.pbft_replica_update_keys(r0, (ctypes.c_uint32 * 2)(1, 2), k[2] + k[1], 2, None) == 0    # a swap
+    assert peer_index(r0, k[1]) == 2 and peer_index(r0, k[2]) == 1
+    # duplicates at creation: slots 1 and 3 share a key (first index wins); slot 1 gets a new identity -> the
+    # shared key now resolves to slot 3, the new one to slot 1
+    dup = bytes(k[0] + k[1] + k[2] + k[1])
+    r = ctypes.c_void_p()
+    assert L.pbft_replica_create(None, 4, 0, dup, ctypes.byref(r)) == 0
+    try:
+        assert peer_index(r, k[1]) == 1
+        assert L.pbft_replica_update_keys(r, one(1), fresh.raw, 1, None) == 0
+        assert peer_index(r, k[1]) == 3 and peer_index(r, fresh.raw) == 1
+    finally:
+        L.pbft_replica_destroy(r)
+    c.close()

@@ -136,6 +136,7 @@ def test_flush_submit_of_a_2p20_round_returns_before_poll_reports_done():
     v.release = True
     assert L.pbft_replica_flush_poll(rep, ev, 8192, ctypes.byref(ne)) == 1
     evs = [(e.view, e.seq, e.kind) for e in ev[: ne.value]]
+    assert [e[:2] for e in evs] == sorted(e[:2] for e in evs)            # (view, seq) order, as delivered
     pre = {q for _, q, k in evs if k == EV_PRE_PREPARED}
     prep = {q for _, q, k in evs if k == EV_PREPARED}
     com = {q for _, q, k in evs if k == EV_COMMITTED}
@@ -375,9 +376,11 @@ def test_parallel_push_many_equals_serial_pushes():
         ev = (Event * 4096)()
         ne = ctypes.c_uint32()
         assert L.pbft_replica_flush(rep, 1, ev, 4096, ctypes.byref(ne)) == 0
-        evs[name] = sorted((e.view, e.seq, e.kind) for e in ev[: ne.value])
+        evs[name] = [(e.view, e.seq, e.kind) for e in ev[: ne.value]]
         v.keep = dfn
+    # the same events in the same order (not sorted first), and that order is (view, seq)
     assert evs["a"] == evs["b"] and stats(a) == stats(b)
+    assert [e[:2] for e in evs["a"]] == sorted(e[:2] for e in evs["a"])
     assert sum(1 for e in evs["a"] if e[2] == EV_COMMITTED) > seqs // 2
     L.pbft_replica_destroy(a)
     L.pbft_replica_destroy(b)

@@ -49,11 +49,28 @@ for k in ("comb_kernel", "finish_kernel"):
     if ns and "GRBM_GUI_ACTIVE" in m:
         out[k]["avg_ns"] = ns
         out[k]["grbm_gui_active"] = m["GRBM_GUI_ACTIVE"]
-        # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back)
+        # rocprofv3 sums GRBM_GUI_ACTIVE over the 8 XCDs (MI355X_MICROARCH.md, DVFS give-back).  The quotient
+        # "reads high on dispatches shorter than about 0.3 ms" (same section): the 131k shard's kernels gave 2.46 and
+        # 3.20 GHz, above the 2.4-GHz engine clock.  So below 0.3 ms no clock is derived
+        # from it; the in-kernel clock (s_memtime / s_memrealtime stamps, PMC_CLOCK_GHZ=<GHz>) is used when given.
         cyc = m["GRBM_GUI_ACTIVE"] / 8
-        out[k]["clock_ghz"] = cyc / ns
-        # VALU wave-instructions per SIMD per cycle (1024 SIMDs) at that clock
-        out[k]["valu_issue_per_simd_cycle"] = m["SQ_INSTS_VALU"] / 1024 / cyc
+        clk = cyc / ns
+        kclk = float(os.environ["PMC_CLOCK_GHZ"]) if os.environ.get("PMC_CLOCK_GHZ") else None
+        if ns >= 300_000 and clk <= 2.4:
+            out[k]["clock_ghz"] = clk
+            out[k]["clock_source"] = "GRBM_GUI_ACTIVE / 8 / avg duration"
+        elif kclk:
+            out[k]["clock_ghz"] = kclk
+            out[k]["clock_source"] = "in-kernel s_memtime / s_memrealtime (PMC_CLOCK_GHZ)"
+            out[k]["grbm_clock_ghz_invalid"] = clk
+        else:
+            out[k]["clock_ghz"] = None
+            out[k]["clock_source"] = (f"none: GRBM_GUI_ACTIVE / 8 / avg duration = {clk:.2f} GHz is not valid for a "
+                                      f"{ns / 1e3:.0f}-us dispatch (< 300 us, MI355X_MICROARCH.md DVFS give-back)")
+        if out[k]["clock_ghz"]:
+            c = out[k]["clock_ghz"] * ns  # cycles of the dispatch at that clock
+            # VALU wave-instructions per SIMD per cycle (1024 SIMDs) at that clock
+            out[k]["valu_issue_per_simd_cycle"] = m["SQ_INSTS_VALU"] / 1024 / c
     tot += fb + wbytes
 out["traffic_bytes_per_launch"] = tot
 out["valu_insts_per_sig_total"] = sum(out[k]["valu_insts_per_sig"] for k in ("comb_kernel", "finish_kernel"))
