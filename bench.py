@@ -142,7 +142,7 @@ def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_prof.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
-    for rel in ("r04/pmc_comb", "r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
+    for rel in ("r05/pmc_comb", "r04/pmc_comb", "r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
         p = os.path.join(ROOT, "profiles", rel, "derived.json")
         try:
             d = json.load(open(p))
@@ -324,7 +324,7 @@ def votes_device_round(v, d, msg, expect, stream, torch, dev, iters: int = 50):
             "path": "device-resident votes form: envelope-schedule kernel + comb + finish per call"}
 
 
-def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9):
+def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9, n_ctx: int = 1):
     """config #4's round through the replica state machine (include/pbft_replica.h)
     on this GPU, the way a reference replica runs it, ingest included: ONE long-lived pbft_replica (n = 256; its
     windows are recycled from round to round, as a running replica's are) receives each round's 2048 signed
@@ -334,7 +334,9 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     chunk launched as soon as it is filled) and pbft_replica_flush_poll from the loop until the bitmap is applied
     and the events are out.  Timed: push_many -> last poll (`value`), and submit -> last poll (`flush_*`).  Round r
     covers seqs r * 2048 + 1 .. (r + 1) * 2048 (every round re-signed on the GPU: new envelopes); its bitmap
-    pattern is the headline round's."""
+    pattern is the headline round's.  n_ctx > 1: pbft_replica_create_multi over the context and n_ctx - 1 clones
+    (each context stages, launches and returns its own slice of the batch; on a node they would
+    be one context per GPU, each with its own PCIe link -- here they share this GPU and its link)."""
     import ctypes
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from replica_sim import Event, Stats, lib
@@ -351,7 +353,9 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     res = {k: [] for k in ("push_ms", "submit_ms", "flush_ms", "total_ms", "polls", "apply_ms")}
     ev = (Event * 16384)()
     rep = ctypes.c_void_p()
-    assert L.pbft_replica_create(v._ctx, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+    clones = [v.clone() for _ in range(n_ctx - 1)]
+    ctxs = (ctypes.c_void_p * n_ctx)(v._ctx.value, *[c._ctx.value for c in clones])
+    assert L.pbft_replica_create_multi(ctxs, n_ctx, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
     st_prev = Stats()
     for r in range(rounds + 1):
         seq0 = 1 + r * n_seq
@@ -403,6 +407,8 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             res["apply_ms"].append((st.apply_ns - st_prev.apply_ns) * 1e-6)
         st_prev = st
     L.pbft_replica_destroy(rep)
+    for c in clones:
+        c.close()
     med = {k: float(np.median(x)) for k, x in res.items()}
     return {"value": n / (med["total_ms"] * 1e-3), "unit": "verifies/s", "ms_per_round": med["total_ms"],
             "ms_per_round_min_max": [float(np.min(res["total_ms"])), float(np.max(res["total_ms"]))],
@@ -410,7 +416,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             "flush_verifies_per_s": n / (med["flush_ms"] * 1e-3),
             "flush_submit_ms": med["submit_ms"], "apply_ms": med["apply_ms"],
             "gpu_wait_ms": max(0.0, med["flush_ms"] - med["submit_ms"] - med["apply_ms"]),  # (medians of separate series)
-            "polls_while_running": int(med["polls"]), "sigs": n + n_seq, "rounds": rounds,
+            "polls_while_running": int(med["polls"]), "sigs": n + n_seq, "rounds": rounds, "contexts": n_ctx,
             "path": "one long-lived pbft_replica: push_many (2^20 votes; + 2048 PrePrepares via on_pre_prepare, "
                     "untimed) -> flush_submit (votes form filled into pinned staging by worker threads, each 2^18-row "
                     "chunk's H2D + kernels + bitmap D2H launched as soon as it is filled) -> flush_poll loop applying "
@@ -929,6 +935,9 @@ def main():
         extras["config2"] = config2_leg(v, torch, dev, stream, cpu=not args.no_cpu)
         extras["config3"] = config3_leg(v, torch, dev, stream, cpu=not args.no_cpu)
         extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect)
+        # the same round through pbft_replica_create_multi over this context + 1 clone (one slice each; on a node the
+        # contexts would be two GPUs with a PCIe link each -- here both share this GPU and its link)
+        extras["replica_flush_2^20_2ctx"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, n_ctx=2)
         extras["shuffled_2^20"] = shuffled_leg(v, d, n, stream, torch, dev, expect)
         # the C ABI's single-process multi-GPU form on this process's one GPU (a 1-rank RCCL communicator): its
         # bitmap must equal the headline path's; unmeasured on 8 GPUs in this pipeline

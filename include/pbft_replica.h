@@ -140,6 +140,16 @@ typedef int (*pbft_digest_fn)(void *user, const uint8_t *op, uint32_t op_len, ui
  * verifier override is installed before the first flush.  The primary of view v
  * is replica v mod n (Castro-Liskov p = v mod |R|). */
 int pbft_replica_create(pbft_ctx *ctx, uint32_t n, uint32_t self_id, const uint8_t *keys, pbft_replica **out);
+/* The same replica over several verifier contexts (one per GPU of the node, or clones of one GPU's context; distinct,
+ * each with the replica key set installed; ctxs[0] also serves digests and small batches).  A flush of >= 2^16 rows
+ * is cut into one contiguous slice per context (balanced by rows, at window-phase boundaries, each slice 64-row
+ * aligned); every context stages its slice and the envelope table in its own pinned staging and launches it chunk
+ * by chunk as the worker threads fill it, so the slices' host-to-device copies run on every GPU's PCIe link at once
+ * (one replica used one GPU and one link of eight); flush_poll applies rows as each context's bitmap
+ * words land, in row order.  n_ctx <= PBFT_MAX_REPLICA_CTX.  pbft_replica_update_keys updates every context. */
+#define PBFT_MAX_REPLICA_CTX 16
+int pbft_replica_create_multi(pbft_ctx *const *ctxs, uint32_t n_ctx, uint32_t n, uint32_t self_id,
+                              const uint8_t *keys, pbft_replica **out);
 /* Replica idx[i] (< n, distinct) gets the key A[i][32] -- a peer admitted after start-up (Pbft::add_peer,
  * src/behavior.rs:45-61, fed by mDNS discovery src/network_behaviour_composer.rs:24-33): its PeerId now maps to
  * replica idx[i] (pbft_replica_peer_index) and, with a GPU context, only its comb tables are rebuilt

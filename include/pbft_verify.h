@@ -312,6 +312,18 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  * an 8-GPU round) asks for enough LDS that no CU takes more than its even share of the blocks; 0: the kernels'
  * own LDS (the dispatcher then packs up to 4 blocks on some CUs). */
 #define PBFT_OPT_COMB_SPREAD 12
+/* 1: the one-lane comb (chain form, 85-byte messages, >= 2^16 signatures) runs 8-wave blocks whose two waves per
+ * SIMD trade priorities so that they progress together (instead of oldest-first); 0: 4-wave blocks; any other
+ * value (default; env PBFT_COMB_PRIO) = by batch size: 8-wave blocks where they fit one per CU (the 131k shard). */
+#define PBFT_OPT_COMB_PRIO 13
+/* 1: the chain-form comb (85-byte messages, >= 2^16 signatures, not pipelined) runs the finish in the same launch:
+ * the last block of each group of comb blocks to finish verifies the group's signatures; 0 (default; env
+ * PBFT_COMB_FUSE): a separate finish launch. */
+#define PBFT_OPT_COMB_FUSE 14
+/* 1: 8-wave comb launches (PBFT_OPT_COMB_PRIO) stagger the two waves of a SIMD -- one hashes before its base-point
+ * positions, the other after them -- so one's latency-bound SHA-512 runs under the other's multiplications;
+ * 0 (default; env PBFT_COMB_STAGGER): both hash first. */
+#define PBFT_OPT_COMB_STAGGER 15
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

@@ -55,6 +55,9 @@ pub const PBFT_OPT_VOTES_ZERO_COPY: c_int = 9;
 pub const PBFT_OPT_COMB_PAIR: c_int = 10;
 pub const PBFT_OPT_FAULT_INJECT: c_int = 11;
 pub const PBFT_OPT_COMB_SPREAD: c_int = 12;
+pub const PBFT_OPT_COMB_PRIO: c_int = 13;
+pub const PBFT_OPT_COMB_FUSE: c_int = 14;
+pub const PBFT_OPT_COMB_STAGGER: c_int = 15;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
 pub const PBFT_KIND_PREPARE: u8 = 1;

@@ -309,7 +309,8 @@ static uint64_t now_ns() {
 
 struct pbft_replica {
   std::vector<TraceEv> trace;
-  pbft_ctx* ctx = nullptr;
+  pbft_ctx* ctx = nullptr;         // ctxs[0]: digests, small batches
+  std::vector<pbft_ctx*> ctxs;     // pbft_replica_create_multi: large batches split over these (one per GPU)
   uint32_t n = 0, f = 0, self = 0;
   uint64_t current_view = 1;  // src/view.rs:5-8: the view starts at 1 (no view change)
   uint64_t h = 0;             // low watermark: every seq <= h is done (committed prefix or checkpoint)
@@ -338,6 +339,11 @@ struct pbft_replica {
   size_t seg_next = 0;            // segments [0, seg_next) already applied (progressive completion)
   std::vector<uint8_t> touched;   // per segment: some candidate accepted
   uint64_t rows = 0;
+  uint64_t rows_span = 0;         // rows of the bitmap: rows + the padding that 64-aligns each context's slice
+  // multi-context batch: context k verifies rows [slice_lo[k], slice_lo[k + 1]) (its staged rows; the last
+  // slice_lo[k + 1] - slice_hi[k] of them padding); slice_end[k]: its rows known verified (bitmap words landed)
+  std::vector<uint64_t> slice_lo, slice_hi, slice_end;
+  std::vector<uint8_t> slice_fin;
   bool erased_in_flight = false;  // a stable checkpoint erased windows while the batch was in flight
   std::vector<uint64_t> bitmap;
   // host buffers of the verifier overrides (the GPU path fills the context's pinned staging instead)
@@ -719,13 +725,15 @@ static void finish_batch(pbft_replica* r) {
 // Copy the candidates of segments [s0, s1) into the batch: the GPU context's staged votes rows (rs =
 // PBFT_VOTES_ROW_BYTES: signature, key index and envelope index side by side, include/pbft_verify.h) or the
 // overrides' columns (rs = 0: SIG [N][64], K [N], IDX [N]).
-static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, size_t rs) {
+// (base: the batch row SIG's first row holds -- a multi-context slice's start)
+static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint16_t* K, uint32_t* IDX, size_t rs,
+                      uint64_t base = 0) {
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
     Phase& p = g.w->ph[g.kind];
     const bool one = p.digs.size() == 1;
     if (rs) {
-      uint8_t* row = SIG + rs * g.row0;
+      uint8_t* row = SIG + rs * (g.row0 - base);
 #if defined(__x86_64__)
       if (g_stream_stores) {  // streaming stores: no read-for-ownership of the staging lines (the DMA reads them next)
         for (uint32_t i = 0; i < g.count; ++i, row += rs) {
@@ -832,6 +840,138 @@ static int fill_and_launch(pbft_replica* r, size_t T, uint8_t* SIG, uint16_t* K,
   return rc;
 }
 
+// Multi-context batch (pbft_replica_create_multi): the segments are cut into one contiguous slice per context
+// (balanced by rows, at segment boundaries; each slice 64-aligned so that no bitmap word has two writers, the gap
+// padded with rows that verify as 0 and are never applied), each context stages its slice and the envelope table
+// in its own pinned staging, and the fill steps go round-robin over the contexts' chunk schedules so every GPU
+// starts on its first chunk at once.  Returns the contexts that opened a batch in *opened (to be drained on
+// failure).
+static int fill_and_launch_multi(pbft_replica* r, size_t T, uint32_t E, size_t* opened) {
+  *opened = 0;
+  const size_t G = r->segs.size();
+  const size_t K = r->slice_lo.size() - 1;
+  std::vector<size_t> sg(K + 1);  // slice k = segments [sg[k], sg[k + 1])
+  {
+    size_t gi = 0;
+    for (size_t k = 0; k <= K; ++k) {
+      while (gi < G && r->segs[gi].row0 < r->slice_lo[k]) ++gi;
+      sg[k] = k == K ? G : gi;
+    }
+  }
+  std::vector<pbft_votes_staging> st(K);
+  for (size_t k = 0; k < K; ++k) {
+    const uint64_t nk = r->slice_lo[k + 1] - r->slice_lo[k];
+    int rc = pbft_verify_votes_stage(r->ctxs[k], nk, E, &st[k]);
+    if (rc) return rc;
+    // padding rows (key 0, envelope 0, zero signature: bit 0, never applied)
+    const uint64_t real = r->slice_hi[k] - r->slice_lo[k];
+    if (nk > real) memset(st[k].sig + (size_t)st[k].row_stride * real, 0, (size_t)st[k].row_stride * (nk - real));
+  }
+  // fill steps: chunk c of every context's schedule, then chunk c + 1 ...
+  struct Step { size_t k, a, b; uint64_t launch_rows; };
+  std::vector<Step> steps;
+  {
+    std::vector<std::vector<uint64_t>> ends(K);
+    size_t W = 0;
+    for (size_t k = 0; k < K; ++k) {
+      const uint64_t nk = r->slice_lo[k + 1] - r->slice_lo[k];
+      for (uint64_t lo = 0; lo < nk; lo = PBFT_VOTES_CHUNK_END(lo, nk)) ends[k].push_back(PBFT_VOTES_CHUNK_END(lo, nk));
+      W = std::max(W, ends[k].size());
+    }
+    std::vector<size_t> next(K);
+    for (size_t k = 0; k < K; ++k) next[k] = sg[k];
+    for (size_t c = 0; c < W; ++c)
+      for (size_t k = 0; k < K; ++k) {
+        if (c >= ends[k].size()) continue;
+        const uint64_t nk = r->slice_lo[k + 1] - r->slice_lo[k];
+        const uint64_t end_abs = r->slice_lo[k] + ends[k][c];
+        size_t b = next[k];
+        if (c + 1 == ends[k].size()) b = sg[k + 1];
+        else while (b < sg[k + 1] && r->segs[b].row0 < end_abs) ++b;
+        const uint64_t launch = b < sg[k + 1] ? r->segs[b].row0 - r->slice_lo[k] : nk;
+        steps.push_back({k, next[k], b, launch});
+        next[k] = b;
+      }
+  }
+  const size_t S = steps.size();
+  std::unique_ptr<std::atomic<uint32_t>[]> done(new std::atomic<uint32_t>[S]);
+  for (size_t q = 0; q < S; ++q) done[q].store(0, std::memory_order_relaxed);
+  std::atomic<uint32_t> envs_done{0};
+  auto first_at = [&](uint64_t row) {
+    return (size_t)(std::lower_bound(r->segs.begin(), r->segs.end(), row,
+                                     [](const Seg& g, uint64_t x) { return g.row0 < x; }) - r->segs.begin());
+  };
+  uint8_t* const env0 = st[0].envelopes;
+  WorkerPool::get().start(T, [&](size_t t) {
+    fill_envs(r, G * t / T, G * (t + 1) / T, env0);
+    envs_done.fetch_add(1, std::memory_order_release);
+    for (size_t q = 0; q < S; ++q) {
+      const Step& sp = steps[q];
+      if (sp.b > sp.a) {  // part t of the step, balanced by rows
+        const uint64_t lo = r->segs[sp.a].row0, hi = r->segs[sp.b - 1].row0 + r->segs[sp.b - 1].count;
+        const size_t x = t == 0 ? sp.a : std::max(sp.a, first_at(lo + (hi - lo) * t / T));
+        const size_t y = t + 1 == T ? sp.b : std::min(sp.b, first_at(lo + (hi - lo) * (t + 1) / T));
+        const size_t rs = st[sp.k].row_stride;
+        // rows addressed from the slice's start: row0 - slice_lo[k] in context k's staging
+        if (y > x) fill_rows(r, x, y, st[sp.k].sig, nullptr, nullptr, rs, r->slice_lo[sp.k]);
+      }
+      fill_fence();
+      done[q].fetch_add(1, std::memory_order_release);
+    }
+  });
+  while (envs_done.load(std::memory_order_acquire) < T) std::this_thread::yield();
+  for (size_t k = 1; k < K; ++k) memcpy(st[k].envelopes, env0, (size_t)PBFT_ENVELOPE_BYTES * E);
+  RTRACE(r, "envs", E);
+  int rc = PBFT_OK;
+  for (size_t k = 0; k < K && rc == PBFT_OK; ++k) {
+    rc = pbft_verify_votes_submit_begin(r->ctxs[k], r->slice_lo[k + 1] - r->slice_lo[k], E,
+                                        r->bitmap.data() + r->slice_lo[k] / 64);
+    if (rc == PBFT_OK) *opened = k + 1;
+  }
+  RTRACE(r, "begin", r->rows_span);
+  for (size_t q = 0; q < S && rc == PBFT_OK; ++q) {
+    while (done[q].load(std::memory_order_acquire) < T) std::this_thread::yield();
+    rc = pbft_verify_votes_submit_rows(r->ctxs[steps[q].k], steps[q].launch_rows);
+    RTRACE(r, "launched", q);
+  }
+  WorkerPool::get().wait();
+  return rc;
+}
+
+// Cut the batch's segments into one slice per context (balanced by rows, at segment boundaries) and renumber the
+// rows so that every slice starts 64-aligned; false if fewer than two non-empty slices result.
+static bool plan_slices(pbft_replica* r) {
+  const size_t G = r->segs.size(), K = r->ctxs.size();
+  const uint64_t N = r->rows;
+  std::vector<size_t> cut{0};
+  for (size_t k = 1; k < K; ++k) {
+    const uint64_t target = N * k / K;
+    size_t b = cut.back();
+    while (b < G && r->segs[b].row0 < target) ++b;
+    if (b > cut.back() && b < G) cut.push_back(b);
+  }
+  cut.push_back(G);
+  if (cut.size() < 3) return false;
+  const size_t S = cut.size() - 1;
+  r->slice_lo.assign(S + 1, 0);
+  r->slice_hi.assign(S, 0);
+  uint64_t shift = 0;
+  for (size_t k = 0; k < S; ++k) {
+    const uint64_t old_lo = r->segs[cut[k]].row0;
+    const uint64_t lo = k == 0 ? 0 : (old_lo + shift + 63) / 64 * 64;
+    shift = lo - old_lo;
+    for (size_t gi = cut[k]; gi < cut[k + 1]; ++gi) r->segs[gi].row0 += shift;
+    r->slice_lo[k] = lo;
+    r->slice_hi[k] = r->segs[cut[k + 1] - 1].row0 + r->segs[cut[k + 1] - 1].count;
+  }
+  for (size_t k = 0; k + 1 < S; ++k) r->slice_lo[k + 1] = std::max(r->slice_lo[k + 1], r->slice_hi[k]);
+  r->slice_lo[S] = r->slice_hi[S - 1];
+  r->rows_span = r->slice_lo[S];
+  r->slice_end.assign(S, 0);
+  r->slice_fin.assign(S, 0);
+  return true;
+}
+
 extern "C" {
 
 void pbft_envelope(uint8_t out[PBFT_ENVELOPE_BYTES], uint8_t kind, uint64_t view, uint64_t seq,
@@ -844,9 +984,21 @@ void pbft_envelope(uint8_t out[PBFT_ENVELOPE_BYTES], uint8_t kind, uint64_t view
 }
 
 int pbft_replica_create(pbft_ctx* ctx, uint32_t n, uint32_t self_id, const uint8_t* keys, pbft_replica** out) {
-  if (!out || !keys || n < 1 || n > 65535 || self_id >= n) return PBFT_EINVAL;
+  return pbft_replica_create_multi(ctx ? &ctx : nullptr, ctx ? 1 : 0, n, self_id, keys, out);
+}
+
+int pbft_replica_create_multi(pbft_ctx* const* ctxs, uint32_t n_ctx, uint32_t n, uint32_t self_id,
+                              const uint8_t* keys, pbft_replica** out) {
+  if (!out || !keys || n < 1 || n > 65535 || self_id >= n || n_ctx > PBFT_MAX_REPLICA_CTX || (n_ctx && !ctxs))
+    return PBFT_EINVAL;
+  for (uint32_t k = 0; k < n_ctx; ++k) {
+    if (!ctxs[k]) return PBFT_EINVAL;
+    for (uint32_t j = 0; j < k; ++j)
+      if (ctxs[j] == ctxs[k]) return PBFT_EINVAL;  // one batch in flight per context: distinct contexts
+  }
   pbft_replica* r = new pbft_replica();
-  r->ctx = ctx;
+  r->ctxs.assign(ctxs, ctxs + n_ctx);
+  r->ctx = n_ctx ? ctxs[0] : nullptr;
   r->n = n;
   r->f = (n - 1) / 3;
   r->self = self_id;
@@ -873,8 +1025,10 @@ int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t
     if (it != r->key_index.end() && it->second != idx[i] && !replaced(it->second)) return PBFT_EINVAL;
   }
   if (r->ctx && m) {
-    const int rc = pbft_verify_update_keys(r->ctx, idx, A, m, key_ok);
-    if (rc) return rc;
+    for (size_t k = 0; k < r->ctxs.size(); ++k) {  // every GPU's key set (a clone listed twice: rebuilt twice)
+      const int rc = pbft_verify_update_keys(r->ctxs[k], idx, A, m, key_ok);
+      if (rc) return rc;
+    }
   } else if (key_ok) {
     memset(key_ok, 1, m);  // (no GPU context: the installed verifier override judges the keys)
   }
@@ -900,7 +1054,14 @@ int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t
 
 int pbft_replica_destroy(pbft_replica* r) {
   if (!r) return PBFT_OK;
-  if (r->in_flight && r->in_flight_via == 0 && r->ctx) (void)pbft_verify_wait(r->ctx);
+  if (r->in_flight && r->in_flight_via == 0) {
+    if (!r->slice_lo.empty()) {
+      for (size_t k = 0; k < r->slice_fin.size(); ++k)
+        if (!r->slice_fin[k]) (void)pbft_verify_wait(r->ctxs[k]);
+    } else if (r->ctx) {
+      (void)pbft_verify_wait(r->ctx);
+    }
+  }
   if (r->in_flight && r->in_flight_via == 1 && r->vpoll)
     while (r->vpoll(r->vuser) == 0) std::this_thread::yield();
   delete r;
@@ -1173,10 +1334,15 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     }
   }
   r->rows = N;
+  r->rows_span = N;
+  r->slice_lo.clear();
   RTRACE(r, "segs", r->segs.size());
   if (n_rows) *n_rows = N;
   if (N == 0) { r->segs.clear(); return PBFT_OK; }
-  r->bitmap.assign((N + 63) / 64, 0);
+  // several contexts (pbft_replica_create_multi) and a batch large enough for the threaded fill: one slice each
+  const bool multi = r->ctxs.size() > 1 && !r->verify_fn && !r->vsub && N >= (1u << 16) && plan_slices(r);
+  if (!multi) r->slice_lo.clear();
+  r->bitmap.assign((r->rows_span + 63) / 64, 0);
   // 2. fill the batch: the GPU context's pinned staging (zero-copy votes form) or the overrides' buffers; large
   //    batches with several threads (a memcpy per phase: the replica's side is memory-bound)
   int rc = PBFT_OK;
@@ -1184,6 +1350,23 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   uint16_t* K;
   uint32_t* IDX;
   size_t rs = 0;  // staged rows' stride (0: the overrides' columns)
+  if (multi) {
+    const size_t G = r->segs.size();
+    r->touched.assign(G, 0);
+    r->seg_next = 0;
+    const unsigned hw = std::thread::hardware_concurrency();
+    const size_t T = std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), G);
+    size_t opened = 0;
+    rc = fill_and_launch_multi(r, T < 1 ? 1 : T, E, &opened);
+    r->in_flight_via = 0;
+    if (rc) {  // drain what was opened (its kernels write this batch's bitmap), then the candidates are pending again
+      for (size_t k = 0; k < opened; ++k) (void)pbft_verify_wait(r->ctxs[k]);
+      revert_segs(r);
+      return rc;
+    }
+    r->in_flight = true;
+    return PBFT_OK;
+  }
   if (r->verify_fn || r->vsub) {
     r->hSig.resize(64 * N); r->hK.resize(N); r->hI.resize(N);
     r->hE.assign(PBFT_ENVELOPE_BYTES * (size_t)E + 16, 0);
@@ -1256,15 +1439,40 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
   if (r->in_flight) {
     int st = 1;
     uint64_t rows_done = 0;
-    if (r->in_flight_via == 0) st = pbft_verify_poll_rows(r->ctx, &rows_done);
-    else if (r->in_flight_via == 1) st = r->vpoll(r->vuser);
+    if (r->in_flight_via == 0 && !r->slice_lo.empty()) {
+      // multi-context batch: the prefix of rows known verified -- slice by slice, each context's own prefix
+      const size_t S = r->slice_end.size();
+      for (size_t k = 0; k < S; ++k) {
+        if (r->slice_fin[k]) continue;
+        uint64_t d = 0;
+        const int sk = pbft_verify_poll_rows(r->ctxs[k], &d);
+        if (sk < 0) {
+          for (size_t j = 0; j < S; ++j)
+            if (j != k && !r->slice_fin[j]) (void)pbft_verify_wait(r->ctxs[j]);
+          revert_segs(r);
+          return sk;
+        }
+        r->slice_end[k] = r->slice_lo[k] + std::min<uint64_t>(d, r->slice_lo[k + 1] - r->slice_lo[k]);
+        if (sk == 1) r->slice_fin[k] = 1, r->slice_end[k] = r->slice_lo[k + 1];
+      }
+      st = 1;
+      rows_done = 0;
+      for (size_t k = 0; k < S; ++k) {
+        rows_done = r->slice_end[k];
+        if (!r->slice_fin[k]) { st = 0; break; }
+      }
+    } else if (r->in_flight_via == 0) {
+      st = pbft_verify_poll_rows(r->ctx, &rows_done);
+    } else if (r->in_flight_via == 1) {
+      st = r->vpoll(r->vuser);
+    }
     if (st < 0) { revert_segs(r); return st; }
     const auto t0 = std::chrono::steady_clock::now();
     if (st == 0) {
       // a large batch comes back chunk by chunk: apply the segments whose rows are all in while the GPU runs on
       // (a window's segments stay in order: a prefix of the batch)
       const size_t G = r->segs.size();
-      if (rows_done >= (r->seg_next < G ? r->segs[r->seg_next].row0 : r->rows) + (1u << 16)) {
+      if (rows_done >= (r->seg_next < G ? r->segs[r->seg_next].row0 : r->rows_span) + (1u << 16)) {
         RTRACE(r, "landed", rows_done);
         size_t s1 = r->seg_next;
         while (s1 < G && r->segs[s1].row0 + r->segs[s1].count <= rows_done) ++s1;
@@ -1303,7 +1511,7 @@ int pbft_replica_flush(pbft_replica* r, int force, pbft_round_event* events, uin
   if (n_events) *n_events = 0;
   // a batch submitted earlier completes first (its events are queued, not lost)
   while (r->in_flight) {
-    if (r->in_flight_via == 0) {
+    if (r->in_flight_via == 0 && r->slice_lo.empty()) {
       const int w = pbft_verify_wait(r->ctx);
       if (w < 0) { revert_segs(r); return w; }
     }
@@ -1314,7 +1522,7 @@ int pbft_replica_flush(pbft_replica* r, int force, pbft_round_event* events, uin
   int rc = pbft_replica_flush_submit(r, force, nullptr);
   if (rc) return rc;
   for (;;) {
-    if (r->in_flight && r->in_flight_via == 0) {
+    if (r->in_flight && r->in_flight_via == 0 && r->slice_lo.empty()) {  // (a multi-context batch: polled)
       const int w = pbft_verify_wait(r->ctx);
       if (w < 0) { revert_segs(r); return w; }
     }

@@ -161,6 +161,11 @@ struct pbft_ctx {
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   int comb_pair = -1;                  // comb_pair_kernel: 1 on, 0 off, -1 by batch size (PBFT_OPT_COMB_PAIR)
   int comb_spread = 1;                 // even block placement of one-generation comb launches (PBFT_OPT_COMB_SPREAD)
+  int comb_prio = -1;                  // 8-wave comb blocks with paired wave priorities: 1, 0, -1 by batch size
+                                       // (PBFT_OPT_COMB_PRIO)
+  int comb_stagger = 0;                // 8-wave comb launches stagger their waves' hashes (PBFT_OPT_COMB_STAGGER)
+  int comb_fuse = 0;                   // the finish inside the chain-form comb launch: 1, 0, -1 by size
+                                       // (PBFT_OPT_COMB_FUSE)
   int cus = 0;                         // compute units of the device
   bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
@@ -424,7 +429,7 @@ static_assert(steps<PLB, PLA_SMALL>::N >= steps<PLB, PLA_MID>::N && steps<PLB, P
               "");
 static inline size_t eidx_offset(uint64_t N) { return (121 * (size_t)N + 255) & ~(size_t)255; }
 static inline size_t eidx_bytes(uint64_t N) {
-  const uint64_t Npad = (N + BLOCK - 1) / BLOCK * BLOCK;
+  const uint64_t Npad = (N + 2 * BLOCK - 1) / (2 * BLOCK) * (2 * BLOCK);  // (8-wave comb blocks: PBFT_OPT_COMB_PRIO)
   // (latency mode: 4 or 8 lanes per signature, 8-byte entry addresses, ceil(steps / lanes) per lane)
   const size_t split4 = 8 * (size_t)((MAX_STEPS + 3) / 4) * (Npad * 4 + BLOCK);
   const size_t split8 = 8 * (size_t)((MAX_STEPS + 7) / 8) * (Npad * 8 + BLOCK);
@@ -462,13 +467,17 @@ static inline size_t half1_offset(uint64_t N) { return eidx_offset(N) + eidx_byt
 static inline size_t rcopy_offset(uint64_t W, bool two) {
   return ((two ? half1_offset(W) + eidx_offset(W) : half1_offset(W)) + 255) & ~(size_t)255;
 }
+// the fused comb's per-group arrival counters (comb_kernel<..., FG>: zero between launches -- zeroed here when the
+// workspace is allocated, and by the last arriver of each group in every launch), after the R copy
+static inline size_t ctr_offset(uint64_t W, bool two) { return (rcopy_offset(W, two) + 32 * (size_t)W + 255) & ~(size_t)255; }
+static inline size_t ctr_bytes(uint64_t W) { return 4 * ((W + BLOCK - 1) / BLOCK + 64); }
 // The layout is a function of c->work_n only, never of the batch at hand: a smaller batch must not move
 // the entry-index region onto the xyz/flags half a pipelined finish may still be reading.
 static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   if (N <= c->work_n && (!two_halves || c->work_two)) return PBFT_OK;
   const uint64_t W = N > c->work_n ? N : c->work_n;
   const bool two = two_halves || c->work_two;
-  const size_t need = rcopy_offset(W, two) + 32 * (size_t)W + 256;
+  const size_t need = ctr_offset(W, two) + ctr_bytes(W);
   // nothing may still read the old workspace: the finishes of earlier pipelined launches, then this stream
   for (int h = 0; h < 2; ++h)
     if (c->fin_pending[h]) { HIP_TRY(hipEventSynchronize(c->ev_fin[h])); c->fin_pending[h] = false; }
@@ -480,6 +489,7 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   c->work_n = 0;
   c->work_two = false;
   if (hipMalloc(&c->d_work, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
+  HIP_TRY(hipMemset(c->d_work + ctr_offset(W, two), 0, ctr_bytes(W)));
   c->work_cap = need;
   c->work_n = W;
   c->work_two = two;
@@ -490,7 +500,7 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
 static int ensure_work2(pbft_ctx* c, uint64_t N) {
   if (N <= c->work2_n) return PBFT_OK;
   const uint64_t W = N;
-  const size_t need = rcopy_offset(W, false) + 32 * (size_t)W + 256;
+  const size_t need = ctr_offset(W, false) + ctr_bytes(W);
   if (c->d_work2) {
     HIP_TRY(hipStreamSynchronize(c->stream2));
     HIP_TRY(hipFree(c->d_work2));
@@ -499,6 +509,7 @@ static int ensure_work2(pbft_ctx* c, uint64_t N) {
   c->work2_cap = 0;
   c->work2_n = 0;
   if (hipMalloc(&c->d_work2, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
+  HIP_TRY(hipMemset(c->d_work2 + ctr_offset(W, false), 0, ctr_bytes(W)));
   c->work2_cap = need;
   c->work2_n = W;
   return PBFT_OK;
@@ -541,6 +552,11 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.pair = c->comb_pair;
   a.cus = c->cus;
   a.spread = c->comb_spread;
+  a.prio = c->comb_prio;
+  // the finish inside the comb launch: not in the pipelined form (its finish runs on the second stream)
+  a.fuse = fst ? 0 : c->comb_fuse;
+  a.stagger = c->comb_stagger;
+  a.group_ctr = (uint32_t*)(wbase + ctr_offset(W, wtwo));
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
   // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
   if (r_host && !latency_mode) a.r_copy = (uint32_t*)(wbase + rcopy_offset(W, wtwo));
@@ -557,7 +573,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     HIP_TRY(hipStreamWaitEvent(fst, c->ev_comb, 0));
     st = fst;
   }
-  if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
+  if (!latency_mode && !comb_fused(a)) {  // (the latency kernel, and the fused comb, write the bitmap themselves)
     // signatures per finish lane, product tree and waves per SIMD by batch size (PBFT_FIN_* above)
     const bool big = N >= ((uint64_t)1 << 19);
     int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID
@@ -945,6 +961,15 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   c->device = device;
   c->cus = prop.multiProcessorCount;
   if (const char* e = getenv("PBFT_COMB_SPREAD")) c->comb_spread = strtol(e, nullptr, 10) != 0;
+  if (const char* e = getenv("PBFT_COMB_STAGGER")) c->comb_stagger = strtol(e, nullptr, 10) != 0;
+  if (const char* e = getenv("PBFT_COMB_FUSE")) {
+    const long v = strtol(e, nullptr, 10);
+    c->comb_fuse = (v == 0 || v == 1) ? (int)v : -1;
+  }
+  if (const char* e = getenv("PBFT_COMB_PRIO")) {
+    const long v = strtol(e, nullptr, 10);
+    c->comb_prio = (v == 0 || v == 1) ? (int)v : -1;
+  }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
   if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
@@ -1206,6 +1231,9 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->two_streams = parent->two_streams;
   c->comb_pair = parent->comb_pair;
   c->comb_spread = parent->comb_spread;
+  c->comb_prio = parent->comb_prio;
+  c->comb_fuse = parent->comb_fuse;
+  c->comb_stagger = parent->comb_stagger;
   c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
@@ -1826,6 +1854,9 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
     case PBFT_OPT_COMB_PAIR: c->comb_pair = value <= 1 ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
     case PBFT_OPT_COMB_SPREAD: c->comb_spread = value != 0; return PBFT_OK;
+    case PBFT_OPT_COMB_PRIO: c->comb_prio = value <= 1 ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_COMB_FUSE: c->comb_fuse = value <= 1 ? (int)value : -1; return PBFT_OK;
+    case PBFT_OPT_COMB_STAGGER: c->comb_stagger = value != 0; return PBFT_OK;
     case PBFT_OPT_FAULT_INJECT:
       if (value > 2) return set_err(PBFT_EINVAL, "fault injection point");
       c->fault_inject = (int)value;

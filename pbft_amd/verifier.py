@@ -296,6 +296,9 @@ class GpuBatchVerifier:
     OPT_COMB_PAIR = 10
     OPT_FAULT_INJECT = 11
     OPT_COMB_SPREAD = 12
+    OPT_COMB_PRIO = 13
+    OPT_COMB_FUSE = 14
+    OPT_COMB_STAGGER = 15
 
     def set_option(self, option: int, value: int) -> None:
         """pbft_verify_set_option: latency-mode threshold, finish width, key-table budget (include/pbft_verify.h)."""

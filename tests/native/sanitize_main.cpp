@@ -62,6 +62,7 @@ struct FakeGpu {
   uint64_t* out = nullptr;
   bool staged = false, open = false, in_flight = false;
   uint64_t batches = 0, chunk_launches = 0;
+  uint32_t lag = 1, polls = 0;  // polls per chunk landing (3 contexts: each slice is one chunk of the schedule)
 };
 
 extern "C" {
@@ -100,7 +101,7 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
 int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   FakeGpu* g = (FakeGpu*)c;
   if (!g->in_flight) { *rows_done = g->N; return 1; }
-  if (g->done < g->launched) {  // one more chunk "lands"
+  if (g->done < g->launched && ++g->polls % g->lag == 0) {  // one more chunk "lands"
     const uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
     for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
     for (uint64_t i = g->done; i < hi; ++i)
@@ -574,14 +575,17 @@ static void test_replica_async(const Keys& k) {
 
 // ---- 5. a large round through the GPU path (fake context above): the multithreaded fill launching chunk by
 // chunk, and the application of each chunk's rows while later chunks are "running" ------------------------------
-static void test_replica_progressive() {
+// n_ctx > 1: pbft_replica_create_multi over that many fake contexts (one slice of the batch each)
+static void test_replica_progressive(uint32_t n_ctx) {
   const uint32_t n = 256, seqs = 1100;  // 2 x 256 x 1100 + 1100 = 564,300 rows: 3 chunks
   std::vector<uint8_t> keys(32 * (size_t)n);
   for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = (uint8_t)(i >> 8); }
-  FakeGpu g;
-  g.n_keys = n;
+  std::vector<FakeGpu> gs(n_ctx);
+  std::vector<pbft_ctx*> cs(n_ctx);
+  for (uint32_t k = 0; k < n_ctx; ++k) { gs[k].n_keys = n; gs[k].lag = n_ctx > 1 ? 3 : 1; cs[k] = (pbft_ctx*)&gs[k]; }
+  FakeGpu& g = gs[0];
   pbft_replica* r = nullptr;
-  CHECK(pbft_replica_create((pbft_ctx*)&g, n, 0, keys.data(), &r) == 0);
+  CHECK(pbft_replica_create_multi(cs.data(), n_ctx, n, 0, keys.data(), &r) == 0);
   pbft_replica_set_digest_fn(r, host_digest, nullptr);
   pbft_replica_set_log_window(r, 4096);
   const char op[] = "testOperation";
@@ -605,7 +609,12 @@ static void test_replica_progressive() {
       }
   uint64_t rows = 0;
   CHECK(pbft_replica_flush_submit(r, 0, &rows) == 0 && rows == pushed + seqs);
-  CHECK(g.chunk_launches >= 2);  // launched in steps, not in one go
+  uint64_t staged = 0;
+  for (const FakeGpu& x : gs) {
+    CHECK(x.batches == 1 && x.chunk_launches >= (n_ctx > 1 ? 1u : 2u));  // every slice launched, in steps
+    staged += x.N;
+  }
+  CHECK(staged >= rows && staged < rows + 64 * n_ctx);  // + the padding that 64-aligns each slice
   std::vector<pbft_round_event> ev(4 * seqs);
   uint32_t ne = 0;
   int polls = 0, st;
@@ -633,8 +642,8 @@ static void test_replica_progressive() {
   pbft_replica_get_stats(r, &s);
   CHECK(s.batches == 1 && s.accepted + s.rejected_sig <= pushed + seqs);
   pbft_replica_destroy(r);
-  printf("replica progressive: %llu rows in %llu launch steps, %d polls, %u commits\n", (unsigned long long)rows,
-         (unsigned long long)g.chunk_launches, polls, committed);
+  printf("replica progressive (%u contexts): %llu rows in %llu launch steps on context 0, %d polls, %u commits\n",
+         n_ctx, (unsigned long long)rows, (unsigned long long)g.chunk_launches, polls, committed);
 }
 
 int main() {
@@ -644,7 +653,8 @@ int main() {
   test_wire(rng);
   test_replica(k, rng);
   test_replica_async(k);
-  test_replica_progressive();
+  test_replica_progressive(1);
+  test_replica_progressive(3);
   printf("sanitized host run ok\n");
   return 0;
 }

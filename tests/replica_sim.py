@@ -41,6 +41,8 @@ def lib():
     L = pbft_amd.load()
     vp = ctypes.c_void_p
     L.pbft_replica_create.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p, ctypes.POINTER(vp)]
+    L.pbft_replica_create_multi.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_char_p,
+                                            ctypes.POINTER(vp)]
     L.pbft_replica_destroy.argtypes = [vp]
     L.pbft_replica_update_keys.argtypes = [vp, vp, ctypes.c_char_p, ctypes.c_uint32, vp]
     L.pbft_replica_set_verifier.argtypes = [vp, VERIFY_FN, vp]

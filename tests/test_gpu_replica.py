@@ -107,10 +107,14 @@ def test_gpu_phase_ordered_rounds_async_flush(gpu_cluster):
     c.close()
 
 
-def test_gpu_replica_2p20_round(gpu_cluster):
+@pytest.mark.parametrize("n_ctx", [1, 3])
+def test_gpu_replica_2p20_round(gpu_cluster, n_ctx):
     """Config #4's round through one replica on the GPU: n = 256, 2048 seqs, 2^20 GPU-signed votes + 2048
     PrePrepares pushed, ONE flush_submit (votes form into the pinned staging), polled to completion; the windows
-    whose quorum was broken by corrupted votes neither prepare nor commit, every other one commits."""
+    whose quorum was broken by corrupted votes neither prepare nor commit, every other one commits.  n_ctx = 3:
+    pbft_replica_create_multi over the context and two clones (a slice of the batch per context,
+    each staged, launched and applied on its own -- one GPU here, one per GPU on a node): the same events and
+    counters."""
     import ctypes
     import hashlib
     import time
@@ -142,7 +146,9 @@ def test_gpu_replica_2p20_round(gpu_cluster):
           ((seq == 9) & (kind == KIND_COMMIT) & (signer < 90)) | (np.arange(N) % 997 == 5)
     sigs[bad, 40] ^= 1
     rep = ctypes.c_void_p()
-    assert L.pbft_replica_create(v._ctx, n, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+    clones = [v.clone() for _ in range(n_ctx - 1)]        # (after set_keys: clones share the installed key set)
+    ctxs = (ctypes.c_void_p * n_ctx)(v._ctx.value, *[c._ctx.value for c in clones])
+    assert L.pbft_replica_create_multi(ctxs, n_ctx, n, 0, pub.tobytes(), ctypes.byref(rep)) == 0
     from replica_sim import DIGEST_FN
     dfn = DIGEST_FN(lambda u, op, ln, out: ctypes.memmove(out, hashlib.blake2b(ctypes.string_at(op, ln),
                                                                                 digest_size=64).digest(), 64) and 0)
@@ -180,5 +186,9 @@ def test_gpu_replica_2p20_round(gpu_cluster):
     st = Stats()
     L.pbft_replica_get_stats(rep, ctypes.byref(st))
     assert st.rejected_sig == int(bad.sum()) and st.accepted == N + seqs - int(bad.sum())
+    assert st.verified == N + seqs and st.batches == 1
     L.pbft_replica_destroy(rep)
-    print(f"replica 2^20: submit {(t1 - t0) * 1e3:.1f} ms, submit->done {(t2 - t0) * 1e3:.1f} ms, {polls} polls")
+    for c in clones:
+        c.close()
+    print(f"replica 2^20 ({n_ctx} contexts): submit {(t1 - t0) * 1e3:.1f} ms, submit->done {(t2 - t0) * 1e3:.1f} ms, "
+          f"{polls} polls")

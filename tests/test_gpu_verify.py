@@ -208,6 +208,46 @@ def test_comb_pair_matches_oracle(gv, coracle):
         gv.set_option(gv.OPT_COMB_PAIR, 2)
 
 
+def test_comb_fuse_and_prio_match_oracle(gv, coracle):
+    """r05 comb variants, forced on and off and by size, against the oracle's bits: PBFT_OPT_COMB_STAGGER (the two
+    waves of a SIMD hash at opposite ends of their base-point steps), PBFT_OPT_COMB_PRIO (8-wave blocks
+    whose SIMD-sharing waves trade priorities), PBFT_OPT_COMB_FUSE (the finish inside the comb launch: the last block
+    of each group verifies the group, after agent-scope hand-off of the others' R'), PBFT_OPT_COMB_SPREAD (LDS-capped
+    placement) -- at the 131k shard, ragged sizes whose last group / block is partial, and a size with several
+    generations of blocks; the pair comb forced off so that the chain form runs below its threshold too."""
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 2100, tag=7)         # 268,800 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(7)
+    R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
+    assert not exp[idx].any()
+    try:
+        gv.set_option(gv.OPT_COMB_PAIR, 0)
+        for n in (131072, 65536 + 63, 131072 - 256 - 5, 200_003, len(R2)):
+            for fuse, prio, spread, stagger in ((2, 2, 1, 0), (1, 2, 1, 0), (1, 1, 1, 0), (1, 0, 0, 0), (0, 1, 1, 0),
+                                                (0, 0, 0, 0), (0, 1, 1, 1), (0, 2, 1, 1)):
+                gv.set_option(gv.OPT_COMB_FUSE, fuse)
+                gv.set_option(gv.OPT_COMB_PRIO, prio)
+                gv.set_option(gv.OPT_COMB_SPREAD, spread)
+                gv.set_option(gv.OPT_COMB_STAGGER, stagger)
+                got, bm = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
+                assert (got == exp[:n]).all(), (n, fuse, prio, spread, stagger, np.nonzero(got != exp[:n])[0][:10])
+                if n % 64:
+                    assert int(bm[-1]) >> (n % 64) == 0
+            # twice in a row with the fused forms: the group counters were reset by the first launch
+            for prio in (0, 1):
+                gv.set_option(gv.OPT_COMB_FUSE, 1)
+                gv.set_option(gv.OPT_COMB_PRIO, prio)
+                got, _ = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
+                assert (got == exp[:n]).all(), (n, "repeat", prio)
+    finally:
+        gv.set_option(gv.OPT_COMB_PAIR, 2)
+        gv.set_option(gv.OPT_COMB_FUSE, 2)
+        gv.set_option(gv.OPT_COMB_PRIO, 2)
+        gv.set_option(gv.OPT_COMB_SPREAD, 1)
+        gv.set_option(gv.OPT_COMB_STAGGER, 0)
+
+
 def test_config4_full_size_properties(gv, coracle):
     """2^20 signatures (BASELINE configs[3] round): size-independent properties + oracle checksum."""
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 256, 2048, tag=4)
