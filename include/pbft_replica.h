@@ -201,7 +201,7 @@ int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, con
                            const uint8_t *digests, const uint32_t *signer, const uint8_t *sigs, uint64_t *queued);
 
 /* Ingress straight from one connection's byte stream (include/pbft_wire.h):
- * decode UviBytes frames (src/protocol_config.rs:50-76 upgrade_inbound); signed
+ * decode UviBytes frames (src/protocol_config.rs:49-69 upgrade_inbound); signed
  * Prepare / Commit frames whose "replica" equals peer_idx (the authenticated
  * connection) are pushed, signed PrePrepare frames go to on_pre_prepare (their
  * signature must be the view's primary's), everything else is counted in

@@ -5,13 +5,13 @@
  *
  * Reference interfaces mirrored (ameya-deshmukh/pbft):
  *   pbft_uvi_encode / pbft_uvi_decode  unsigned-varint length prefix of the
- *       UviBytes framing (src/protocol_config.rs:58, :88 `UviBytes::default()`,
+ *       UviBytes framing (src/protocol_config.rs:51, :82 `UviBytes::default()`,
  *       unsigned-varint crate; max frame 128 MiB as its codec default)
- *   pbft_wire_encode_json              message_to_json src/protocol_config.rs:121-129
+ *   pbft_wire_encode_json              message_to_json src/protocol_config.rs:116-123
  *       = serde_json::to_string of the externally tagged `Message` enum
  *       (src/message.rs:7-31; structs :34-38, :105-115, :174-179, :214-219):
  *         {"Prepare":{"view":1,"sequence_number":2,"digest":"<128 hex>"}}
- *   pbft_wire_decode_json              bytes_to_message src/protocol_config.rs:131-135
+ *   pbft_wire_decode_json              bytes_to_message src/protocol_config.rs:125-129
  *       -> `impl From<Vec<u8>> for Message` (src/message.rs:15-19), which panics
  *       on bad input; here an error code is returned instead.
  *   pbft_wire_decode_votes             the ingress path PbftHandler ->

@@ -58,6 +58,7 @@ pub const PBFT_OPT_COMB_SPREAD: c_int = 12;
 pub const PBFT_OPT_COMB_PRIO: c_int = 13;
 pub const PBFT_OPT_COMB_FUSE: c_int = 14;
 pub const PBFT_OPT_COMB_STAGGER: c_int = 15;
+pub const PBFT_MAX_REPLICA_CTX: u32 = 16;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
 pub const PBFT_KIND_PREPARE: u8 = 1;
@@ -218,6 +219,8 @@ extern "C" {
     // ---- include/pbft_replica.h
     pub fn pbft_replica_create(ctx: *mut pbft_ctx, n: u32, self_id: u32, keys: *const u8,
                                out: *mut *mut pbft_replica) -> c_int;
+    pub fn pbft_replica_create_multi(ctxs: *const *mut pbft_ctx, n_ctx: u32, n: u32, self_id: u32, keys: *const u8,
+                                     out: *mut *mut pbft_replica) -> c_int;
     pub fn pbft_replica_destroy(r: *mut pbft_replica) -> c_int;
     pub fn pbft_replica_update_keys(r: *mut pbft_replica, idx: *const u32, a: *const u8, m: u32,
                                     key_ok: *mut u8) -> c_int;

@@ -8,7 +8,10 @@
 //! * [`GpuVerifier`]: the HIP implementation (libpbft_verify.so, gfx950).
 //! * [`CpuVerifier`] (feature `cpu`): ed25519-dalek 1.0.1 `PublicKey::verify_strict` per
 //!   signature -- the reference's own crypto (libp2p-core 0.31.1 -> ed25519-dalek 1.0.1,
-//!   Cargo.lock:668-679); bit-exact with the GPU on every vector class (tests/golden).
+//!   Cargo.lock:668-679).  UNTESTED: there is no Rust toolchain in the build image, so this
+//!   implementation has never been compiled or run; the GPU path's bit-exactness is established
+//!   against the repository's C and Python restatements of verify_strict (tests/golden), not
+//!   against this code.
 //! * [`Replica`]: the native round batcher + quorum state machine
 //!   (include/pbft_replica.h) that replaces `validate_prepare` / `validate_commit`
 //!   (src/behavior.rs:159-195) and keys votes by the authenticated peer
@@ -489,6 +492,18 @@ impl<'a> Replica<'a> {
         let ctx = gpu.map(|g| g.raw()).unwrap_or(ptr::null_mut());
         check(unsafe {
             ffi::pbft_replica_create(ctx, keys.len() as u32, self_id, keys.as_ptr() as *const u8, &mut raw)
+        })?;
+        Ok(Replica { raw, verifier: None, events: vec![ffi::pbft_round_event::default(); 4096], _gpu: PhantomData })
+    }
+    /// One replica over several GPU contexts (one per GPU of the node, each with `keys` installed;
+    /// pbft_replica_create_multi): a large flush is cut into one slice per context, staged and launched
+    /// on every GPU's own PCIe link at once, and applied in row order as each slice's bitmap lands.
+    pub fn new_multi(gpus: &[&'a GpuVerifier], self_id: u32, keys: &[[u8; 32]]) -> Result<Self> {
+        let ctxs: Vec<*mut ffi::pbft_ctx> = gpus.iter().map(|g| g.raw()).collect();
+        let mut raw = ptr::null_mut();
+        check(unsafe {
+            ffi::pbft_replica_create_multi(ctxs.as_ptr(), ctxs.len() as u32, keys.len() as u32, self_id,
+                                           keys.as_ptr() as *const u8, &mut raw)
         })?;
         Ok(Replica { raw, verifier: None, events: vec![ffi::pbft_round_event::default(); 4096], _gpu: PhantomData })
     }

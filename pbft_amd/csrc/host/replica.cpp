@@ -1534,7 +1534,7 @@ int pbft_replica_flush(pbft_replica* r, int force, pbft_round_event* events, uin
 
 int pbft_replica_in_flight(pbft_replica* r) { return r ? (r->in_flight ? 1 : 0) : PBFT_EINVAL; }
 
-// One connection's byte stream of UviBytes/JSON frames (src/protocol_config.rs:50-76 ->
+// One connection's byte stream of UviBytes/JSON frames (src/protocol_config.rs:49-69 ->
 // src/handler.rs:533-548 -> inject_node_event).  peer_idx = the authenticated peer.
 int pbft_replica_push_frames(pbft_replica* r, uint32_t peer_idx, const uint8_t* stream, size_t len,
                              uint64_t* consumed, uint64_t* pushed, uint64_t* dropped) {

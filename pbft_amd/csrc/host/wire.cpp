@@ -1,5 +1,5 @@
 // Wire codec of the PBFT messages feeding the GPU verifier (include/pbft_wire.h):
-// UviBytes framing (src/protocol_config.rs:41-135) + serde_json encoding of the
+// UviBytes framing (src/protocol_config.rs:41-129) + serde_json encoding of the
 // reference's externally tagged Message enum (src/message.rs:7-31), extended
 // with the signed-envelope fields "replica" and "signature".
 //

@@ -1,7 +1,7 @@
 """ctypes binding of the wire codec (include/pbft_wire.h, pbft_amd/csrc/host/wire.cpp).
 
 Plumbing for tests and tools: UviBytes framing + serde_json Message encoding of
-the reference (src/protocol_config.rs:41-135, src/message.rs:7-31) with the
+the reference (src/protocol_config.rs:41-129, src/message.rs:7-31) with the
 signed-envelope fields, and the stream -> struct-of-arrays vote decoder that
 feeds the GPU verifier.  The codec itself is the C++ library code.
 """

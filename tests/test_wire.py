@@ -3,8 +3,8 @@
 Oracle: Python's json.dumps(obj, separators=(",", ":"), ensure_ascii=False) is
 byte-identical to serde_json::to_string for these structs (same field order,
 same escapes), which is what the reference sends (message_to_json,
-src/protocol_config.rs:121-129).  Varint vectors follow the unsigned-varint /
-LEB128 spec used by UviBytes (src/protocol_config.rs:58, :88).  The one
+src/protocol_config.rs:116-123).  Varint vectors follow the unsigned-varint /
+LEB128 spec used by UviBytes (src/protocol_config.rs:51, :82).  The one
 message the reference itself holds is the client request in README.md:42.
 """
 import hashlib
