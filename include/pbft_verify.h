@@ -210,6 +210,18 @@ static inline uint64_t pbft_votes_chunk_end(uint64_t lo, uint64_t n) {
 #define PBFT_VOTES_CHUNK_END(lo, n) pbft_votes_chunk_end((uint64_t)(lo), (uint64_t)(n))
 int pbft_verify_votes_submit_rows(pbft_ctx *ctx, uint64_t rows);
 int pbft_verify_poll_rows(pbft_ctx *ctx, uint64_t *rows_done);
+/* Votes rows the caller already holds in pinned host memory (pbft_host_alloc): rows[N] of PBFT_VOTES_ROW_BYTES laid
+ * out as pbft_verify_votes_stage describes, then envelopes[n_env][85] in a buffer of its own (+ 16 readable bytes);
+ * both stay unchanged until the batch completes.  Launches the whole batch at once on the chunk schedule above, each
+ * chunk's H2D straight from the caller's rows (no staging, no fill), and completes like the progressive form
+ * (pbft_verify_poll_rows / pbft_verify_wait).  pbft_replica writes every vote's row into such a buffer when the vote
+ * is pushed, so its flush touches no vote a second time. */
+int pbft_verify_votes_submit_host(pbft_ctx *ctx, const uint8_t *rows, uint64_t N, const uint8_t *envelopes,
+                                  uint32_t n_env, uint64_t *bitmap_out);
+/* Pinned host memory the context's device (and the node's other GPUs) can DMA from: hipHostMalloc, portable and
+ * mapped.  *out = NULL and PBFT_ENOMEM on failure.  Free with pbft_host_free (it may wait for the device). */
+int pbft_host_alloc(pbft_ctx *ctx, size_t bytes, void **out);
+int pbft_host_free(pbft_ctx *ctx, void *p);
 
 /* Device-resident form: all pointers are device pointers on the context's
  * device; stream is a hipStream_t (NULL = the context's stream).  Enqueues the

@@ -50,80 +50,27 @@ using Digest = std::array<uint8_t, 64>;
 enum : uint8_t { V_PENDING = 0, V_IN_FLIGHT = 1 };
 
 // Candidates of one kind in one round window, as columns in push order (a candidate leaves when its batch
-// completes, so between batches every candidate is pending and a batch takes a whole phase): the 64-byte
-// signatures are copied into the verifier's staging with one memcpy per phase.  Per signer: the candidate
-// count (flood bound) and the accepted digest (HashMap<PeerId, _>::insert, src/state.rs:49-67: the last
+// completes, so between batches every candidate is pending and a batch takes a whole phase).  A candidate's
+// signature lives in its staged row (include/pbft_verify.h: R || S, key index, envelope index), written into one of
+// the replica's two row arenas when the vote is pushed (the flush then hands the arena to the
+// GPU as it is, without a second pass over every vote); the phase keeps the row's reference.  Per signer: the
+// candidate count (flood bound) and the accepted digest (HashMap<PeerId, _>::insert, src/state.rs:49-67: the last
 // accepted vote of a signer wins).  Phase 0 of a window holds its PrePrepare candidates (signer = primary).
-// Growable byte buffer whose appends leave the new bytes uninitialised (std::vector would zero them first: a
-// second write of every signature byte before push_many's streaming stores).
-class ByteBuf {
- public:
-  size_t size() const { return n_; }
-  size_t capacity() const { return cap_; }
-  uint8_t* data() { return p_.get(); }
-  const uint8_t* data() const { return p_.get(); }
-  uint8_t& operator[](size_t i) { return p_[i]; }
-  const uint8_t& operator[](size_t i) const { return p_[i]; }
-  void reserve(size_t c) {
-    if (c > cap_) grow_to(c);
-  }
-  uint8_t* append(size_t k) {  // k more bytes at the end, uninitialised
-    if (n_ + k > cap_) grow_to(std::max(2 * cap_, n_ + k));
-    uint8_t* q = p_.get() + n_;
-    n_ += k;
-    return q;
-  }
-  void erase_front(size_t k) {
-    if (k >= n_) { n_ = 0; return; }
-    memmove(p_.get(), p_.get() + k, n_ - k);
-    n_ -= k;
-  }
-  void clear() { n_ = 0; }
-
- private:
-  void grow_to(size_t c) {
-    std::unique_ptr<uint8_t[]> q(new uint8_t[c]);  // (default-initialised: no zeroing)
-    if (n_) memcpy(q.get(), p_.get(), n_);
-    p_ = std::move(q);
-    cap_ = c;
-  }
-  std::unique_ptr<uint8_t[]> p_;
-  size_t n_ = 0, cap_ = 0;
-};
-
-// PBFT_STREAM_STORES=0: plain stores for the candidates' signatures (push) and the staged rows (flush fill); by
-// default both are streaming (non-temporal) stores -- no read-for-ownership of lines that are only written here
-// and read much later (r04 A/B on MI355X boxes: the flush's fill 1.1 -> 0.6 ms less of the calling thread's time).
-static const bool g_stream_stores = !(getenv("PBFT_STREAM_STORES") && atoi(getenv("PBFT_STREAM_STORES")) == 0);
-
-// 64 bytes from src to dst (8-byte aligned) with streaming stores where available
-static inline void copy64_nt(uint8_t* dst, const uint8_t* src) {
-#if defined(__x86_64__)
-  long long v[8];
-  memcpy(v, src, 64);  // (src may be unaligned: a caller's row)
-  for (int q = 0; q < 8; ++q) _mm_stream_si64((long long*)dst + q, v[q]);
-#else
-  memcpy(dst, src, 64);
-#endif
-}
-static inline void stream_fence() {
-#if defined(__x86_64__)
-  _mm_sfence();
-#endif
-}
-
+static constexpr uint32_t ROW_ARENA = 1u << 31, ROW_IDX = ROW_ARENA - 1;  // row reference: arena << 31 | index
 struct Phase {
-  ByteBuf sig;                // [k][64] R || S
+  std::vector<uint32_t> row;  // [k] the candidate's row reference
   std::vector<uint16_t> who;  // signer
   std::vector<uint32_t> dix;  // index into digs
   std::vector<uint8_t> st;    // V_PENDING / V_IN_FLIGHT
   std::vector<Digest> digs;   // distinct digests of the candidates (honest rounds: one)
+  std::vector<uint32_t> denv, dgen;  // per digest: its envelope in the arena of generation dgen (row env_idx)
   std::vector<uint8_t> cnt;   // per signer: candidates
   std::vector<uint32_t> acc;  // per signer: 1 + index into acc_digs (0: none)
   std::vector<Digest> acc_digs;
   std::vector<uint32_t> acc_cnt;  // signers per accepted digest
   uint32_t distinct = 0;          // signers with an accepted vote or a candidate
   uint32_t n_pending = 0;         // candidates not yet in a batch
+  uint64_t row_hi = 0;            // 1 + the largest row index of the candidates
   size_t size() const { return who.size(); }
   void init(uint32_t n) {
     if (cnt.empty()) {
@@ -137,40 +84,53 @@ struct Phase {
       if (memcmp(digs[j].data(), d, 64) == 0) return (int64_t)j;
     return -1;
   }
-  void append(const uint8_t* d, int64_t j, uint32_t signer, const uint8_t* sg, bool nt = false) {
+  void append(const uint8_t* d, int64_t j, uint32_t signer, uint32_t rref, uint32_t env, uint32_t gen) {
     if (j < 0) {
       digs.emplace_back();
       memcpy(digs.back().data(), d, 64);
-      j = (int64_t)digs.size() - 1;
+      denv.push_back(env);
+      dgen.push_back(gen);
+    } else {
+      denv[(size_t)j] = env;  // (the envelope of the arena this row went to)
+      dgen[(size_t)j] = gen;
     }
-    if (nt) copy64_nt(sig.append(64), sg);
-    else memcpy(sig.append(64), sg, 64);
+    row.push_back(rref);
     who.push_back((uint16_t)signer);
-    dix.push_back((uint32_t)j);
+    dix.push_back(j < 0 ? (uint32_t)digs.size() - 1 : (uint32_t)j);
     st.push_back(V_PENDING);
     ++n_pending;
+    if ((rref & ROW_IDX) + 1 > row_hi) row_hi = (rref & ROW_IDX) + 1;
   }
   // drop the first k candidates (a completed batch); re-index the digests of the rest
   void drop_front(size_t k) {
     if (k >= size()) {
-      sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
+      clear_columns();
       return;
     }
-    sig.erase_front(64 * k);
+    row.erase(row.begin(), row.begin() + k);
     who.erase(who.begin(), who.begin() + k);
     dix.erase(dix.begin(), dix.begin() + k);
     st.erase(st.begin(), st.begin() + k);
     std::vector<Digest> nd;
+    std::vector<uint32_t> ne, ng;
     for (uint32_t& x : dix) {
       size_t j = 0;
       while (j < nd.size() && nd[j] != digs[x]) ++j;
-      if (j == nd.size()) nd.push_back(digs[x]);
+      if (j == nd.size()) nd.push_back(digs[x]), ne.push_back(denv[x]), ng.push_back(dgen[x]);
       x = (uint32_t)j;
     }
     digs.swap(nd);
+    denv.swap(ne);
+    dgen.swap(ng);
+    row_hi = 0;
+    for (uint32_t x : row) row_hi = std::max<uint64_t>(row_hi, (x & ROW_IDX) + 1);
+  }
+  void clear_columns() {
+    row.clear(); who.clear(); dix.clear(); st.clear(); digs.clear(); denv.clear(); dgen.clear();
+    row_hi = 0;
   }
   void clear_candidates() {
-    sig.clear(); who.clear(); dix.clear(); st.clear(); digs.clear();
+    clear_columns();
     n_pending = 0;
   }
   // back to a fresh phase, keeping every allocation (recycled windows)
@@ -191,6 +151,35 @@ struct Phase {
   }
 };
 
+// PBFT_STREAM_STORES=0: plain stores for the staged rows push_many writes (and the flush's fill of the staging when
+// the arena cannot be handed over as it is); by default both are streaming (non-temporal) stores -- no
+// read-for-ownership of lines that are only written here and read next by the DMA engine (r04 A/B on MI355X boxes:
+// the flush's fill 1.1 -> 0.6 ms less of the calling thread's time).
+static const bool g_stream_stores = !(getenv("PBFT_STREAM_STORES") && atoi(getenv("PBFT_STREAM_STORES")) == 0);
+// PBFT_REPLICA_DIRECT=0: never hand a row arena to the GPU as it is (every batch filled into the staging: the r04 path)
+static const bool g_direct = !(getenv("PBFT_REPLICA_DIRECT") && atoi(getenv("PBFT_REPLICA_DIRECT")) == 0);
+
+// One staged row (include/pbft_verify.h: R || S, key_idx, two zero bytes, env_idx), streaming stores where available
+static inline void put_row(uint8_t* dst, const uint8_t* sig, uint32_t key, uint32_t env, bool nt) {
+  const uint64_t meta = (uint64_t)(key & 0xFFFF) | (uint64_t)env << 32;
+#if defined(__x86_64__)
+  if (nt) {
+    long long v[8];
+    memcpy(v, sig, 64);  // (sig may be unaligned: a caller's row)
+    for (int q = 0; q < 8; ++q) _mm_stream_si64((long long*)dst + q, v[q]);
+    _mm_stream_si64((long long*)dst + 8, (long long)meta);
+    return;
+  }
+#endif
+  memcpy(dst, sig, 64);
+  memcpy(dst + PBFT_VOTES_ROW_KEY, &meta, 8);
+}
+static inline void stream_fence() {
+#if defined(__x86_64__)
+  _mm_sfence();
+#endif
+}
+
 struct Window {
   Phase ph[3];  // [0] PrePrepare candidates, [1] Prepare, [2] Commit
   bool have_pre_prepare = false;
@@ -207,7 +196,8 @@ using WindowMap = std::map<std::pair<uint64_t, uint64_t>, Window>;
 struct Seg {
   Window* w;  // valid unless a window was erased while the batch was in flight (then looked up by key)
   Key key;
-  uint64_t row0;
+  uint64_t row0;     // its first row in the staged batch (arena batches: the candidates before it)
+  uint64_t row_end;  // every row of its candidates is below this one (the bitmap prefix that completes it)
   uint32_t count;
   uint32_t env0;  // its envelopes: env0 + index into the phase's digs
   uint8_t kind;   // 0 PrePrepare, 1 Prepare, 2 Commit
@@ -307,8 +297,30 @@ static uint64_t now_ns() {
     if (g_trace) (r)->trace.push_back({what, now_ns(), (uint64_t)(arg)}); \
   } while (0)
 
+// A row arena: the staged rows of pushed candidates (and the envelopes their env_idx name), in push order, in
+// pinned host memory when the replica has a GPU context.  Pushes go to the current arena; a flush whose batch is
+// exactly the current arena's live candidates (the common case: every phase ready) hands the arena itself to the GPU
+// (pbft_verify_votes_submit_host) and pushes move to the other one while it is in flight.
+struct Arena {
+  uint8_t* rows = nullptr;  // [cap][PBFT_VOTES_ROW_BYTES]
+  uint8_t* envs = nullptr;  // [ecap][PBFT_ENVELOPE_BYTES] + 64 bytes of read slack
+  uint64_t cap = 0, n = 0;  // rows allocated / written (candidates' rows, push_many's unused tails, dropped ones)
+  uint32_t ecap = 0, ne = 0;
+  bool rows_pinned = false, envs_pinned = false;
+  mutable std::atomic<int64_t> live{0};  // candidates whose rows are here
+  std::atomic<bool> clean{true};         // every row's env_idx names an envelope of this arena
+  uint32_t gen = 0;                      // envelope generation (phases' dgen): renewed when the arena restarts
+  bool busy = false;                     // the batch in flight reads it
+};
+
 struct pbft_replica {
   std::vector<TraceEv> trace;
+  Arena arena[2];
+  uint32_t cur = 0;        // the arena pushes write to (never busy)
+  uint32_t next_gen = 1;
+  bool direct = false;     // the batch in flight is arena `busy_arena` as it is (rows = arena rows)
+  uint32_t busy_arena = 0;
+  uint64_t applied_upto = 0;  // rows_done at the last progressive application
   pbft_ctx* ctx = nullptr;         // ctxs[0]: digests, small batches
   std::vector<pbft_ctx*> ctxs;     // pbft_replica_create_multi: large batches split over these (one per GPU)
   uint32_t n = 0, f = 0, self = 0;
@@ -353,6 +365,139 @@ struct pbft_replica {
 };
 
 static uint32_t primary_of(const pbft_replica* r, uint64_t view) { return (uint32_t)(view % r->n); }
+
+// ---- row arenas ----
+static constexpr size_t ROWB = PBFT_VOTES_ROW_BYTES;
+static void* host_mem(pbft_replica* r, size_t bytes, bool* pinned) {
+  void* p = nullptr;
+  *pinned = false;
+  if (r->ctx && pbft_host_alloc(r->ctx, bytes, &p) == PBFT_OK && p) {
+    *pinned = true;
+    return p;
+  }
+  return aligned_alloc(64, (bytes + 63) / 64 * 64);  // (no GPU context: the overrides read it)
+}
+static void host_mem_free(pbft_replica* r, void* p, bool pinned) {
+  if (!p) return;
+  if (pinned) (void)pbft_host_free(r->ctx, p);
+  else free(p);
+}
+// room for `rows` more rows and `envs` more envelopes (the current arena only: never busy)
+static bool arena_reserve(pbft_replica* r, Arena& a, uint64_t rows, uint64_t envs) {
+  if (a.n + rows > a.cap) {
+    if (a.n + rows > ROW_IDX) return false;
+    const uint64_t c = std::min<uint64_t>(ROW_IDX, std::max<uint64_t>({2 * a.cap, a.n + rows, 1u << 12}));
+    bool pin;
+    uint8_t* q = (uint8_t*)host_mem(r, ROWB * c, &pin);
+    if (!q) return false;
+    if (a.n) memcpy(q, a.rows, ROWB * a.n);
+    host_mem_free(r, a.rows, a.rows_pinned);
+    a.rows = q;
+    a.rows_pinned = pin;
+    a.cap = c;
+  }
+  if (a.ne + envs > a.ecap) {
+    if (a.ne + envs > ROW_IDX) return false;
+    const uint64_t c = std::min<uint64_t>(ROW_IDX, std::max<uint64_t>({2 * (uint64_t)a.ecap, a.ne + envs, 256}));
+    bool pin;
+    uint8_t* q = (uint8_t*)host_mem(r, (size_t)PBFT_ENVELOPE_BYTES * c + 64, &pin);
+    if (!q) return false;
+    if (a.ne) memcpy(q, a.envs, (size_t)PBFT_ENVELOPE_BYTES * a.ne);
+    host_mem_free(r, a.envs, a.envs_pinned);
+    a.envs = q;
+    a.envs_pinned = pin;
+    a.ecap = (uint32_t)c;
+  }
+  return true;
+}
+// Start the arena over (no candidate's row is in it, nothing reads it): envelope 0 is the one of rows no candidate
+// references (push_many's unused tails)
+static const uint8_t g_zero_digest[64] = {0};
+static void arena_restart(pbft_replica* r, Arena& a) {
+  a.n = 0;
+  a.ne = 0;
+  a.gen = r->next_gen++;
+  a.clean.store(true, std::memory_order_relaxed);
+  if (arena_reserve(r, a, 0, 1)) {
+    pbft_envelope(a.envs, 0, 0, 0, g_zero_digest);
+    a.ne = 1;
+  } else {
+    a.clean.store(false, std::memory_order_relaxed);
+  }
+}
+// the arena pushes write to, restarted first when nothing references it any more
+static Arena& push_arena(pbft_replica* r) {
+  Arena& a = r->arena[r->cur];
+  if (a.gen == 0 || (a.n > 0 && a.live.load(std::memory_order_relaxed) == 0 && !a.busy)) arena_restart(r, a);
+  return a;
+}
+static inline const uint8_t* row_at(const pbft_replica* r, uint32_t rref) {
+  return r->arena[rref >> 31].rows + ROWB * (rref & ROW_IDX);
+}
+// the first k candidates of p leave (their rows are dead from here on)
+static void release_rows(const pbft_replica* r, const Phase& p, size_t k) {
+  int64_t c[2] = {0, 0};
+  const size_t m = std::min(k, p.row.size());
+  for (size_t i = 0; i < m; ++i) ++c[p.row[i] >> 31];
+  for (int a = 0; a < 2; ++a)
+    if (c[a]) r->arena[a].live.fetch_sub(c[a], std::memory_order_relaxed);
+}
+static void release_window(const pbft_replica* r, Window& w) {
+  for (Phase& p : w.ph) {
+    release_rows(r, p, p.size());
+    p.clear_candidates();
+  }
+}
+
+// Where one pusher writes rows and envelopes: the current arena's end (a single push: grows it), or a range of it
+// reserved for one push_many thread (sized for the thread's rows; envelopes beyond its share leave the arena
+// unclean, which sends the next batch through the staging fill instead).
+struct Sink {
+  Arena* a;
+  uint32_t aid;
+  uint64_t row, row_end;
+  uint32_t env, env_end;
+  bool grow, nt;
+  int64_t added = 0;
+};
+static Sink single_sink(pbft_replica* r) {
+  Arena& a = push_arena(r);
+  return Sink{&a, r->cur, a.n, ~0ull, a.ne, ~0u, true, false};
+}
+static void sink_done(Sink& s) {  // (single sinks) the arena's counts
+  if (s.grow) {
+    s.a->n = s.row;
+    s.a->ne = s.env;
+  }
+  s.a->live.fetch_add(s.added, std::memory_order_relaxed);
+  s.added = 0;
+}
+static uint32_t sink_env(pbft_replica* r, Sink& s, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t* d) {
+  if (s.grow) {
+    s.a->n = s.row;
+    s.a->ne = s.env;
+    if (!arena_reserve(r, *s.a, 0, 1)) {
+      s.a->clean.store(false, std::memory_order_relaxed);
+      return 0;
+    }
+  } else if (s.env >= s.env_end) {
+    s.a->clean.store(false, std::memory_order_relaxed);
+    return 0;
+  }
+  pbft_envelope(s.a->envs + (size_t)PBFT_ENVELOPE_BYTES * s.env, kind, view, seq, d);
+  return s.env++;
+}
+static bool sink_row(pbft_replica* r, Sink& s, uint64_t* idx) {
+  if (s.grow) {
+    s.a->n = s.row;
+    s.a->ne = s.env;
+    if (!arena_reserve(r, *s.a, 1, 0)) return false;
+  } else if (s.row >= s.row_end) {
+    return false;  // (never: a thread's range holds every row it may push)
+  }
+  *idx = s.row++;
+  return true;
+}
 
 static bool in_log(const pbft_replica* r, uint64_t seq) { return seq > r->h && seq - r->h <= r->log_window; }
 
@@ -417,6 +562,7 @@ static Window& window_at(pbft_replica* r, const Key& k) {
 static WindowMap::iterator drop_window(pbft_replica* r, WindowMap::iterator it) {
   auto next = std::next(it);
   if (r->in_flight) r->erased_in_flight = true;
+  release_window(r, it->second);  // (an in-flight batch skips the window's rows: erased_in_flight)
   if (r->spare.size() < 4096) r->spare.push_back(r->windows.extract(it));
   else r->windows.erase(it);
   return next;
@@ -513,7 +659,7 @@ static void evaluate_window(const pbft_replica* r, uint64_t view, uint64_t seq, 
   if (!w.committed_reported && is_committed_local(r, view, w)) {
     w.committed_reported = true;
     out.push_back({view, seq, PBFT_EVENT_COMMITTED_LOCAL});
-    for (Phase& p : w.ph) p.clear_candidates();  // decided: stragglers are never needed
+    release_window(r, w);  // decided: stragglers are never needed
   }
 }
 
@@ -559,6 +705,8 @@ static void revert_segs(pbft_replica* r) {
   r->seg_next = 0;
   r->in_flight = false;
   r->erased_in_flight = false;
+  if (r->direct) r->arena[r->busy_arena].busy = false;
+  r->direct = false;
 }
 
 // The finished batch: State::insert_* for accepted candidates (in push order: the last accepted vote of a signer
@@ -581,10 +729,14 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
     Window& w = *wp;
     Phase& p = w.ph[g.kind];
     const uint64_t* bm = r->bitmap.data();
+    // candidate i's row: its arena row when the arena went to the GPU as it is, else the staged row0 + i
+    const uint32_t* rref = r->direct ? p.row.data() : nullptr;
+    const uint64_t row0 = g.row0;
+    auto row_of = [rref, row0](uint32_t i) -> uint64_t { return rref ? (uint64_t)(rref[i] & ROW_IDX) : row0 + i; };
     uint32_t acc_n = 0;
     if (g.kind == 0) {
       for (uint32_t i = 0; i < g.count; ++i) {
-        const uint64_t row = g.row0 + i;
+        const uint64_t row = row_of(i);
         if (!((bm[row >> 6] >> (row & 63)) & 1)) continue;
         ++acc_n;
         const Digest& d = p.digs[p.dix[i]];
@@ -609,7 +761,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
         const uint32_t a = p.acc_index(p.digs[0]) + 1;
         uint32_t gained = 0;
         for (uint32_t i = 0; i < g.count; ++i) {
-          const uint64_t row = g.row0 + i;
+          const uint64_t row = row_of(i);
           const uint32_t s = who[i];
           const uint32_t prev = acc[s];
           if ((bm[row >> 6] >> (row & 63)) & 1) {
@@ -628,7 +780,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
         st[2] += mism[0] ? acc_n : 0;
       } else {
         for (uint32_t i = 0; i < g.count; ++i) {
-          const uint64_t row = g.row0 + i;
+          const uint64_t row = row_of(i);
           const uint32_t s = who[i];
           if ((bm[row >> 6] >> (row & 63)) & 1) {
             ++acc_n;
@@ -649,6 +801,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
     }
     st[0] += acc_n;
     st[1] += g.count - acc_n;
+    release_rows(r, p, g.count);
     p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
     touched[gi] = acc_n > 0;
     // the window's last segment of this batch: its events are decided now, on this thread (segments come in
@@ -720,6 +873,8 @@ static void finish_batch(pbft_replica* r) {
   r->seg_next = 0;
   r->in_flight = false;
   r->erased_in_flight = false;
+  if (r->direct) r->arena[r->busy_arena].busy = false;
+  r->direct = false;
 }
 
 // Copy the candidates of segments [s0, s1) into the batch: the GPU context's staged votes rows (rs =
@@ -734,26 +889,10 @@ static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
     const bool one = p.digs.size() == 1;
     if (rs) {
       uint8_t* row = SIG + rs * (g.row0 - base);
-#if defined(__x86_64__)
-      if (g_stream_stores) {  // streaming stores: no read-for-ownership of the staging lines (the DMA reads them next)
-        for (uint32_t i = 0; i < g.count; ++i, row += rs) {
-          const long long* src = (const long long*)&p.sig[64 * (size_t)i];
-          long long* dst = (long long*)row;
-          for (int q = 0; q < 8; ++q) _mm_stream_si64(dst + q, src[q]);
-          _mm_stream_si64(dst + 8, (long long)((uint64_t)p.who[i] | (uint64_t)(g.env0 + (one ? 0 : p.dix[i])) << 32));
-        }
-        memset(p.st.data(), V_IN_FLIGHT, g.count);
-        p.n_pending = 0;
-        continue;
-      }
-#endif
-      for (uint32_t i = 0; i < g.count; ++i, row += rs) {
-        memcpy(row, &p.sig[64 * (size_t)i], 64);
-        const uint64_t meta = (uint64_t)p.who[i] | (uint64_t)(g.env0 + (one ? 0 : p.dix[i])) << 32;
-        memcpy(row + PBFT_VOTES_ROW_KEY, &meta, 8);  // key_idx, two zero bytes, env_idx
-      }
+      for (uint32_t i = 0; i < g.count; ++i, row += rs)
+        put_row(row, row_at(r, p.row[i]), p.who[i], g.env0 + (one ? 0 : p.dix[i]), g_stream_stores);
     } else {
-      memcpy(SIG + 64 * g.row0, p.sig.data(), 64 * (size_t)g.count);
+      for (uint32_t i = 0; i < g.count; ++i) memcpy(SIG + 64 * (g.row0 + i), row_at(r, p.row[i]), 64);
       memcpy(K + g.row0, p.who.data(), 2 * (size_t)g.count);
       if (one) {
         std::fill(IDX + g.row0, IDX + g.row0 + g.count, g.env0);
@@ -1064,6 +1203,10 @@ int pbft_replica_destroy(pbft_replica* r) {
   }
   if (r->in_flight && r->in_flight_via == 1 && r->vpoll)
     while (r->vpoll(r->vuser) == 0) std::this_thread::yield();
+  for (Arena& a : r->arena) {
+    host_mem_free(r, a.rows, a.rows_pinned);
+    host_mem_free(r, a.envs, a.envs_pinned);
+  }
   delete r;
   return PBFT_OK;
 }
@@ -1139,9 +1282,17 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
   const int64_t j = p.find_dig(d);
   if (j >= 0)
     for (size_t i = 0; i < p.size(); ++i)
-      if (p.dix[i] == (uint32_t)j && memcmp(&p.sig[64 * i], primary_sig, 64) == 0) { ++r->stats.duplicates; return 0; }
+      if (p.dix[i] == (uint32_t)j && memcmp(row_at(r, p.row[i]), primary_sig, 64) == 0) { ++r->stats.duplicates; return 0; }
   if (p.size() >= PBFT_MAX_CANDIDATES) { ++r->stats.dropped_flood; return 0; }
-  p.append(d, j, primary_of(r, view), primary_sig);
+  Sink s = single_sink(r);
+  const uint32_t prim = primary_of(r, view);
+  const uint32_t env = j >= 0 && p.dgen[(size_t)j] == s.a->gen ? p.denv[(size_t)j] : sink_env(r, s, 0, view, seq, d);
+  uint64_t ri;
+  if (!sink_row(r, s, &ri)) { sink_done(s); return PBFT_ENOMEM; }
+  put_row(s.a->rows + ROWB * ri, primary_sig, prim, env, false);
+  p.append(d, j, prim, s.aid << 31 | (uint32_t)ri, env, s.a->gen);
+  ++s.added;
+  sink_done(s);
   return 1;
 }
 
@@ -1150,9 +1301,10 @@ struct PushCounts {
   uint64_t pushed = 0, rejected_view = 0, rejected_watermark = 0, duplicates = 0, dropped_flood = 0, queued = 0;
 };
 
-// The part of a push that touches one window (State::insert_* candidates, src/state.rs:49-67): 1 queued, 0 dropped.
-static int push_into(const pbft_replica* r, Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer,
-                     const uint8_t* sig, PushCounts& st, bool nt = false) {
+// The part of a push that touches one window (State::insert_* candidates, src/state.rs:49-67): 1 queued, 0 dropped,
+// PBFT_ENOMEM (no arena row).  The candidate's staged row goes to the sink's arena.
+static int push_into(pbft_replica* r, Window& w, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t* digest,
+                     uint32_t signer, const uint8_t* sig, PushCounts& st, Sink& sk) {
   if (w.committed_reported) { ++st.duplicates; return 0; }  // late vote for a decided round
   Phase& p = w.ph[kind];
   p.init(r->n);
@@ -1164,20 +1316,25 @@ static int push_into(const pbft_replica* r, Window& w, uint8_t kind, const uint8
   if (p.cnt[signer]) {
     if (j >= 0)
       for (size_t i = 0; i < p.size(); ++i)
-        if (p.who[i] == signer && p.dix[i] == (uint32_t)j && memcmp(&p.sig[64 * i], sig, 64) == 0) {
+        if (p.who[i] == signer && p.dix[i] == (uint32_t)j && memcmp(row_at(r, p.row[i]), sig, 64) == 0) {
           ++st.duplicates;
           return 0;
         }
     if (p.cnt[signer] >= PBFT_MAX_CANDIDATES) { ++st.dropped_flood; return 0; }
-  } else if (!p.acc[signer]) {
-    ++p.distinct;
   }
-  if (p.sig.capacity() == 0) {  // one allocation per phase for the common case (every signer votes once)
+  if (p.row.capacity() == 0) {  // one allocation per phase for the common case (every signer votes once)
     const size_t c = r->n < 1024 ? r->n : 1024;
-    p.sig.reserve(64 * c); p.who.reserve(c); p.dix.reserve(c); p.st.reserve(c);
+    p.row.reserve(c); p.who.reserve(c); p.dix.reserve(c); p.st.reserve(c);
   }
-  p.append(digest, j, signer, sig, nt);
+  const uint32_t env =
+      j >= 0 && p.dgen[(size_t)j] == sk.a->gen ? p.denv[(size_t)j] : sink_env(r, sk, kind, view, seq, digest);
+  uint64_t ri;
+  if (!sink_row(r, sk, &ri)) return PBFT_ENOMEM;
+  put_row(sk.a->rows + ROWB * ri, sig, signer, env, sk.nt);
+  if (!p.cnt[signer] && !p.acc[signer]) ++p.distinct;
+  p.append(digest, j, signer, sk.aid << 31 | (uint32_t)ri, env, sk.a->gen);
   ++p.cnt[signer];
+  ++sk.added;
   ++st.queued;
   return 1;
 }
@@ -1199,7 +1356,11 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
   int rc = 0;
   if (signer >= r->n || view != r->current_view) ++c.rejected_view;  // validate_commit :187-190
   else if (!in_log(r, seq)) ++c.rejected_watermark;
-  else rc = push_into(r, window_at(r, {view, seq}), kind, digest, signer, sig, c);
+  else {
+    Sink sk = single_sink(r);
+    rc = push_into(r, window_at(r, {view, seq}), kind, view, seq, digest, signer, sig, c, sk);
+    sink_done(sk);
+  }
   add_counts(r, c);
   return rc;
 }
@@ -1217,14 +1378,20 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
   const size_t T = n_ok >= PUSH_PAR_MIN ? std::min<size_t>(hw ? hw : 1, host_threads()) : 1;
   uint64_t q = 0;
   if (T <= 1) {
-    for (uint64_t i = 0; i < n_ok; ++i)
-      q += (uint64_t)pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
+    for (uint64_t i = 0; i < n_ok; ++i) {
+      const int rc = pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
+      if (rc < 0) {
+        if (queued) *queued = q;
+        return rc;
+      }
+      q += (uint64_t)rc;
+    }
   } else {
     // The windows are independent: every window's rows go to ONE thread, in input order (per-window order is
     // all the state machine depends on: the last accepted vote of a signer wins).
     //  1. (threads, by input slices) the per-row checks that need no window, and runs of consecutive rows with
     //     one (view, seq); rejected rows are flagged and do not break a run;
-    struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; };
+    struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; };
     RTRACE(r, "push", n_ok);
     std::vector<std::vector<Run>> slice_runs(T);
     std::vector<uint8_t> bad(n_ok);
@@ -1235,7 +1402,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       // (locals: the byte stores below may alias anything, which would reload every field per row)
       const uint32_t n = r->n;
       const uint64_t cur = r->current_view, h = r->h, win = r->log_window;
-      uint64_t rv = 0, rw = 0, run_seq = ~0ull, run_lo = 0;
+      uint64_t rv = 0, rw = 0, run_seq = ~0ull, run_lo = 0, run_good = 0;
       uint8_t* bd = bad.data();
       for (uint64_t i = lo; i < hi; ++i) {
         const uint64_t q = seq[i];
@@ -1246,39 +1413,72 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         bd[i] = v_bad | w_bad;
         if (v_bad | w_bad) continue;
         if (q != run_seq) {
-          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0});
+          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0, run_good});
           run_seq = q;
           run_lo = i;
+          run_good = 0;
         }
+        ++run_good;
       }
-      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0});
+      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good});
       cnt[t].pushed += hi - lo;
       cnt[t].rejected_view += rv;
       cnt[t].rejected_watermark += rw;
     });
     //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
-    //     owner: the thread whose share of the rows its first run starts in;
+    //     owner: the thread whose share of the rows its first run starts in; each thread's range of the arena:
+    //     a row per row it may push, two envelopes per window it owns (one per kind: honest rounds) + 64
     RTRACE(r, "push_checked", T);
     std::vector<Run> runs;
     for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
     std::unordered_map<Window*, uint32_t> owner;
     owner.reserve(runs.size() < 8192 ? runs.size() : 8192);
+    std::vector<uint64_t> t_rows(T, 0), t_envs(T, 64);
     for (Run& u : runs) {
       u.w = &window_at(r, {r->current_view, u.seq});
-      auto it = owner.emplace(u.w, (uint32_t)(u.lo * T / n_ok)).first;
-      u.owner = it->second;
+      auto ins = owner.emplace(u.w, (uint32_t)(u.lo * T / n_ok));
+      u.owner = ins.first->second;
+      t_rows[u.owner] += u.good;
+      if (ins.second) t_envs[u.owner] += 2;
+    }
+    Arena& A = push_arena(r);
+    uint64_t rows_all = 0, envs_all = 0;
+    for (size_t t = 0; t < T; ++t) rows_all += t_rows[t], envs_all += t_envs[t];
+    if (!arena_reserve(r, A, rows_all, envs_all)) return PBFT_ENOMEM;  // (nothing pushed)
+    std::vector<Sink> sinks;
+    {
+      uint64_t row = A.n, env = A.ne;
+      for (size_t t = 0; t < T; ++t) {
+        sinks.push_back(Sink{&A, r->cur, row, row + t_rows[t], (uint32_t)env, (uint32_t)(env + t_envs[t]), false,
+                             g_stream_stores});
+        row += t_rows[t];
+        env += t_envs[t];
+      }
     }
     RTRACE(r, "push_windows", runs.size());
-    //  3. (threads) every thread pushes the rows of the windows it owns, in input order.
+    //  3. (threads) every thread pushes the rows of the windows it owns, in input order, into its range; the range's
+    //     unused rows (rejected pushes) become rows no candidate references (key 0, envelope 0), its unused
+    //     envelopes copies of envelope 0
     WorkerPool::get().run(T, [&](size_t t) {
-      PushCounts& c = cnt[t];
+      // (thread-local copies: the threads' entries of cnt / sinks share cache lines, and every row updates them)
+      PushCounts c = cnt[t];
+      Sink sk = sinks[t];
       for (const Run& u : runs) {
         if (u.owner != t) continue;
         for (uint64_t i = u.lo; i < u.hi; ++i)
-          if (!bad[i]) push_into(r, *u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, g_stream_stores);
+          if (!bad[i]) push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
       }
+      static const uint8_t zero_sig[64] = {0};
+      for (; sk.row < sk.row_end; ++sk.row) put_row(A.rows + ROWB * sk.row, zero_sig, 0, 0, g_stream_stores);
+      for (; sk.env < sk.env_end; ++sk.env)
+        memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
       if (g_stream_stores) stream_fence();  // (streaming stores are weakly ordered: drained before the join)
+      cnt[t] = c;
+      sinks[t] = sk;
     });
+    A.n += rows_all;
+    A.ne += (uint32_t)envs_all;
+    for (Sink& sk : sinks) A.live.fetch_add(sk.added, std::memory_order_relaxed);
     for (const PushCounts& c : cnt) {
       add_counts(r, c);
       q += c.queued;
@@ -1298,6 +1498,66 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
 // Verify every READY sub-window (force: every pending candidate) in one batch, asynchronously.
 static uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
   return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+}
+
+// The batch is the current arena as it is (flush_submit_impl checked that its live candidates are exactly the
+// batch's): rows [0, A.n) -- the candidates' rows, push_many's unused tails and rows of candidates that left before
+// the flush, which verify and are never applied -- go to the GPU straight from the pinned arena, over every context
+// in 64-aligned slices; the segments read their candidates' bits at their row references.
+static int submit_arena(pbft_replica* r, uint64_t N) {
+  const uint32_t a = r->cur;
+  Arena& A = r->arena[a];
+  for (Seg& g : r->segs) {
+    Phase& p = g.w->ph[g.kind];
+    g.row_end = p.row_hi;
+    memset(p.st.data(), V_IN_FLIGHT, g.count);
+    p.n_pending = 0;
+  }
+  const uint64_t rows = A.n;
+  r->rows = N;
+  r->rows_span = rows;
+  r->bitmap.assign((rows + 63) / 64, 0);
+  r->touched.assign(r->segs.size(), 0);
+  r->seg_next = 0;
+  r->slice_lo.clear();
+  const size_t K = r->ctxs.size();
+  int rc = PBFT_OK;
+  RTRACE(r, "arena", rows);
+  if (K > 1 && rows >= (1u << 16)) {
+    r->slice_lo.assign(K + 1, rows);
+    for (size_t k = 0; k < K; ++k) r->slice_lo[k] = (rows * k / K) & ~(uint64_t)63;
+    r->slice_hi.assign(r->slice_lo.begin() + 1, r->slice_lo.end());
+    r->slice_end.assign(K, 0);
+    r->slice_fin.assign(K, 0);
+    size_t opened = 0;
+    for (size_t k = 0; k < K && rc == PBFT_OK; ++k) {
+      const uint64_t lo = r->slice_lo[k], hi = r->slice_lo[k + 1];
+      rc = pbft_verify_votes_submit_host(r->ctxs[k], A.rows + ROWB * lo, hi - lo, A.envs, A.ne,
+                                         r->bitmap.data() + lo / 64);
+      if (rc == PBFT_OK) opened = k + 1;
+    }
+    if (rc) {
+      for (size_t k = 0; k < opened; ++k) (void)pbft_verify_wait(r->ctxs[k]);
+      r->direct = false;
+      revert_segs(r);
+      return rc;
+    }
+  } else {
+    rc = pbft_verify_votes_submit_host(r->ctx, A.rows, rows, A.envs, A.ne, r->bitmap.data());
+    if (rc) {
+      r->direct = false;
+      revert_segs(r);
+      return rc;
+    }
+  }
+  RTRACE(r, "launched", K);
+  A.busy = true;
+  r->busy_arena = a;
+  r->direct = true;
+  r->cur = a ^ 1;  // (the other arena holds no candidate: restarted by the next push)
+  r->in_flight = true;
+  r->in_flight_via = 0;
+  return PBFT_OK;
 }
 
 static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows);
@@ -1328,7 +1588,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     for (int kind = 0; kind < 3; ++kind) {
       if (!rd[kind]) continue;
       Phase& p = w.ph[kind];
-      r->segs.push_back({&w, kv.first, N, (uint32_t)p.size(), E, (uint8_t)kind});
+      r->segs.push_back({&w, kv.first, N, N + p.size(), (uint32_t)p.size(), E, (uint8_t)kind});
       N += p.size();
       E += (uint32_t)p.digs.size();
     }
@@ -1339,9 +1599,22 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   RTRACE(r, "segs", r->segs.size());
   if (n_rows) *n_rows = N;
   if (N == 0) { r->segs.clear(); return PBFT_OK; }
+  r->applied_upto = 0;
+  {
+    // the batch is exactly the current arena's candidates: the arena goes to the GPU as it is
+    Arena& A = r->arena[r->cur];
+    Arena& B = r->arena[r->cur ^ 1];
+    const bool direct = g_direct && r->ctx && !r->verify_fn && !r->vsub && A.rows_pinned && A.envs_pinned &&
+                        A.clean.load() && A.gen && B.live.load() == 0 && !B.busy &&
+                        (int64_t)N == A.live.load() && A.n <= N + std::max<uint64_t>(4096, N / 16);
+    if (direct) return submit_arena(r, N);
+    // (else the staging fill below; pushes during the flight go to the other arena when nothing is left in it)
+    if (B.live.load() == 0 && !B.busy) r->cur ^= 1;
+  }
   // several contexts (pbft_replica_create_multi) and a batch large enough for the threaded fill: one slice each
   const bool multi = r->ctxs.size() > 1 && !r->verify_fn && !r->vsub && N >= (1u << 16) && plan_slices(r);
   if (!multi) r->slice_lo.clear();
+  for (Seg& g : r->segs) g.row_end = g.row0 + g.count;  // (after plan_slices moved the slices' rows)
   r->bitmap.assign((r->rows_span + 63) / 64, 0);
   // 2. fill the batch: the GPU context's pinned staging (zero-copy votes form) or the overrides' buffers; large
   //    batches with several threads (a memcpy per phase: the replica's side is memory-bound)
@@ -1472,10 +1745,12 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
       // a large batch comes back chunk by chunk: apply the segments whose rows are all in while the GPU runs on
       // (a window's segments stay in order: a prefix of the batch)
       const size_t G = r->segs.size();
-      if (rows_done >= (r->seg_next < G ? r->segs[r->seg_next].row0 : r->rows_span) + (1u << 16)) {
+      // (at least 2^16 more rows in since the last application: the pool wakes for a chunk, not per poll)
+      if (r->seg_next < G && rows_done >= r->applied_upto + (1u << 16)) {
         RTRACE(r, "landed", rows_done);
         size_t s1 = r->seg_next;
-        while (s1 < G && r->segs[s1].row0 + r->segs[s1].count <= rows_done) ++s1;
+        while (s1 < G && r->segs[s1].row_end <= rows_done) ++s1;
+        if (s1 > r->seg_next) r->applied_upto = rows_done;
         apply_segs(r, r->seg_next, s1);
         r->stats.apply_ns += ns_since(t0);
         RTRACE(r, "applied", s1);

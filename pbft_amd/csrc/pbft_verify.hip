@@ -1427,6 +1427,54 @@ int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   return rc;
 }
 
+int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, const uint8_t* env, uint32_t n_env,
+                                  uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (N == 0 || !rows || !env || n_env == 0 || !out) return set_err(PBFT_EINVAL, "empty batch or null argument");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  c->staged = false;  // (as every host-buffer submit: a pending stage is void)
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = votes_begin(c, env, n_env, N, true);
+  if (rc) return rc;
+  c->in_flight = true;
+  c->async_out = out;
+  c->async_words = (N + 63) / 64;
+  rc = votes_launch(c, rows, rows + 32, (const uint16_t*)(rows + PBFT_VOTES_ROW_KEY),
+                    (const uint32_t*)(rows + PBFT_VOTES_ROW_ENV), ROW, N);
+  if (rc == PBFT_OK)
+    rc = hipEventRecord(c->ev_done, c->stream) == hipSuccess ? PBFT_OK : set_err(PBFT_EHIP, "event record");
+  if (rc) {  // the batch is lost: drain what was launched, the context stays usable
+    (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    (void)hipStreamSynchronize(c->cstream);
+    c->in_flight = false;
+    c->v_open = false;
+  }
+  return rc;
+}
+
+int pbft_host_alloc(pbft_ctx* c, size_t bytes, void** out) {
+  if (!out) return set_err(PBFT_EINVAL, "null argument");
+  *out = nullptr;
+  if (!c || bytes == 0) return set_err(PBFT_EINVAL, "null context or empty allocation");
+  HIP_TRY(hipSetDevice(c->device));
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return set_err(PBFT_ENOMEM, "pinned host alloc");
+  }
+  *out = p;
+  return PBFT_OK;
+}
+
+int pbft_host_free(pbft_ctx* c, void* p) {
+  if (!p) return PBFT_OK;
+  if (c) HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipHostFree(p));
+  return PBFT_OK;
+}
+
 int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   if (!c) return set_err(PBFT_EINVAL, "null context");
   if (c->in_flight && c->v_readback) {

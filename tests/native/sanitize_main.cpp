@@ -53,23 +53,34 @@ int pbft_verify_update_keys(pbft_ctx*, const uint32_t*, const uint8_t*, uint32_t
 // pbft_verify_poll_rows): exactly-sized staging, key_idx pre-set to a sentinel so that a chunk launched before
 // its rows were filled is caught, and one chunk of the library's schedule (PBFT_VOTES_CHUNK_END) "completing" per poll.  A row verifies iff its
 // signature's first byte is not 0xEE (no curve arithmetic: the point is the host's threads and bookkeeping).
+// pbft_verify_votes_submit_host (the replica's arena handed over as it is): the rows are read in place when each
+// chunk "lands" (a use after free of a busy arena is an ASan error) and hashed at submit and again at completion
+// (the replica must not write a busy arena).
 struct FakeGpu {
   std::vector<uint8_t> rows, env;  // staged rows of PBFT_VOTES_ROW_BYTES (include/pbft_verify.h), envelopes
-  uint16_t key(uint64_t i) const { uint16_t k; memcpy(&k, &rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY], 2); return k; }
-  uint32_t idx(uint64_t i) const { uint32_t x; memcpy(&x, &rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_ENV], 4); return x; }
+  const uint8_t* ext = nullptr;     // submit_host: the caller's rows
+  const uint8_t* base() const { return ext ? ext : rows.data(); }
+  uint16_t key(uint64_t i) const { uint16_t k; memcpy(&k, base() + (size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY, 2); return k; }
+  uint32_t idx(uint64_t i) const { uint32_t x; memcpy(&x, base() + (size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_ENV, 4); return x; }
   uint64_t N = 0, launched = 0, done = 0;
   uint32_t n_env = 0, n_keys = 0;
   uint64_t* out = nullptr;
   bool staged = false, open = false, in_flight = false;
-  uint64_t batches = 0, chunk_launches = 0;
+  uint64_t batches = 0, chunk_launches = 0, direct_batches = 0, ext_hash = 0;
   uint32_t lag = 1, polls = 0;  // polls per chunk landing (3 contexts: each slice is one chunk of the schedule)
 };
+static uint64_t fnv(const uint8_t* p, size_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < n; ++i) h = (h ^ p[i]) * 1099511628211ull;
+  return h;
+}
 
 extern "C" {
 int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_staging* st) {
   FakeGpu* g = (FakeGpu*)c;
   if (!g) return PBFT_ENODEV;
   CHECK(!g->in_flight);
+  g->ext = nullptr;
   g->rows.assign((size_t)PBFT_VOTES_ROW_BYTES * N, 0);
   for (uint64_t i = 0; i < N; ++i) memset(&g->rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY], 0xFF, 2);
   g->env.assign((size_t)PBFT_ENVELOPE_BYTES * n_env, 0);
@@ -104,14 +115,43 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   if (g->done < g->launched && ++g->polls % g->lag == 0) {  // one more chunk "lands"
     const uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
     for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
-    for (uint64_t i = g->done; i < hi; ++i)
-      if (g->rows[(size_t)PBFT_VOTES_ROW_BYTES * i] != 0xEE && g->key(i) < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
+    for (uint64_t i = g->done; i < hi; ++i) {
+      CHECK(g->idx(i) < g->n_env);
+      const uint8_t* sg = g->base() + (size_t)PBFT_VOTES_ROW_BYTES * i;
+      bool zero = true;  // (a row no candidate references: zero signature -- verifies as 0)
+      for (int b = 0; b < 64 && zero; ++b) zero = sg[b] == 0;
+      if (!zero && sg[0] != 0xEE && g->key(i) < g->n_keys) g->out[i / 64] |= 1ull << (i % 64);
+    }
     g->done = hi;
   }
   *rows_done = g->done;
   if (g->open || g->done < g->N) return 0;
+  if (g->ext) CHECK(fnv(g->ext, (size_t)PBFT_VOTES_ROW_BYTES * g->N) == g->ext_hash);  // untouched while in flight
   g->in_flight = false;
   return 1;
+}
+int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, const uint8_t* env, uint32_t n_env,
+                                  uint64_t* out) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && !g->in_flight && rows && env && n_env && out && N);
+  for (uint32_t e = 0; e < n_env; ++e) CHECK(memcmp(env + (size_t)PBFT_ENVELOPE_BYTES * e, "PBFT", 4) == 0);
+  g->staged = false;
+  g->ext = rows;
+  g->ext_hash = fnv(rows, (size_t)PBFT_VOTES_ROW_BYTES * N);
+  g->N = N; g->n_env = n_env; g->out = out;
+  g->open = false; g->in_flight = true; g->launched = N; g->done = 0;
+  ++g->batches;
+  ++g->direct_batches;
+  for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ++g->chunk_launches;
+  return 0;
+}
+int pbft_host_alloc(pbft_ctx*, size_t bytes, void** out) {
+  *out = malloc(bytes);
+  return *out ? 0 : PBFT_ENOMEM;
+}
+int pbft_host_free(pbft_ctx*, void* p) {
+  free(p);
+  return 0;
 }
 int pbft_verify_votes_submit(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
   int rc = pbft_verify_votes_submit_begin(c, N, n_env, out);
@@ -576,7 +616,9 @@ static void test_replica_async(const Keys& k) {
 // ---- 5. a large round through the GPU path (fake context above): the multithreaded fill launching chunk by
 // chunk, and the application of each chunk's rows while later chunks are "running" ------------------------------
 // n_ctx > 1: pbft_replica_create_multi over that many fake contexts (one slice of the batch each)
-static void test_replica_progressive(uint32_t n_ctx) {
+// many: the votes through pbft_replica_push_many (its threads' arena ranges), with 500 duplicates among them (rows
+// the threads reserved and left unused)
+static void test_replica_progressive(uint32_t n_ctx, bool many) {
   const uint32_t n = 256, seqs = 1100;  // 2 x 256 x 1100 + 1100 = 564,300 rows: 3 chunks
   std::vector<uint8_t> keys(32 * (size_t)n);
   for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = (uint8_t)(i >> 8); }
@@ -594,7 +636,14 @@ static void test_replica_progressive(uint32_t n_ctx) {
   uint8_t sg[64] = {1};
   for (uint32_t q = 1; q <= seqs; ++q)
     CHECK(pbft_replica_on_pre_prepare(r, 1, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
-  uint64_t bad = 0, pushed = 0;
+  uint64_t bad = 0, pushed = 0, dups = 0;
+  std::vector<uint8_t> mk, mdig, msig;
+  std::vector<uint64_t> mview, mseq;
+  std::vector<uint32_t> msigner;
+  auto add = [&](uint8_t kind, uint32_t q, uint32_t i) {
+    mk.push_back(kind); mview.push_back(1); mseq.push_back(q); msigner.push_back(i);
+    mdig.insert(mdig.end(), d, d + 64); msig.insert(msig.end(), sg, sg + 64);
+  };
   for (uint32_t q = 1; q <= seqs; ++q)
     for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})
       for (uint32_t i = 0; i < n; ++i) {
@@ -605,16 +654,28 @@ static void test_replica_progressive(uint32_t n_ctx) {
         sg[1] = (uint8_t)i;
         bad += forged;
         ++pushed;
-        CHECK(pbft_replica_push(r, kind, 1, q, d, i, sg) == 1);
+        if (!many) {
+          CHECK(pbft_replica_push(r, kind, 1, q, d, i, sg) == 1);
+          continue;
+        }
+        add(kind, q, i);
+        if (q % 2 == 0 && i == 17 && dups < 500) { add(kind, q, i); ++dups; }  // the same vote again: a duplicate
       }
+  if (many) {
+    uint64_t queued = 0;
+    CHECK(pbft_replica_push_many(r, mk.size(), mk.data(), mview.data(), mseq.data(), mdig.data(), msigner.data(),
+                                 msig.data(), &queued) == 0 && queued == pushed);
+  }
   uint64_t rows = 0;
   CHECK(pbft_replica_flush_submit(r, 0, &rows) == 0 && rows == pushed + seqs);
-  uint64_t staged = 0;
+  uint64_t staged = 0, direct = 0;
   for (const FakeGpu& x : gs) {
     CHECK(x.batches == 1 && x.chunk_launches >= (n_ctx > 1 ? 1u : 2u));  // every slice launched, in steps
     staged += x.N;
+    direct += x.direct_batches;
   }
-  CHECK(staged >= rows && staged < rows + 64 * n_ctx);  // + the padding that 64-aligns each slice
+  // + the padding that 64-aligns each slice (staging fill), or push_many's unused rows (the arena as it is)
+  CHECK(staged >= rows && staged < rows + 64 * n_ctx + dups);
   std::vector<pbft_round_event> ev(4 * seqs);
   uint32_t ne = 0;
   int polls = 0, st;
@@ -641,9 +702,23 @@ static void test_replica_progressive(uint32_t n_ctx) {
   pbft_replica_stats s;
   pbft_replica_get_stats(r, &s);
   CHECK(s.batches == 1 && s.accepted + s.rejected_sig <= pushed + seqs);
+  CHECK(s.verified == rows && s.duplicates == dups);
+  // a second round after the first: pushes go to the other arena (restarted), then back
+  for (uint32_t q = seqs + 1; q <= seqs + 40; ++q) {
+    CHECK(pbft_replica_on_pre_prepare(r, 1, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+    for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})
+      for (uint32_t i = 0; i < n; ++i) {
+        sg[0] = 1;
+        sg[1] = (uint8_t)(i + 3);
+        CHECK(pbft_replica_push(r, kind, 1, q, d, i, sg) == 1);
+      }
+  }
+  std::vector<pbft_round_event> ev2(200);
+  CHECK(pbft_replica_flush(r, 0, ev2.data(), (uint32_t)ev2.size(), &ne) == 0 && ne == 120);
   pbft_replica_destroy(r);
-  printf("replica progressive (%u contexts): %llu rows in %llu launch steps on context 0, %d polls, %u commits\n",
-         n_ctx, (unsigned long long)rows, (unsigned long long)g.chunk_launches, polls, committed);
+  printf("replica progressive (%u contexts, %s): %llu rows in %llu launch steps on context 0, %d polls, %u commits, "
+         "%llu direct batches\n", n_ctx, many ? "push_many" : "push", (unsigned long long)rows,
+         (unsigned long long)g.chunk_launches, polls, committed, (unsigned long long)direct);
 }
 
 int main() {
@@ -653,8 +728,10 @@ int main() {
   test_wire(rng);
   test_replica(k, rng);
   test_replica_async(k);
-  test_replica_progressive(1);
-  test_replica_progressive(3);
+  for (bool many : {false, true}) {
+    test_replica_progressive(1, many);
+    test_replica_progressive(3, many);
+  }
   printf("sanitized host run ok\n");
   return 0;
 }

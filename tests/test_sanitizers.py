@@ -34,9 +34,13 @@ def _build():
     subprocess.run(cmd, check=True, timeout=600)
 
 
-def test_host_code_clean_under_asan_ubsan():
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_host_code_clean_under_asan_ubsan(direct):
+    """direct 1: the replica's large batches go to the (fake) GPU as the row arena the pushes wrote; 0
+    (PBFT_REPLICA_DIRECT=0): through the staging fill, one slice per context."""
     _build()
     env = dict(os.environ)
+    env["PBFT_REPLICA_DIRECT"] = direct
     sym = "/opt/rocm/lib/llvm/bin/llvm-symbolizer"
     if os.path.exists(sym):
         env["ASAN_SYMBOLIZER_PATH"] = sym
@@ -45,3 +49,8 @@ def test_host_code_clean_under_asan_ubsan():
     assert p.returncode == 0, (p.returncode, p.stdout[-2000:], p.stderr[-4000:])
     assert "sanitized host run ok" in p.stdout
     assert "arithmetic: 120 accepted, 120 rejected" in p.stdout
+    lines = [l for l in p.stdout.splitlines() if l.startswith("replica progressive")]
+    assert len(lines) == 4
+    for l in lines:  # every context's batch the arena itself (direct), or none of them
+        n_ctx = int(l.split("(")[1].split()[0])
+        assert l.endswith(f"{n_ctx if direct == '1' else 0} direct batches"), l

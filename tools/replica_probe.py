@@ -18,6 +18,7 @@ def main():
     from pbft_amd import GpuBatchVerifier
     torch.cuda.set_device(0)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    n_ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 1
     seeds = bench.key_seeds(bench.N_REPLICAS)
     msg, key_idx = bench.envelopes(1, bench.SEQS, bench.N_REPLICAS)
     v = GpuBatchVerifier(0)
@@ -26,7 +27,8 @@ def main():
     expect = np.ones(len(msg), bool)
     expect[bad] = False
     assert v.set_keys(pub).all()
-    print(json.dumps(bench.replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=rounds)), flush=True)
+    print(json.dumps(bench.replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=rounds,
+                                               n_ctx=n_ctx)), flush=True)
     v.close()
 
 
