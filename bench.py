@@ -324,7 +324,8 @@ def votes_device_round(v, d, msg, expect, stream, torch, dev, iters: int = 50):
             "path": "device-resident votes form: envelope-schedule kernel + comb + finish per call"}
 
 
-def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9, n_ctx: int = 1):
+def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9, n_ctx: int = 1, modes=None,
+                      mode_env: str = "PBFT_REPLICA_DIRECT"):
     """config #4's round through the replica state machine (include/pbft_replica.h)
     on this GPU, the way a reference replica runs it, ingest included: ONE long-lived pbft_replica (n = 256; its
     windows are recycled from round to round, as a running replica's are) receives each round's 2048 signed
@@ -337,7 +338,9 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     covers seqs r * 2048 + 1 .. (r + 1) * 2048 (every round re-signed on the GPU: new envelopes); its bitmap
     pattern is the headline round's.  n_ctx > 1: pbft_replica_create_multi over the context and n_ctx - 1 clones
     (each context stages, launches and returns its own slice of the batch; on a node they would
-    be one context per GPU, each with its own PCIe link -- here they share this GPU and its link)."""
+    be one context per GPU, each with its own PCIe link -- here they share this GPU and its link).  modes: values of
+    an environment variable (mode_env, default PBFT_REPLICA_DIRECT) cycled round by round (an interleaved A/B in one
+    process; medians per mode in `by_mode`)."""
     import ctypes
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     from replica_sim import Event, Stats, lib
@@ -359,7 +362,10 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     assert L.pbft_replica_create_multi(ctxs, n_ctx, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
     st_prev = Stats()
     warm = 2  # rounds 0 and 1 size the replica's two row arenas (pushes alternate between them) and its windows
+    mode_of = []
     for r in range(rounds + warm):
+        if modes:
+            os.environ[mode_env] = modes[r % len(modes)]
         seq0 = 1 + r * n_seq
         m, _ = envelopes(seq0, n_seq, n_rep) if r else (msg, None)
         if r:
@@ -407,12 +413,20 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             res["total_ms"].append((t2 - t) * 1e3)
             res["polls"].append(polls)
             res["apply_ms"].append((st.apply_ns - st_prev.apply_ns) * 1e-6)
+            mode_of.append(modes[r % len(modes)] if modes else None)
         st_prev = st
+    if modes:
+        os.environ.pop(mode_env, None)
     L.pbft_replica_destroy(rep)
     for c in clones:
         c.close()
     med = {k: float(np.median(x)) for k, x in res.items()}
+    by_mode = None
+    if modes:
+        by_mode = {m: {k: float(np.median([x for x, mm in zip(v_, mode_of) if mm == m])) for k, v_ in res.items()}
+                   for m in sorted(set(modes))}
     return {"value": n / (med["total_ms"] * 1e-3), "unit": "verifies/s", "ms_per_round": med["total_ms"],
+            **({"by_mode": by_mode} if by_mode else {}),
             "ms_per_round_min_max": [float(np.min(res["total_ms"])), float(np.max(res["total_ms"]))],
             "push_many_ms": med["push_ms"], "flush_ms": med["flush_ms"],
             "flush_verifies_per_s": n / (med["flush_ms"] * 1e-3),

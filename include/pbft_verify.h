@@ -218,8 +218,9 @@ int pbft_verify_poll_rows(pbft_ctx *ctx, uint64_t *rows_done);
  * is pushed, so its flush touches no vote a second time. */
 int pbft_verify_votes_submit_host(pbft_ctx *ctx, const uint8_t *rows, uint64_t N, const uint8_t *envelopes,
                                   uint32_t n_env, uint64_t *bitmap_out);
-/* Pinned host memory the context's device (and the node's other GPUs) can DMA from: hipHostMalloc, portable and
- * mapped.  *out = NULL and PBFT_ENOMEM on failure.  Free with pbft_host_free (it may wait for the device). */
+/* Pinned host memory the context's device (and the node's other GPUs) can DMA from: anonymous pages registered
+ * with hipHostRegister (portable; the copy engine reads them faster than later hipHostMalloc buffers).  *out = NULL
+ * and PBFT_ENOMEM on failure.  Free with pbft_host_free (it may wait for the device). */
 int pbft_host_alloc(pbft_ctx *ctx, size_t bytes, void **out);
 int pbft_host_free(pbft_ctx *ctx, void *p);
 

@@ -156,8 +156,12 @@ struct Phase {
 // read-for-ownership of lines that are only written here and read next by the DMA engine (r04 A/B on MI355X boxes:
 // the flush's fill 1.1 -> 0.6 ms less of the calling thread's time).
 static const bool g_stream_stores = !(getenv("PBFT_STREAM_STORES") && atoi(getenv("PBFT_STREAM_STORES")) == 0);
-// PBFT_REPLICA_DIRECT=0: never hand a row arena to the GPU as it is (every batch filled into the staging: the r04 path)
-static const bool g_direct = !(getenv("PBFT_REPLICA_DIRECT") && atoi(getenv("PBFT_REPLICA_DIRECT")) == 0);
+// PBFT_REPLICA_DIRECT=0: never hand a row arena to the GPU as it is (every batch filled into the staging: the r04
+// path); read at every flush (A/B within one process)
+static bool direct_enabled() {
+  const char* e = getenv("PBFT_REPLICA_DIRECT");
+  return !(e && atoi(e) == 0);
+}
 
 // One staged row (include/pbft_verify.h: R || S, key_idx, two zero bytes, env_idx), streaming stores where available
 static inline void put_row(uint8_t* dst, const uint8_t* sig, uint32_t key, uint32_t env, bool nt) {
@@ -182,6 +186,8 @@ static inline void stream_fence() {
 
 struct Window {
   Phase ph[3];  // [0] PrePrepare candidates, [1] Prepare, [2] Commit
+  uint64_t push_call = 0;  // the last push_many that routed rows here, and the thread it gave the window to
+  uint32_t push_owner = 0;
   bool have_pre_prepare = false;
   Digest digest{};
   bool pre_prepared_reported = false, prepared_reported = false, committed_reported = false;
@@ -319,6 +325,7 @@ struct pbft_replica {
   uint32_t cur = 0;        // the arena pushes write to (never busy)
   uint32_t next_gen = 1;
   bool direct = false;     // the batch in flight is arena `busy_arena` as it is (rows = arena rows)
+  uint64_t push_calls = 0;  // threaded push_many calls (Window::push_call)
   uint32_t busy_arena = 0;
   uint64_t applied_upto = 0;  // rows_done at the last progressive application
   pbft_ctx* ctx = nullptr;         // ctxs[0]: digests, small batches
@@ -434,13 +441,21 @@ static Arena& push_arena(pbft_replica* r) {
 static inline const uint8_t* row_at(const pbft_replica* r, uint32_t rref) {
   return r->arena[rref >> 31].rows + ROWB * (rref & ROW_IDX);
 }
-// the first k candidates of p leave (their rows are dead from here on)
-static void release_rows(const pbft_replica* r, const Phase& p, size_t k) {
-  int64_t c[2] = {0, 0};
+// the first k candidates of p leave (their rows are dead from here on): counted into c[arena] (the caller
+// subtracts them from the arenas' live counts once -- one atomic per batch, not per phase: 16 threads updating one
+// cache line per segment cost the r05 apply ~0.5 ms), or subtracted at once
+static void count_rows(const Phase& p, size_t k, int64_t c[2]) {
   const size_t m = std::min(k, p.row.size());
   for (size_t i = 0; i < m; ++i) ++c[p.row[i] >> 31];
+}
+static void release_counts(const pbft_replica* r, const int64_t c[2]) {
   for (int a = 0; a < 2; ++a)
     if (c[a]) r->arena[a].live.fetch_sub(c[a], std::memory_order_relaxed);
+}
+static void release_rows(const pbft_replica* r, const Phase& p, size_t k) {
+  int64_t c[2] = {0, 0};
+  count_rows(p, k, c);
+  release_counts(r, c);
 }
 static void release_window(const pbft_replica* r, Window& w) {
   for (Phase& p : w.ph) {
@@ -541,16 +556,18 @@ static std::string key_str(const uint8_t* A) { return std::string((const char*)A
 
 static Window& window_at(pbft_replica* r, const Key& k) {
   if (r->last_w && r->last_key == k) return *r->last_w;
-  auto it = r->windows.find(k);
+  // (rounds arrive in ascending (view, seq): a key above the last window's is new and goes at the end, no search)
+  const bool above = r->windows.empty() || r->windows.rbegin()->first < k;
+  auto it = above ? r->windows.end() : r->windows.find(k);
   if (it == r->windows.end()) {
     if (!r->spare.empty()) {
       auto nh = std::move(r->spare.back());
       r->spare.pop_back();
       nh.key() = k;
       nh.mapped().reset();
-      it = r->windows.insert(std::move(nh)).position;
+      it = r->windows.insert(above ? r->windows.end() : r->windows.lower_bound(k), std::move(nh));
     } else {
-      it = r->windows.emplace(k, Window()).first;
+      it = r->windows.emplace_hint(above ? r->windows.end() : r->windows.lower_bound(k), k, Window());
     }
   }
   r->last_key = k;
@@ -713,13 +730,34 @@ static void revert_segs(pbft_replica* r) {
 // wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
 // candidates leave the windows.  Segments [s0, s1) (whole windows: a window's segments stay on one thread, in
 // order); counts into st[3] = accepted, rejected_sig, rejected_digest; touched[g] = some candidate accepted.
+static bool apply_prefetch() {  // PBFT_APPLY_PREFETCH=0: off (read per call: A/B in one process)
+  const char* e = getenv("PBFT_APPLY_PREFETCH");
+  return !(e && atoi(e) == 0);
+}
+static inline void prefetch_bytes(const void* p, size_t n) {
+  for (size_t o = 0; o < n; o += 64) __builtin_prefetch((const uint8_t*)p + o);
+}
+static void prefetch_phase(const Phase& p) {
+  const size_t k = p.size();
+  prefetch_bytes(p.who.data(), 2 * k);
+  prefetch_bytes(p.row.data(), 4 * k);
+  prefetch_bytes(p.st.data(), k);
+  prefetch_bytes(p.acc.data(), 4 * p.acc.size());
+  prefetch_bytes(p.cnt.data(), p.cnt.size());
+  if (!p.digs.empty()) prefetch_bytes(p.digs.data(), 64);
+}
 static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3], uint8_t* touched,
                         std::vector<pbft_round_event>& events) {
   std::vector<int64_t> amap;
   std::vector<uint8_t> mism;
   uint64_t st[3] = {0, 0, 0};  // local: the threads' st_out entries share cache lines
+  int64_t rel[2] = {0, 0};     // candidates leaving each arena (one atomic update per call)
+  const bool pf = apply_prefetch();
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
+    // the next segment's columns and per-signer arrays, fetched while this one is applied (a batch handed over as
+    // the arena reaches the application with them cold: nothing since the push has touched them)
+    if (pf && gi + 1 < s1 && !r->erased_in_flight) prefetch_phase(r->segs[gi + 1].w->ph[r->segs[gi + 1].kind]);
     Window* wp = g.w;
     if (r->erased_in_flight) {
       auto wi = r->windows.find(g.key);
@@ -801,7 +839,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
     }
     st[0] += acc_n;
     st[1] += g.count - acc_n;
-    release_rows(r, p, g.count);
+    count_rows(p, g.count, rel);
     p.drop_front(g.count);  // pushes that arrived during the flight stay, in order
     touched[gi] = acc_n > 0;
     // the window's last segment of this batch: its events are decided now, on this thread (segments come in
@@ -812,6 +850,7 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
       if (any) evaluate_window(r, g.key.first, g.key.second, w, events);
     }
   }
+  release_counts(r, rel);
   for (int k = 0; k < 3; ++k) st_out[k] += st[k];
 }
 
@@ -1431,15 +1470,18 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     RTRACE(r, "push_checked", T);
     std::vector<Run> runs;
     for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
-    std::unordered_map<Window*, uint32_t> owner;
-    owner.reserve(runs.size() < 8192 ? runs.size() : 8192);
+    const uint64_t call = ++r->push_calls;
     std::vector<uint64_t> t_rows(T, 0), t_envs(T, 64);
     for (Run& u : runs) {
-      u.w = &window_at(r, {r->current_view, u.seq});
-      auto ins = owner.emplace(u.w, (uint32_t)(u.lo * T / n_ok));
-      u.owner = ins.first->second;
+      Window& w = window_at(r, {r->current_view, u.seq});
+      u.w = &w;
+      if (w.push_call != call) {  // the window's first run in this call: its owner
+        w.push_call = call;
+        w.push_owner = (uint32_t)(u.lo * T / n_ok);
+        t_envs[w.push_owner] += 2;
+      }
+      u.owner = w.push_owner;
       t_rows[u.owner] += u.good;
-      if (ins.second) t_envs[u.owner] += 2;
     }
     Arena& A = push_arena(r);
     uint64_t rows_all = 0, envs_all = 0;
@@ -1507,12 +1549,6 @@ static uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
 static int submit_arena(pbft_replica* r, uint64_t N) {
   const uint32_t a = r->cur;
   Arena& A = r->arena[a];
-  for (Seg& g : r->segs) {
-    Phase& p = g.w->ph[g.kind];
-    g.row_end = p.row_hi;
-    memset(p.st.data(), V_IN_FLIGHT, g.count);
-    p.n_pending = 0;
-  }
   const uint64_t rows = A.n;
   r->rows = N;
   r->rows_span = rows;
@@ -1551,6 +1587,13 @@ static int submit_arena(pbft_replica* r, uint64_t N) {
     }
   }
   RTRACE(r, "launched", K);
+  // (after the launch: the copies start while this thread marks the batch's candidates)
+  for (Seg& g : r->segs) {
+    Phase& p = g.w->ph[g.kind];
+    g.row_end = p.row_hi;
+    memset(p.st.data(), V_IN_FLIGHT, g.count);
+    p.n_pending = 0;
+  }
   A.busy = true;
   r->busy_arena = a;
   r->direct = true;
@@ -1604,7 +1647,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     // the batch is exactly the current arena's candidates: the arena goes to the GPU as it is
     Arena& A = r->arena[r->cur];
     Arena& B = r->arena[r->cur ^ 1];
-    const bool direct = g_direct && r->ctx && !r->verify_fn && !r->vsub && A.rows_pinned && A.envs_pinned &&
+    const bool direct = direct_enabled() && r->ctx && !r->verify_fn && !r->vsub && A.rows_pinned && A.envs_pinned &&
                         A.clean.load() && A.gen && B.live.load() == 0 && !B.busy &&
                         (int64_t)N == A.live.load() && A.n <= N + std::max<uint64_t>(4096, N / 16);
     if (direct) return submit_arena(r, N);

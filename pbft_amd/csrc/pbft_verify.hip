@@ -11,6 +11,7 @@
 #include <dlfcn.h>
 #include <sched.h>
 #include <hip/hip_runtime.h>
+#include <sys/mman.h>
 #include <rccl/rccl.h>  // types only: librccl.so.1 is dlopen'ed by pbft_multi_create
 #include <stdio.h>
 #include <stdlib.h>
@@ -232,6 +233,8 @@ struct pbft_ctx {
   bool v_open = false;      // begun, not every chunk launched
   bool v_readback = false;  // progressive: each chunk's bitmap words come back on their own (ev_rows)
   std::vector<hipEvent_t> ev_rows;  // per chunk: its bitmap words are in h_bitmap
+  std::vector<uint64_t> v_ends;     // per launched chunk: its end row
+  bool v_short_tail = false;        // the batch's schedule ends with a VOTES_TAIL-row chunk (votes_chunk_end)
   uint64_t rows_out = 0;            // rows whose bitmap words are in the caller's bitmap
   uint64_t chunk_out = 0;           // chunks whose bitmap words are in the caller's bitmap
 };
@@ -751,7 +754,21 @@ static const uint8_t* zc_map(const pbft_ctx* c, const void* p, size_t bytes) {
 // votes_begin copies the envelope table and launches its schedule; votes_launch then launches every whole chunk
 // inside rows [0, rows) (all the rest once rows >= N): the kernels of chunk c run on the context stream after
 // its copies (copy stream), overlapping the copies of chunk c+1.
-static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t N, bool readback) {
+// Chunk schedule of a votes batch: PBFT_VOTES_CHUNK_END, or (v_short_tail: rows that are all in host memory when
+// the batch starts, pbft_verify_votes_submit_host) the same with its last chunk cut down to ~VOTES_TAIL rows -- what
+// is left once the last copy lands is that chunk's kernels and the caller's application of its rows
+// (r05: the replica's flush ended with 64k rows of both).
+static constexpr uint64_t VOTES_TAIL = 16384;
+static uint64_t votes_chunk_end(const pbft_ctx* c, uint64_t lo, uint64_t N) {
+  const uint64_t e = PBFT_VOTES_CHUNK_END(lo, N);
+  if (c->v_short_tail && e == N && N > VOTES_CHUNK && N - lo > VOTES_TAIL + 64) return lo + ((N - lo - VOTES_TAIL) & ~(uint64_t)63);
+  return e;
+}
+
+static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t N, bool readback,
+                       bool short_tail = false) {
+  c->v_short_tail = short_tail;
+  c->v_ends.clear();
   const uint64_t words = (N + 63) / 64;
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
   const uint64_t ch = N < VOTES_CHUNK ? N : VOTES_CHUNK;
@@ -768,7 +785,7 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   }
   if (readback) {
     uint64_t chunks = 0;
-    for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ++chunks;
+    for (uint64_t lo = 0; lo < N; lo = votes_chunk_end(c, lo, N)) ++chunks;
     while (c->ev_rows.size() < chunks) {
       hipEvent_t e;
       HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -811,9 +828,10 @@ static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const u
                         uint32_t rs_stride, uint64_t rows) {
   const uint64_t N = c->v_n;
   const votes_layout L(N < VOTES_CHUNK ? N : VOTES_CHUNK);
-  while (c->v_next < N && (rows >= N || PBFT_VOTES_CHUNK_END(c->v_next, N) <= rows)) {
+  while (c->v_next < N && (rows >= N || votes_chunk_end(c, c->v_next, N) <= rows)) {
     const uint64_t lo = c->v_next;
-    const uint64_t n = PBFT_VOTES_CHUNK_END(lo, N) - lo;
+    const uint64_t n = votes_chunk_end(c, lo, N) - lo;
+    c->v_ends.push_back(lo + n);
     const int b = (int)(c->v_chunk % VOTES_BUFS);
     const int slot = c->v_two ? (int)(c->v_chunk & 1) : 0;
     hipStream_t st = slot ? c->stream2 : c->stream;
@@ -1435,7 +1453,7 @@ int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, 
   if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
   c->staged = false;  // (as every host-buffer submit: a pending stage is void)
   HIP_TRY(hipSetDevice(c->device));
-  int rc = votes_begin(c, env, n_env, N, true);
+  int rc = votes_begin(c, env, n_env, N, true, true);
   if (rc) return rc;
   c->in_flight = true;
   c->async_out = out;
@@ -1454,15 +1472,25 @@ int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, 
   return rc;
 }
 
+// Anonymous pages pinned with hipHostRegister rather than hipHostMalloc: on the MI355X boxes the copy engine reads
+// them at 56.5 GB/s wherever they are placed, while hipHostMalloc buffers after a process's first one read at 46-50
+// GB/s (tools/microbench/pinned_write.cpp, numa_h2d.cpp; profiles/r05/pinned_h2d.txt).  One header page in front
+// holds the mapping's length for pbft_host_free.
+static constexpr size_t HOST_HDR = 4096;
 int pbft_host_alloc(pbft_ctx* c, size_t bytes, void** out) {
   if (!out) return set_err(PBFT_EINVAL, "null argument");
   *out = nullptr;
   if (!c || bytes == 0) return set_err(PBFT_EINVAL, "null context or empty allocation");
   HIP_TRY(hipSetDevice(c->device));
-  void* p = nullptr;
-  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+  const size_t len = HOST_HDR + ((bytes + 4095) & ~(size_t)4095);
+  void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (m == MAP_FAILED) return set_err(PBFT_ENOMEM, "host mmap");
+  memcpy(m, &len, sizeof len);
+  uint8_t* p = (uint8_t*)m + HOST_HDR;
+  if (hipHostRegister(p, len - HOST_HDR, hipHostRegisterPortable) != hipSuccess) {
     (void)hipGetLastError();
-    return set_err(PBFT_ENOMEM, "pinned host alloc");
+    munmap(m, len);
+    return set_err(PBFT_ENOMEM, "pinned host register");
   }
   *out = p;
   return PBFT_OK;
@@ -1471,7 +1499,11 @@ int pbft_host_alloc(pbft_ctx* c, size_t bytes, void** out) {
 int pbft_host_free(pbft_ctx* c, void* p) {
   if (!p) return PBFT_OK;
   if (c) HIP_TRY(hipSetDevice(c->device));
-  HIP_TRY(hipHostFree(p));
+  uint8_t* m = (uint8_t*)p - HOST_HDR;
+  size_t len;
+  memcpy(&len, m, sizeof len);
+  HIP_TRY(hipHostUnregister(p));
+  munmap(m, len);
   return PBFT_OK;
 }
 
@@ -1486,7 +1518,7 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
         c->v_open = false;
         HIP_TRY(e);
       }
-      const uint64_t hi = PBFT_VOTES_CHUNK_END(c->rows_out, c->v_n);
+      const uint64_t hi = c->v_ends[c->chunk_out];
       memcpy(c->async_out + c->rows_out / 64, c->h_bitmap + c->rows_out / 64, (hi - c->rows_out + 63) / 64 * 8);
       c->rows_out = hi;
       ++c->chunk_out;

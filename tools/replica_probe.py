@@ -19,6 +19,12 @@ def main():
     torch.cuda.set_device(0)
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     n_ctx = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+    modes, mode_env = None, "PBFT_REPLICA_DIRECT"
+    if len(sys.argv) > 3:
+        spec = sys.argv[3]
+        if "=" in spec:
+            mode_env, spec = spec.split("=", 1)
+        modes = spec.split(",")
     seeds = bench.key_seeds(bench.N_REPLICAS)
     msg, key_idx = bench.envelopes(1, bench.SEQS, bench.N_REPLICAS)
     v = GpuBatchVerifier(0)
@@ -28,7 +34,7 @@ def main():
     expect[bad] = False
     assert v.set_keys(pub).all()
     print(json.dumps(bench.replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=rounds,
-                                               n_ctx=n_ctx)), flush=True)
+                                               n_ctx=n_ctx, modes=modes, mode_env=mode_env)), flush=True)
     v.close()
 
 
