@@ -297,7 +297,9 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *                                 batch size (8 up to 8,192 signatures, else 4)
  *   PBFT_OPT_FINISH_WAVES         product-tree finish compiled for 1 wave per SIMD (widths 1-16, X/Y/Z prefetched)
  *                                 or 2 (widths 1, 2, 4, 8; width 1 prefetched); any other value = by batch size
- *   PBFT_OPT_KERNEL_TIMING        1 (default): two HIP events bracket every launch for pbft_last_kernel_ms; 0: none
+ *   PBFT_OPT_KERNEL_TIMING        1: two HIP events bracket every launch for pbft_last_kernel_ms; 0 (default since
+ *                                 r05: the two event records cost ~7.5 us per launch, 4.5 % of an 8-GPU shard): none,
+ *                                 and pbft_last_kernel_ms returns -1
  *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers)
  *   PBFT_OPT_VOTES_ZERO_COPY      1: votes rows that sit in the context's pinned staging (pbft_verify_votes_stage
  *                                 / _submit_begin, the replica's flush, pageable inputs copied there) are read by

@@ -168,7 +168,9 @@ struct pbft_ctx {
   int comb_fuse = 0;                   // the finish inside the chain-form comb launch: 1, 0, -1 by size
                                        // (PBFT_OPT_COMB_FUSE)
   int cus = 0;                         // compute units of the device
-  bool timing = true;                  // ev0 / ev1 around every launch (pbft_last_kernel_ms)
+  // ev0 / ev1 around every launch (pbft_last_kernel_ms).  Off by default since r05: the two event records cost 7.5 us
+  // per comb + finish pair, 4.5 % of the 131k shard (profiles/r05/shard/timing_events.txt)
+  bool timing = false;
   uint64_t key_budget_mb = 0;          // key-table budget override (0 = env / default)
   pbft_key_stats kstats{};             // the last pbft_verify_set_keys / _update_keys (pbft_verify_key_stats)
   int fault_inject = 0;                // PBFT_OPT_FAULT_INJECT (tests): fail the next pbft_verify_update_keys

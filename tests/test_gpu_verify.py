@@ -397,6 +397,8 @@ def test_device_entry_point(gv, golden):
         dB = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
         st = torch.cuda.Stream(dev)
         torch.cuda.synchronize()
+        assert gv.last_kernel_ms() == -1  # (timing events are off by default since r05)
+        gv.set_option(gv.OPT_KERNEL_TIMING, 1)
         with torch.cuda.stream(st):
             gv.verify_device(dR.data_ptr(), dS.data_ptr(), dK.data_ptr(), dM.data_ptr(), 85, stride, n,
                              dB.data_ptr(), st.cuda_stream)
@@ -419,7 +421,7 @@ def test_device_entry_point(gv, golden):
                 bm = gv.verify(SigBatch(b["R"], b["S"], b["key_idx"], b["msg"], 85))
                 assert (bitmap_to_bool(bm, n) == b["expected"].astype(bool)).all()
         finally:
-            gv.set_option(gv.OPT_KERNEL_TIMING, 1)
+            gv.set_option(gv.OPT_KERNEL_TIMING, 0)
 
 
 def test_digests_match_hashlib(gv):
