@@ -107,14 +107,15 @@ def test_gpu_phase_ordered_rounds_async_flush(gpu_cluster):
     c.close()
 
 
-@pytest.mark.parametrize("n_ctx", [1, 3])
-def test_gpu_replica_2p20_round(gpu_cluster, n_ctx):
+@pytest.mark.parametrize("n_ctx,direct", [(1, "1"), (3, "1"), (1, "0"), (3, "0")])
+def test_gpu_replica_2p20_round(gpu_cluster, n_ctx, direct, monkeypatch):
     """Config #4's round through one replica on the GPU: n = 256, 2048 seqs, 2^20 GPU-signed votes + 2048
-    PrePrepares pushed, ONE flush_submit (votes form into the pinned staging), polled to completion; the windows
-    whose quorum was broken by corrupted votes neither prepare nor commit, every other one commits.  n_ctx = 3:
-    pbft_replica_create_multi over the context and two clones (a slice of the batch per context,
-    each staged, launched and applied on its own -- one GPU here, one per GPU on a node): the same events and
-    counters."""
+    PrePrepares pushed, ONE flush_submit, polled to completion; the windows whose quorum was broken by corrupted votes
+    neither prepare nor commit, every other one commits.  n_ctx = 3: pbft_replica_create_multi over the context and
+    two clones (a slice of the batch per context, each launched and applied on its own -- one GPU
+    here, one per GPU on a node): the same events and counters.  direct "1": the replica's row arena (written at push
+    time) goes to the GPU as it is (r05); "0" (PBFT_REPLICA_DIRECT=0): the staging fill."""
+    monkeypatch.setenv("PBFT_REPLICA_DIRECT", direct)
     import ctypes
     import hashlib
     import time
