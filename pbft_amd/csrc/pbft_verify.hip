@@ -1307,16 +1307,25 @@ int pbft_verify_batch_async(pbft_ctx* c, const uint8_t* R, const uint8_t* S, con
 // wait (spin briefly, then sleep on the completion interrupt) sometimes wakes milliseconds late.  A serving
 // thread that waits for its batch is latency-critical, so it polls (yielding the core between polls) -- the same
 // thing the replica's flush_poll and the bench's poll loops do.  PBFT_SPIN_WAIT=0 restores hipEventSynchronize.
+// The core is yielded only once a wait has lasted 2 ms: a sched_yield that lets another runnable thread in gives the
+// core back a scheduler tick later, and the back-to-back leg's 1.05-ms maxima were exactly that (interleaved
+// processes on one box, profiles/r05/stream_spin.txt: yielding every 64 polls, max 0.37-1.05 ms; never, 0.21-0.53).
+// PBFT_SPIN_WAIT=2: never yield; =3: yield every 64 polls (the first r05 form).
 static hipError_t wait_event(hipEvent_t e) {
-  static const bool spin = [] {
+  static const long spin = [] {
     const char* v = getenv("PBFT_SPIN_WAIT");
-    return !v || strtol(v, nullptr, 10) != 0;
+    return v ? strtol(v, nullptr, 10) : 1L;
   }();
   if (!spin) return hipEventSynchronize(e);
+  const auto t0 = std::chrono::steady_clock::now();
+  bool polite = spin == 3;
   for (uint32_t k = 0;; ++k) {
     const hipError_t q = hipEventQuery(e);
     if (q != hipErrorNotReady) return q;
-    if ((k & 63) == 63) sched_yield();
+    if ((k & 63) == 63) {
+      if (!polite && spin == 1 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) polite = true;
+      if (polite) sched_yield();
+    }
   }
 }
 
