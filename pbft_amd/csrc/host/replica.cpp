@@ -1823,30 +1823,34 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
   return 1;
 }
 
+// Blocking flush: poll until done, so that each chunk is applied as it lands (as the non-blocking form's caller
+// does) instead of waiting for the whole batch first; the polling thread keeps its core for the first 2 ms of a
+// wait and yields after that (the library's own waits do the same: pbft_verify_wait).
+struct Backoff {
+  std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+  uint32_t k = 0;
+  void pause() {
+    if ((++k & 63) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) std::this_thread::yield();
+  }
+};
 int pbft_replica_flush(pbft_replica* r, int force, pbft_round_event* events, uint32_t max_events,
                        uint32_t* n_events) {
   if (!r) return PBFT_EINVAL;
   if (n_events) *n_events = 0;
   // a batch submitted earlier completes first (its events are queued, not lost)
+  Backoff b0;
   while (r->in_flight) {
-    if (r->in_flight_via == 0 && r->slice_lo.empty()) {
-      const int w = pbft_verify_wait(r->ctx);
-      if (w < 0) { revert_segs(r); return w; }
-    }
     const int p = pbft_replica_flush_poll(r, nullptr, 0, nullptr);
     if (p < 0) return p;
-    if (p == 0) std::this_thread::yield();
+    if (p == 0) b0.pause();
   }
   int rc = pbft_replica_flush_submit(r, force, nullptr);
   if (rc) return rc;
+  Backoff b1;
   for (;;) {
-    if (r->in_flight && r->in_flight_via == 0 && r->slice_lo.empty()) {  // (a multi-context batch: polled)
-      const int w = pbft_verify_wait(r->ctx);
-      if (w < 0) { revert_segs(r); return w; }
-    }
     const int p = pbft_replica_flush_poll(r, events, max_events, n_events);
     if (p != 0) return p < 0 ? p : PBFT_OK;
-    std::this_thread::yield();
+    b1.pause();
   }
 }
 
