@@ -817,6 +817,60 @@ def test_progressive_votes_submit(gv, coracle):
     assert (bitmap_to_bool(gv.verify_votes(R, S, K, ei, env), len(R)) == exp).all()
 
 
+@pytest.mark.parametrize("N", [1, 4095, 65536 + 77, (1 << 18) + 1, (1 << 19) + 4099])
+def test_votes_submit_host_rows(gv, coracle, N):
+    """pbft_verify_votes_submit_host (r05: the replica's row arena handed over as it is): staged rows and the
+    envelope table in the caller's pinned memory (pbft_host_alloc), the whole batch launched at once -- the chunk
+    schedule with its last chunk cut to 16k rows above 2^18 rows -- and completed progressively
+    (pbft_verify_poll_rows: every reported prefix equals the oracle).  Ragged sizes from one row to 2^19 + 4099;
+    every adversarial class; argument errors; the context serves an ordinary batch afterwards."""
+    import ctypes
+    from pbft_amd import bitmap_to_bool
+    seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=53)   # 65,536 signatures
+    assert gv.set_keys(pub).all()
+    rng = np.random.default_rng(53)
+    R, S, K, M, _ = adversarial(rng, pub, R, S, key_idx, msg)
+    exp = oracle_bits(coracle, pub, R, S, K, M, 85)
+    env, inv = np.unique(M, axis=0, return_inverse=True)
+    ei = inv.reshape(-1).astype(np.uint32)
+    reps = N // len(R) + 1
+    RR, SS, KK, II, EE = (np.concatenate([a] * reps)[:N] for a in (R, S, K, ei, exp))
+    L, ctx = gv._lib, gv._ctx
+    hr, he = ctypes.c_void_p(), ctypes.c_void_p()
+    assert L.pbft_host_alloc(ctx, 72 * N, ctypes.byref(hr)) == 0 and hr.value
+    assert L.pbft_host_alloc(ctx, 85 * len(env) + 16, ctypes.byref(he)) == 0 and he.value
+    try:
+        rows = np.ctypeslib.as_array((ctypes.c_uint8 * (72 * N)).from_address(hr.value)).reshape(N, 72)
+        envs = np.ctypeslib.as_array((ctypes.c_uint8 * (85 * len(env))).from_address(he.value)).reshape(-1, 85)
+        rows[:, :32], rows[:, 32:64] = RR, SS
+        rows[:, 64:68] = np.stack([KK.astype(np.uint16).view(np.uint8).reshape(N, 2)[:, 0],
+                                   KK.astype(np.uint16).view(np.uint8).reshape(N, 2)[:, 1],
+                                   np.zeros(N, np.uint8), np.zeros(N, np.uint8)], axis=1)
+        rows[:, 68:72] = II.view(np.uint8).reshape(N, 4)
+        envs[:] = env
+        out = np.zeros((N + 63) // 64, np.uint64)
+        # argument errors: nothing launched
+        assert L.pbft_verify_votes_submit_host(ctx, hr, 0, he, len(env), out.ctypes.data) != 0
+        assert L.pbft_verify_votes_submit_host(ctx, None, N, he, len(env), out.ctypes.data) != 0
+        assert L.pbft_verify_votes_submit_host(ctx, hr, N, he, 0, out.ctypes.data) != 0
+        assert L.pbft_verify_votes_submit_host(ctx, hr, N, he, len(env), out.ctypes.data) == 0
+        assert L.pbft_verify_votes_submit_host(ctx, hr, N, he, len(env), out.ctypes.data) != 0   # busy
+        rows_done = ctypes.c_uint64()
+        prev = 0
+        while True:
+            rc = L.pbft_verify_poll_rows(ctx, ctypes.byref(rows_done))
+            assert rc in (0, 1) and rows_done.value >= prev
+            prev = rows_done.value
+            k = min(prev, N) // 64 * 64
+            assert (bitmap_to_bool(out[: k // 64], k) == EE[:k]).all()
+            if rc == 1:
+                break
+        assert prev >= N and (bitmap_to_bool(out, N) == EE).all()
+    finally:
+        assert L.pbft_host_free(ctx, hr) == 0 and L.pbft_host_free(ctx, he) == 0
+    assert (bitmap_to_bool(gv.verify_votes(R[:4096], S[:4096], K[:4096], ei[:4096], env), 4096) == exp[:4096]).all()
+
+
 def test_votes_zero_copy_equals_copied(gv, coracle):
     """PBFT_OPT_VOTES_ZERO_COPY (r04, off by default: slower): votes rows in the context's pinned staging are read
     by the kernels in place over PCIe (the comb leaves an HBM copy of R for the finish) instead of being copied to
