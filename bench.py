@@ -825,8 +825,10 @@ def main():
     # fin_stream); sequential, ONE pair around the whole timed region -- a pair per step adds two timestamp packets
     # between the launches (the finish -> next comb gap grew from ~11 to ~20 us, profiles/r04/shard/), so the
     # launch pair's average is the region's time / K (the ~11-us gap between launches included)
-    # (N > 1: per step as well, so that the all-gather on the same stream stays outside the kernels' time)
-    per_step = pipelined or ws > 1
+    # (N > 1: the region holds the all-gathers too; the kernels' own time is taken after it, untimed for `value`,
+    # rather than by an event pair per step inside it -- two event records cost ~7.5 us per step on the GPU,
+    # profiles/r05/shard/timing_events.txt, 4-5 % of an 8-GPU step)
+    per_step = pipelined
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps if per_step else 1)]
     if ws > 1:
@@ -847,6 +849,8 @@ def main():
         kern_avg = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # pipelined: the comb kernel
     else:
         kern_avg = evs[0][0].elapsed_time(evs[0][1]) / args.steps  # the comb + finish pair
+    if ws > 1 and not per_step and n:
+        kern_avg = time_device(v, stream, d, n, args.steps, torch)[0]  # this rank's launch pairs without the gathers
     if ws > 1:
         t = torch.tensor([dt], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
