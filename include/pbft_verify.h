@@ -218,6 +218,20 @@ int pbft_verify_poll_rows(pbft_ctx *ctx, uint64_t *rows_done);
  * is pushed, so its flush touches no vote a second time. */
 int pbft_verify_votes_submit_host(pbft_ctx *ctx, const uint8_t *rows, uint64_t N, const uint8_t *envelopes,
                                   uint32_t n_env, uint64_t *bitmap_out);
+/* A votes batch in pieces, for rows that are still being written while the first ones are verified
+ * (pbft_replica_push_many launches each part of the replica's row arena as its worker threads finish it):
+ * _open(n_cap, env_cap, bitmap_out) starts a batch of at most n_cap rows over at most env_cap envelopes; each
+ * _piece(rows, row_lo, row_hi, envelopes, env_lo, env_hi) copies envelopes [env_lo, env_hi) (their block-2
+ * schedules computed on the GPU) and launches rows [row_lo, row_hi) -- rows and envelopes addressed from the same
+ * base pointers in every call, pinned (pbft_host_alloc), unchanged until the batch completes; pieces in order and
+ * contiguous (row_lo = the previous row_hi, a multiple of 64; env_lo = the previous env_hi), a row may name any
+ * envelope below its piece's env_hi; _close(n) ends the batch at n rows (= the last row_hi).  Completes like the
+ * progressive form: pbft_verify_poll_rows reports each chunk's bitmap words as they land (also while the batch is
+ * open); pbft_verify_wait refuses an open batch (PBFT_EBUSY).  A failing _piece or _close drops the batch. */
+int pbft_verify_votes_open(pbft_ctx *ctx, uint64_t n_cap, uint32_t env_cap, uint64_t *bitmap_out);
+int pbft_verify_votes_piece(pbft_ctx *ctx, const uint8_t *rows, uint64_t row_lo, uint64_t row_hi,
+                            const uint8_t *envelopes, uint32_t env_lo, uint32_t env_hi);
+int pbft_verify_votes_close(pbft_ctx *ctx, uint64_t n);
 /* Pinned host memory the context's device (and the node's other GPUs) can DMA from: anonymous pages registered
  * with hipHostRegister (portable; the copy engine reads them faster than later hipHostMalloc buffers).  *out = NULL
  * and PBFT_ENOMEM on failure.  Free with pbft_host_free (it may wait for the device). */

@@ -184,6 +184,10 @@ extern "C" {
     pub fn pbft_verify_poll_rows(ctx: *mut pbft_ctx, rows_done: *mut u64) -> c_int;
     pub fn pbft_verify_votes_submit_host(ctx: *mut pbft_ctx, rows: *const u8, n: u64, envelopes: *const u8,
                                          n_env: u32, bitmap_out: *mut u64) -> c_int;
+    pub fn pbft_verify_votes_open(ctx: *mut pbft_ctx, n_cap: u64, env_cap: u32, bitmap_out: *mut u64) -> c_int;
+    pub fn pbft_verify_votes_piece(ctx: *mut pbft_ctx, rows: *const u8, row_lo: u64, row_hi: u64,
+                                   envelopes: *const u8, env_lo: u32, env_hi: u32) -> c_int;
+    pub fn pbft_verify_votes_close(ctx: *mut pbft_ctx, n: u64) -> c_int;
     pub fn pbft_host_alloc(ctx: *mut pbft_ctx, bytes: usize, out: *mut *mut c_void) -> c_int;
     pub fn pbft_host_free(ctx: *mut pbft_ctx, p: *mut c_void) -> c_int;
     pub fn pbft_multi_create(ctxs: *const *mut pbft_ctx, n_ctx: u32, out: *mut *mut pbft_multi) -> c_int;

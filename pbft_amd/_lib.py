@@ -93,6 +93,9 @@ def load() -> ctypes.CDLL:
         "pbft_verify_poll_rows": (i32, [vp, ctypes.POINTER(u64)]),
         "pbft_verify_votes_submit_host": (i32, [vp, vp, u64, vp, u32, vp]),
         "pbft_host_alloc": (i32, [vp, ctypes.c_size_t, ctypes.POINTER(vp)]),
+        "pbft_verify_votes_open": (i32, [vp, u64, u32, vp]),
+        "pbft_verify_votes_piece": (i32, [vp, vp, u64, u64, vp, u32, u32]),
+        "pbft_verify_votes_close": (i32, [vp, u64]),
         "pbft_host_free": (i32, [vp, vp]),
         "pbft_multi_create": (i32, [vp, u32, ctypes.POINTER(vp)]),
         "pbft_multi_destroy": (i32, [vp]),

@@ -47,7 +47,6 @@ namespace {
 using Key = std::pair<uint64_t, uint64_t>;  // (view, seq)
 using Digest = std::array<uint8_t, 64>;
 
-enum : uint8_t { V_PENDING = 0, V_IN_FLIGHT = 1 };
 
 // Candidates of one kind in one round window, as columns in push order (a candidate leaves when its batch
 // completes, so between batches every candidate is pending and a batch takes a whole phase).  A candidate's
@@ -61,7 +60,6 @@ struct Phase {
   std::vector<uint32_t> row;  // [k] the candidate's row reference
   std::vector<uint16_t> who;  // signer
   std::vector<uint32_t> dix;  // index into digs
-  std::vector<uint8_t> st;    // V_PENDING / V_IN_FLIGHT
   std::vector<Digest> digs;   // distinct digests of the candidates (honest rounds: one)
   std::vector<uint32_t> denv, dgen;  // per digest: its envelope in the arena of generation dgen (row env_idx)
   std::vector<uint8_t> cnt;   // per signer: candidates
@@ -70,6 +68,7 @@ struct Phase {
   std::vector<uint32_t> acc_cnt;  // signers per accepted digest
   uint32_t distinct = 0;          // signers with an accepted vote or a candidate
   uint32_t n_pending = 0;         // candidates not yet in a batch
+  uint32_t n_flight = 0;          // the first n_flight candidates are in the batch in flight
   uint64_t row_hi = 0;            // 1 + the largest row index of the candidates
   size_t size() const { return who.size(); }
   void init(uint32_t n) {
@@ -97,7 +96,6 @@ struct Phase {
     row.push_back(rref);
     who.push_back((uint16_t)signer);
     dix.push_back(j < 0 ? (uint32_t)digs.size() - 1 : (uint32_t)j);
-    st.push_back(V_PENDING);
     ++n_pending;
     if ((rref & ROW_IDX) + 1 > row_hi) row_hi = (rref & ROW_IDX) + 1;
   }
@@ -110,7 +108,7 @@ struct Phase {
     row.erase(row.begin(), row.begin() + k);
     who.erase(who.begin(), who.begin() + k);
     dix.erase(dix.begin(), dix.begin() + k);
-    st.erase(st.begin(), st.begin() + k);
+    n_flight = n_flight > k ? n_flight - (uint32_t)k : 0;
     std::vector<Digest> nd;
     std::vector<uint32_t> ne, ng;
     for (uint32_t& x : dix) {
@@ -126,8 +124,9 @@ struct Phase {
     for (uint32_t x : row) row_hi = std::max<uint64_t>(row_hi, (x & ROW_IDX) + 1);
   }
   void clear_columns() {
-    row.clear(); who.clear(); dix.clear(); st.clear(); digs.clear(); denv.clear(); dgen.clear();
+    row.clear(); who.clear(); dix.clear(); digs.clear(); denv.clear(); dgen.clear();
     row_hi = 0;
+    n_flight = 0;
   }
   void clear_candidates() {
     clear_columns();
@@ -326,8 +325,19 @@ struct pbft_replica {
   uint32_t next_gen = 1;
   bool direct = false;     // the batch in flight is arena `busy_arena` as it is (rows = arena rows)
   uint64_t push_calls = 0;  // threaded push_many calls (Window::push_call)
+  // push_many's early batch (r05): the current arena's rows verified in pieces while they are pushed
+  // (pbft_verify_votes_open / _piece / _close); flush_submit adopts it when the arena is unchanged since
+  struct {
+    bool active = false;  // a batch covers arena `arena` rows [0, rows) and envelopes [0, envs); bits -> bitmap
+    bool done = false;    // waited for: every bit is in r->bitmap
+    uint32_t arena = 0;
+    uint64_t rows = 0;
+    uint32_t envs = 0;
+  } eu;
   uint32_t busy_arena = 0;
   uint64_t applied_upto = 0;  // rows_done at the last progressive application
+  bool adopted = false;       // the batch in flight is push_many's early batch: applied once, when done (its rows
+                              // lie part by part, so a landed prefix of rows is no prefix of the windows)
   pbft_ctx* ctx = nullptr;         // ctxs[0]: digests, small batches
   std::vector<pbft_ctx*> ctxs;     // pbft_replica_create_multi: large batches split over these (one per GPU)
   uint32_t n = 0, f = 0, self = 0;
@@ -375,6 +385,27 @@ static uint32_t primary_of(const pbft_replica* r, uint64_t view) { return (uint3
 
 // ---- row arenas ----
 static constexpr size_t ROWB = PBFT_VOTES_ROW_BYTES;
+// ---- push_many's early batch ----
+static bool early_enabled() {  // PBFT_REPLICA_EARLY=0: push_many never launches (read per call: A/B in one process)
+  const char* e = getenv("PBFT_REPLICA_EARLY");
+  return !(e && atoi(e) == 0);
+}
+// wait for the early batch (the context is needed, or its arena is about to change); its bits stay adoptable
+static int eu_settle(pbft_replica* r) {
+  if (!r->eu.active || r->eu.done) return PBFT_OK;
+  const int rc = pbft_verify_wait(r->ctx);
+  if (rc) {
+    r->eu.active = false;  // lost: the flush verifies the rows again
+    return rc;
+  }
+  r->eu.done = true;
+  return PBFT_OK;
+}
+static void eu_drop(pbft_replica* r) {
+  (void)eu_settle(r);
+  r->eu.active = false;
+}
+
 static void* host_mem(pbft_replica* r, size_t bytes, bool* pinned) {
   void* p = nullptr;
   *pinned = false;
@@ -391,6 +422,8 @@ static void host_mem_free(pbft_replica* r, void* p, bool pinned) {
 }
 // room for `rows` more rows and `envs` more envelopes (the current arena only: never busy)
 static bool arena_reserve(pbft_replica* r, Arena& a, uint64_t rows, uint64_t envs) {
+  if ((a.n + rows > a.cap || a.ne + envs > a.ecap) && r->eu.active && &r->arena[r->eu.arena] == &a)
+    eu_drop(r);  // (the early batch's copies read this arena: finished before it moves)
   if (a.n + rows > a.cap) {
     if (a.n + rows > ROW_IDX) return false;
     const uint64_t c = std::min<uint64_t>(ROW_IDX, std::max<uint64_t>({2 * a.cap, a.n + rows, 1u << 12}));
@@ -421,6 +454,7 @@ static bool arena_reserve(pbft_replica* r, Arena& a, uint64_t rows, uint64_t env
 // references (push_many's unused tails)
 static const uint8_t g_zero_digest[64] = {0};
 static void arena_restart(pbft_replica* r, Arena& a) {
+  if (r->eu.active && &r->arena[r->eu.arena] == &a) eu_drop(r);
   a.n = 0;
   a.ne = 0;
   a.gen = r->next_gen++;
@@ -714,8 +748,9 @@ static void revert_segs(pbft_replica* r) {
     auto wi = r->windows.find(g.key);
     if (wi == r->windows.end()) continue;
     Phase& p = wi->second.ph[g.kind];
-    for (uint32_t i = 0; i < g.count && i < p.size(); ++i)
-      if (p.st[i] == V_IN_FLIGHT) { p.st[i] = V_PENDING; ++p.n_pending; }
+    const uint32_t back = std::min<uint32_t>(p.n_flight, (uint32_t)p.size());  // (the batch's: the first ones)
+    p.n_pending += back;
+    p.n_flight = 0;
   }
   if (r->seg_next) mark_dirty(r);
   r->segs.clear();
@@ -724,6 +759,7 @@ static void revert_segs(pbft_replica* r) {
   r->erased_in_flight = false;
   if (r->direct) r->arena[r->busy_arena].busy = false;
   r->direct = false;
+  r->adopted = false;
 }
 
 // The finished batch: State::insert_* for accepted candidates (in push order: the last accepted vote of a signer
@@ -741,7 +777,6 @@ static void prefetch_phase(const Phase& p) {
   const size_t k = p.size();
   prefetch_bytes(p.who.data(), 2 * k);
   prefetch_bytes(p.row.data(), 4 * k);
-  prefetch_bytes(p.st.data(), k);
   prefetch_bytes(p.acc.data(), 4 * p.acc.size());
   prefetch_bytes(p.cnt.data(), p.cnt.size());
   if (!p.digs.empty()) prefetch_bytes(p.digs.data(), 64);
@@ -914,6 +949,7 @@ static void finish_batch(pbft_replica* r) {
   r->erased_in_flight = false;
   if (r->direct) r->arena[r->busy_arena].busy = false;
   r->direct = false;
+  r->adopted = false;
 }
 
 // Copy the candidates of segments [s0, s1) into the batch: the GPU context's staged votes rows (rs =
@@ -939,7 +975,7 @@ static void fill_rows(pbft_replica* r, size_t s0, size_t s1, uint8_t* SIG, uint1
         for (uint32_t i = 0; i < g.count; ++i) IDX[g.row0 + i] = g.env0 + p.dix[i];
       }
     }
-    memset(p.st.data(), V_IN_FLIGHT, g.count);
+    p.n_flight = g.count;
     p.n_pending = 0;
   }
 }
@@ -1203,6 +1239,7 @@ int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t
     if (it != r->key_index.end() && it->second != idx[i] && !replaced(it->second)) return PBFT_EINVAL;
   }
   if (r->ctx && m) {
+    eu_drop(r);  // (its bits were computed under the old keys)
     for (size_t k = 0; k < r->ctxs.size(); ++k) {  // every GPU's key set (a clone listed twice: rebuilt twice)
       const int rc = pbft_verify_update_keys(r->ctxs[k], idx, A, m, key_ok);
       if (rc) return rc;
@@ -1242,6 +1279,7 @@ int pbft_replica_destroy(pbft_replica* r) {
   }
   if (r->in_flight && r->in_flight_via == 1 && r->vpoll)
     while (r->vpoll(r->vuser) == 0) std::this_thread::yield();
+  eu_drop(r);
   for (Arena& a : r->arena) {
     host_mem_free(r, a.rows, a.rows_pinned);
     host_mem_free(r, a.envs, a.envs_pinned);
@@ -1253,6 +1291,7 @@ int pbft_replica_destroy(pbft_replica* r) {
 int pbft_replica_set_verifier(pbft_replica* r, pbft_batch_verify_fn fn, void* user) {
   if (!r) return PBFT_EINVAL;
   if (r->in_flight) return PBFT_EBUSY;
+  eu_drop(r);
   r->verify_fn = fn;
   r->verify_user = user;
   if (fn) r->vsub = nullptr, r->vpoll = nullptr;  // the last installed verifier serves the flushes
@@ -1263,6 +1302,7 @@ int pbft_replica_set_votes_verifier(pbft_replica* r, pbft_votes_submit_fn submit
                                     void* user) {
   if (!r || (!submit) != (!poll)) return PBFT_EINVAL;
   if (r->in_flight) return PBFT_EBUSY;
+  eu_drop(r);
   r->vsub = submit;
   r->vpoll = poll;
   r->vuser = user;
@@ -1302,6 +1342,8 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
     rc = r->digest_fn(r->digest_user, op, op_len, d);
   } else {
     if (!r->ctx) return PBFT_ENODEV;
+    rc = eu_settle(r);  // (the context must be idle)
+    if (rc) return rc;
     const uint64_t off = 0;
     const uint8_t empty = 0;
     rc = pbft_digest_blake2b512(r->ctx, op_len ? op : &empty, &off, &op_len, 1, d);
@@ -1363,7 +1405,7 @@ static int push_into(pbft_replica* r, Window& w, uint8_t kind, uint64_t view, ui
   }
   if (p.row.capacity() == 0) {  // one allocation per phase for the common case (every signer votes once)
     const size_t c = r->n < 1024 ? r->n : 1024;
-    p.row.reserve(c); p.who.reserve(c); p.dix.reserve(c); p.st.reserve(c);
+    p.row.reserve(c); p.who.reserve(c); p.dix.reserve(c);
   }
   const uint32_t env =
       j >= 0 && p.dgen[(size_t)j] == sk.a->gen ? p.denv[(size_t)j] : sink_env(r, sk, kind, view, seq, digest);
@@ -1430,7 +1472,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     // all the state machine depends on: the last accepted vote of a signer wins).
     //  1. (threads, by input slices) the per-row checks that need no window, and runs of consecutive rows with
     //     one (view, seq); rejected rows are flagged and do not break a run;
-    struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; };
+    struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; bool first; };
     RTRACE(r, "push", n_ok);
     std::vector<std::vector<Run>> slice_runs(T);
     std::vector<uint8_t> bad(n_ok);
@@ -1452,14 +1494,14 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         bd[i] = v_bad | w_bad;
         if (v_bad | w_bad) continue;
         if (q != run_seq) {
-          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0, run_good});
+          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0, run_good, false});
           run_seq = q;
           run_lo = i;
           run_good = 0;
         }
         ++run_good;
       }
-      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good});
+      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good, false});
       cnt[t].pushed += hi - lo;
       cnt[t].rejected_view += rv;
       cnt[t].rejected_watermark += rw;
@@ -1475,7 +1517,8 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     for (Run& u : runs) {
       Window& w = window_at(r, {r->current_view, u.seq});
       u.w = &w;
-      if (w.push_call != call) {  // the window's first run in this call: its owner
+      u.first = w.push_call != call;
+      if (u.first) {  // the window's first run in this call: its owner
         w.push_call = call;
         w.push_owner = (uint32_t)(u.lo * T / n_ok);
         t_envs[w.push_owner] += 2;
@@ -1484,11 +1527,54 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       t_rows[u.owner] += u.good;
     }
     Arena& A = push_arena(r);
-    uint64_t rows_all = 0, envs_all = 0;
-    for (size_t t = 0; t < T; ++t) rows_all += t_rows[t], envs_all += t_envs[t];
-    if (!arena_reserve(r, A, rows_all, envs_all)) return PBFT_ENOMEM;  // (nothing pushed)
+    uint64_t rows_all = 0;
+    for (size_t t = 0; t < T; ++t) rows_all += t_rows[t];
+    // Early batch (r05): with one GPU context, no batch in flight and a large call, the arena range of this call is
+    // cut into P parts, each thread's rows split evenly over them (part k of every thread side by side), so that
+    // part k is complete once every thread has pushed the first (k + 1) / P of its rows: this thread launches each
+    // part (pbft_verify_votes_piece) as soon as it is, while the threads push the next -- the copies and kernels of
+    // the round run under push_many instead of after flush_submit.  Each part's envelopes are its own range (two per
+    // window whose first run falls in it, + 8 per thread); rows of rejected pushes and the 64-row padding of a part
+    // are rows no candidate references.
+    constexpr size_t P = 8;
+    const bool early = early_enabled() && direct_enabled() && r->ctx && r->ctxs.size() == 1 && !r->verify_fn && !r->vsub &&
+                       !r->in_flight && !r->eu.active && A.rows_pinned && A.envs_pinned &&
+                       A.clean.load(std::memory_order_relaxed) && rows_all >= (1u << 17);
+    std::vector<uint64_t> q_rows(early ? T * P : 0), q_envs(early ? T * P : 0);  // [t * P + k]
+    std::vector<uint64_t> r_off(early ? T * P : 0), e_off(early ? T * P : 0), piece_end(P), env_end(P), part_end(P);
+    uint64_t rows_total = rows_all, envs_total = 0;
+    for (size_t t = 0; t < T; ++t) envs_total += t_envs[t];
+    if (early) {
+      for (size_t t = 0; t < T; ++t)
+        for (size_t k = 0; k < P; ++k) {
+          q_rows[t * P + k] = t_rows[t] * (k + 1) / P - t_rows[t] * k / P;
+          q_envs[t * P + k] = 8;
+        }
+      std::vector<uint64_t> cum(T, 0);
+      for (const Run& u : runs) {  // (a window's envelopes are written with its first row: the part of that row)
+        const uint64_t g = t_rows[u.owner];
+        if (u.first && g) q_envs[u.owner * P + std::min<uint64_t>(P - 1, cum[u.owner] * P / g)] += 2;
+        cum[u.owner] += u.good;
+      }
+      uint64_t row = A.n, env = A.ne;
+      for (size_t k = 0; k < P; ++k) {
+        for (size_t t = 0; t < T; ++t) {
+          r_off[t * P + k] = row;
+          e_off[t * P + k] = env;
+          row += q_rows[t * P + k];
+          env += q_envs[t * P + k];
+        }
+        part_end[k] = row;
+        if (k + 1 < P) row = (row + 63) & ~(uint64_t)63;  // (pieces start 64-aligned: bitmap words)
+        piece_end[k] = row;
+        env_end[k] = env;
+      }
+      rows_total = piece_end[P - 1] - A.n;
+      envs_total = env_end[P - 1] - A.ne;
+    }
+    if (!arena_reserve(r, A, rows_total, envs_total)) return PBFT_ENOMEM;  // (nothing pushed)
     std::vector<Sink> sinks;
-    {
+    if (!early) {
       uint64_t row = A.n, env = A.ne;
       for (size_t t = 0; t < T; ++t) {
         sinks.push_back(Sink{&A, r->cur, row, row + t_rows[t], (uint32_t)env, (uint32_t)(env + t_envs[t]), false,
@@ -1496,30 +1582,101 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         row += t_rows[t];
         env += t_envs[t];
       }
+    } else {
+      for (size_t t = 0; t < T; ++t) sinks.push_back(Sink{&A, r->cur, 0, 0, 0, 0, false, g_stream_stores});
     }
+    bool launched = false;
+    if (early) {  // the batch is opened before the threads start: envelope 0 and the rows pushed before this call
+      r->bitmap.assign((piece_end[P - 1] + 63) / 64, 0);
+      launched = pbft_verify_votes_open(r->ctx, piece_end[P - 1], (uint32_t)env_end[P - 1], r->bitmap.data()) == PBFT_OK;
+    }
+    std::unique_ptr<std::atomic<uint32_t>[]> parts_done(new std::atomic<uint32_t>[P]);
+    for (size_t k = 0; k < P; ++k) parts_done[k].store(0, std::memory_order_relaxed);
     RTRACE(r, "push_windows", runs.size());
     //  3. (threads) every thread pushes the rows of the windows it owns, in input order, into its range; the range's
     //     unused rows (rejected pushes) become rows no candidate references (key 0, envelope 0), its unused
     //     envelopes copies of envelope 0
-    WorkerPool::get().run(T, [&](size_t t) {
+    static const uint8_t zero_sig[64] = {0};
+    WorkerPool::get().start(T, [&](size_t t) {
       // (thread-local copies: the threads' entries of cnt / sinks share cache lines, and every row updates them)
       PushCounts c = cnt[t];
       Sink sk = sinks[t];
-      for (const Run& u : runs) {
-        if (u.owner != t) continue;
-        for (uint64_t i = u.lo; i < u.hi; ++i)
-          if (!bad[i]) push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
+      if (!early) {
+        for (const Run& u : runs) {
+          if (u.owner != t) continue;
+          for (uint64_t i = u.lo; i < u.hi; ++i)
+            if (!bad[i]) push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
+        }
+        for (; sk.row < sk.row_end; ++sk.row) put_row(A.rows + ROWB * sk.row, zero_sig, 0, 0, g_stream_stores);
+        for (; sk.env < sk.env_end; ++sk.env)
+          memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
+      } else {
+        // every good row takes the next slot of the current part (its row, or a row no candidate references)
+        size_t k = 0;
+        uint64_t used = 0, slot = r_off[t * P];
+        sk.env = (uint32_t)e_off[t * P];
+        sk.env_end = (uint32_t)(e_off[t * P] + q_envs[t * P]);
+        auto close_part = [&]() {  // part k of this thread is written: its unused envelopes, then the signal
+          for (; sk.env < sk.env_end; ++sk.env)
+            memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
+          stream_fence();
+          parts_done[k].fetch_add(1, std::memory_order_release);
+          ++k;
+          used = 0;
+          if (k < P) {
+            slot = r_off[t * P + k];
+            sk.env = (uint32_t)e_off[t * P + k];
+            sk.env_end = (uint32_t)(e_off[t * P + k] + q_envs[t * P + k]);
+          }
+        };
+        while (k < P && q_rows[t * P + k] == 0) close_part();
+        for (const Run& u : runs) {
+          if (u.owner != t) continue;
+          for (uint64_t i = u.lo; i < u.hi; ++i) {
+            if (bad[i]) continue;
+            sk.row = slot;
+            sk.row_end = slot + 1;
+            if (push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk) != 1)
+              put_row(A.rows + ROWB * slot, zero_sig, 0, 0, g_stream_stores);
+            ++slot;
+            if (++used == q_rows[t * P + k])
+              do close_part(); while (k < P && q_rows[t * P + k] == 0);
+          }
+        }
+        while (k < P) close_part();  // (never: the quotas add up to the thread's good rows)
       }
-      static const uint8_t zero_sig[64] = {0};
-      for (; sk.row < sk.row_end; ++sk.row) put_row(A.rows + ROWB * sk.row, zero_sig, 0, 0, g_stream_stores);
-      for (; sk.env < sk.env_end; ++sk.env)
-        memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
       if (g_stream_stores) stream_fence();  // (streaming stores are weakly ordered: drained before the join)
       cnt[t] = c;
       sinks[t] = sk;
     });
-    A.n += rows_all;
-    A.ne += (uint32_t)envs_all;
+    if (early) {  // launch part k as soon as every thread has finished it (its 64-row padding written here first)
+      for (size_t k = 0; k < P; ++k) {
+        while (parts_done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
+        for (uint64_t x = part_end[k]; x < piece_end[k]; ++x) put_row(A.rows + ROWB * x, zero_sig, 0, 0, false);
+        if (launched) {
+          const uint64_t lo = k ? piece_end[k - 1] : 0;
+          const uint32_t elo = k ? (uint32_t)env_end[k - 1] : 0;
+          launched = pbft_verify_votes_piece(r->ctx, A.rows, lo, piece_end[k], A.envs, elo, (uint32_t)env_end[k]) ==
+                     PBFT_OK;
+        }
+      }
+    }
+    WorkerPool::get().wait();
+    if (early) {
+      A.n = piece_end[P - 1];
+      A.ne = (uint32_t)env_end[P - 1];
+      if (launched && pbft_verify_votes_close(r->ctx, A.n) == PBFT_OK) {
+        r->eu.active = true;
+        r->eu.done = false;
+        r->eu.arena = r->cur;
+        r->eu.rows = A.n;
+        r->eu.envs = A.ne;
+      }
+      RTRACE(r, "early", launched);
+    } else {
+      A.n += rows_all;
+      A.ne += (uint32_t)envs_total;
+    }
     for (Sink& sk : sinks) A.live.fetch_add(sk.added, std::memory_order_relaxed);
     for (const PushCounts& c : cnt) {
       add_counts(r, c);
@@ -1591,7 +1748,7 @@ static int submit_arena(pbft_replica* r, uint64_t N) {
   for (Seg& g : r->segs) {
     Phase& p = g.w->ph[g.kind];
     g.row_end = p.row_hi;
-    memset(p.st.data(), V_IN_FLIGHT, g.count);
+    p.n_flight = g.count;
     p.n_pending = 0;
   }
   A.busy = true;
@@ -1600,6 +1757,34 @@ static int submit_arena(pbft_replica* r, uint64_t N) {
   r->cur = a ^ 1;  // (the other arena holds no candidate: restarted by the next push)
   r->in_flight = true;
   r->in_flight_via = 0;
+  return PBFT_OK;
+}
+
+// The batch is the current arena as push_many's early batch already verifies it (running, or done): this flush only
+// marks its candidates; r->bitmap was the early batch's output from the start.
+static int adopt_early(pbft_replica* r, uint64_t N) {
+  const uint32_t a = r->cur;
+  Arena& A = r->arena[a];
+  r->rows = N;
+  r->rows_span = A.n;
+  r->touched.assign(r->segs.size(), 0);
+  r->seg_next = 0;
+  r->slice_lo.clear();
+  for (Seg& g : r->segs) {
+    Phase& p = g.w->ph[g.kind];
+    g.row_end = p.row_hi;
+    p.n_flight = g.count;
+    p.n_pending = 0;
+  }
+  A.busy = true;
+  r->busy_arena = a;
+  r->direct = true;
+  r->cur = a ^ 1;
+  r->in_flight = true;
+  r->in_flight_via = 0;
+  r->eu.active = false;
+  r->adopted = true;
+  RTRACE(r, "adopted", A.n);
   return PBFT_OK;
 }
 
@@ -1650,6 +1835,10 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     const bool direct = direct_enabled() && r->ctx && !r->verify_fn && !r->vsub && A.rows_pinned && A.envs_pinned &&
                         A.clean.load() && A.gen && B.live.load() == 0 && !B.busy &&
                         (int64_t)N == A.live.load() && A.n <= N + std::max<uint64_t>(4096, N / 16);
+    if (r->eu.active) {  // push_many's early batch: adopted when it covers exactly this arena as it is now
+      if (direct && r->eu.arena == r->cur && A.n == r->eu.rows && A.ne == r->eu.envs) return adopt_early(r, N);
+      eu_drop(r);
+    }
     if (direct) return submit_arena(r, N);
     // (else the staging fill below; pushes during the flight go to the other arena when nothing is left in it)
     if (B.live.load() == 0 && !B.busy) r->cur ^= 1;
@@ -1789,7 +1978,7 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
       // (a window's segments stay in order: a prefix of the batch)
       const size_t G = r->segs.size();
       // (at least 2^16 more rows in since the last application: the pool wakes for a chunk, not per poll)
-      if (r->seg_next < G && rows_done >= r->applied_upto + (1u << 16)) {
+      if (!r->adopted && r->seg_next < G && rows_done >= r->applied_upto + (1u << 16)) {
         RTRACE(r, "landed", rows_done);
         size_t s1 = r->seg_next;
         while (s1 < G && r->segs[s1].row_end <= rows_done) ++s1;

@@ -236,6 +236,8 @@ struct pbft_ctx {
   bool v_readback = false;  // progressive: each chunk's bitmap words come back on their own (ev_rows)
   std::vector<hipEvent_t> ev_rows;  // per chunk: its bitmap words are in h_bitmap
   std::vector<uint64_t> v_ends;     // per launched chunk: its end row
+  uint32_t v_env_cap = 0;           // a batch opened in pieces (pbft_verify_votes_open): its envelope capacity
+  hipEvent_t ev_envp = nullptr;     // a piece's envelopes copied
   bool v_short_tail = false;        // the batch's schedule ends with a VOTES_TAIL-row chunk (votes_chunk_end)
   uint64_t rows_out = 0;            // rows whose bitmap words are in the caller's bitmap
   uint64_t chunk_out = 0;           // chunks whose bitmap words are in the caller's bitmap
@@ -701,7 +703,7 @@ __global__ void __launch_bounds__(BLOCK) env_sched_kernel(const uint8_t* __restr
 }
 
 // (the buffer grows on first use for a bigger table: not inside a stream capture)
-static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, hipStream_t st, const uint64_t** out) {
+static int ensure_wk(pbft_ctx* c, uint32_t n_env) {
   if (n_env > c->wk_cap) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->d_wk) {
@@ -714,6 +716,11 @@ static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, h
       return set_err(PBFT_ENOMEM, "envelope schedule alloc");
     c->wk_cap = n_env;
   }
+  return PBFT_OK;
+}
+static int prepare_env_sched(pbft_ctx* c, const uint8_t* dENV, uint32_t n_env, hipStream_t st, const uint64_t** out) {
+  int rc = ensure_wk(c, n_env);
+  if (rc) return rc;
   hipLaunchKernelGGL(env_sched_kernel, dim3((n_env + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, dENV, n_env, c->d_wk);
   HIP_TRY(hipGetLastError());
   *out = c->d_wk;
@@ -770,6 +777,7 @@ static uint64_t votes_chunk_end(const pbft_ctx* c, uint64_t lo, uint64_t N) {
 static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t N, bool readback,
                        bool short_tail = false) {
   c->v_short_tail = short_tail;
+  c->v_env_cap = 0;  // (not a batch in pieces)
   c->v_ends.clear();
   const uint64_t words = (N + 63) / 64;
   const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * n_env + 64 + 255) & ~(size_t)255;  // + read slack
@@ -826,76 +834,96 @@ static int votes_begin(pbft_ctx* c, const uint8_t* ENV, uint32_t n_env, uint64_t
   return PBFT_OK;
 }
 
-static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* IDX,
-                        uint32_t rs_stride, uint64_t rows) {
+// One chunk of a votes batch: rows [lo, lo + n) -- their copy (or the mapped staging read in place), the kernels
+// on the chunk's stream, its bitmap words back (progressive form) -- then v_next / v_chunk advance.
+static int votes_chunk(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* IDX,
+                       uint32_t rs_stride, uint64_t lo, uint64_t n) {
   const uint64_t N = c->v_n;
   const votes_layout L(N < VOTES_CHUNK ? N : VOTES_CHUNK);
-  while (c->v_next < N && (rows >= N || votes_chunk_end(c, c->v_next, N) <= rows)) {
-    const uint64_t lo = c->v_next;
-    const uint64_t n = votes_chunk_end(c, lo, N) - lo;
-    c->v_ends.push_back(lo + n);
-    const int b = (int)(c->v_chunk % VOTES_BUFS);
-    const int slot = c->v_two ? (int)(c->v_chunk & 1) : 0;
-    hipStream_t st = slot ? c->stream2 : c->stream;
-    if (slot && !c->v_s2_ready) {
-      LT("wait_env2", HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_env, 0)));
-      c->v_s2_ready = true;
-    }
-    const bool rows_form = rs_stride == ROW;
-    const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
-    const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
-    const uint8_t* zK = rows_form ? zR + PBFT_VOTES_ROW_KEY : zc_dev(c, K + lo, 2 * n);
-    const uint8_t* zI = rows_form ? zR + PBFT_VOTES_ROW_ENV : zc_dev(c, IDX + lo, 4 * n);
-    const uint32_t ks = rows_form ? ROW : 2, mis = rows_form ? ROW / 4 : 1;
-    if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
-      int rc = 0;
-      LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
-                                       PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st, rs_stride, ks, nullptr,
-                                       (const uint32_t*)zI, c->v_env, c->v_wk, true, mis, slot));
-      if (rc) return rc;
-      if (c->v_readback) {
-        LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
-        LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
-      }
-      c->v_next += n;
-      ++c->v_chunk;
-      continue;
-    }
-    uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
-    if (c->v_chunk >= VOTES_BUFS) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
-    if (rows_form) {  // the chunk's rows: one copy
-      LT("h2d_rows", HIP_TRY(hipMemcpyAsync(base, R + (size_t)ROW * lo, (size_t)ROW * n, hipMemcpyHostToDevice,
-                                            c->cstream)));
-    } else {
-      HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
-      HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
-      LT("h2d_key", HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream)));
-      LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
-    }
-    LT("rec_copied", HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream)));
-    LT("wait_copied", HIP_TRY(hipStreamWaitEvent(st, c->ev_copied[b], 0)));
+  const int b = (int)(c->v_chunk % VOTES_BUFS);
+  const int slot = c->v_two ? (int)(c->v_chunk & 1) : 0;
+  hipStream_t st = slot ? c->stream2 : c->stream;
+  if (slot && !c->v_s2_ready) {
+    LT("wait_env2", HIP_TRY(hipStreamWaitEvent(c->stream2, c->ev_env, 0)));
+    c->v_s2_ready = true;
+  }
+  if (c->v_readback && c->ev_rows.size() <= c->v_chunk) {  // (pieces: the chunk count is not known up front)
+    hipEvent_t e;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->ev_rows.push_back(e);
+  }
+  c->v_ends.push_back(lo + n);
+  const bool rows_form = rs_stride == ROW;
+  const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
+  const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
+  const uint8_t* zK = rows_form ? zR + PBFT_VOTES_ROW_KEY : zc_dev(c, K + lo, 2 * n);
+  const uint8_t* zI = rows_form ? zR + PBFT_VOTES_ROW_ENV : zc_dev(c, IDX + lo, 4 * n);
+  const uint32_t ks = rows_form ? ROW : 2, mis = rows_form ? ROW / 4 : 1;
+  if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
     int rc = 0;
-    LT("kernels", rc = launch_verify(c, base, base + (rows_form ? 32 : L.offS),
-                                     (const uint16_t*)(base + (rows_form ? PBFT_VOTES_ROW_KEY : L.offK)), c->d_stage,
-                                     PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st,
-                                     rs_stride, ks, nullptr,
-                                     (const uint32_t*)(base + (rows_form ? PBFT_VOTES_ROW_ENV : L.offI)), c->v_env,
-                                     c->v_wk, false, mis, slot));
+    LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
+                                     PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st, rs_stride, ks, nullptr,
+                                     (const uint32_t*)zI, c->v_env, c->v_wk, true, mis, slot));
     if (rc) return rc;
-    LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], st)));
-    if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
+    if (c->v_readback) {
       LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
       LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
     }
     c->v_next += n;
     ++c->v_chunk;
+    return PBFT_OK;
+  }
+  uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
+  if (c->v_chunk >= VOTES_BUFS) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
+  if (rows_form) {  // the chunk's rows: one copy
+    LT("h2d_rows", HIP_TRY(hipMemcpyAsync(base, R + (size_t)ROW * lo, (size_t)ROW * n, hipMemcpyHostToDevice,
+                                          c->cstream)));
+  } else {
+    HIP_TRY(hipMemcpyAsync(base, R + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    HIP_TRY(hipMemcpyAsync(base + L.offS, S + 32 * lo, 32 * n, hipMemcpyHostToDevice, c->cstream));
+    LT("h2d_key", HIP_TRY(hipMemcpyAsync(base + L.offK, K + lo, 2 * n, hipMemcpyHostToDevice, c->cstream)));
+    LT("h2d_idx", HIP_TRY(hipMemcpyAsync(base + L.offI, IDX + lo, 4 * n, hipMemcpyHostToDevice, c->cstream)));
+  }
+  LT("rec_copied", HIP_TRY(hipEventRecord(c->ev_copied[b], c->cstream)));
+  LT("wait_copied", HIP_TRY(hipStreamWaitEvent(st, c->ev_copied[b], 0)));
+  int rc = 0;
+  LT("kernels", rc = launch_verify(c, base, base + (rows_form ? 32 : L.offS),
+                                   (const uint16_t*)(base + (rows_form ? PBFT_VOTES_ROW_KEY : L.offK)), c->d_stage,
+                                   PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st,
+                                   rs_stride, ks, nullptr,
+                                   (const uint32_t*)(base + (rows_form ? PBFT_VOTES_ROW_ENV : L.offI)), c->v_env,
+                                   c->v_wk, false, mis, slot));
+  if (rc) return rc;
+  LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], st)));
+  if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
+    LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
+    LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
+  }
+  c->v_next += n;
+  ++c->v_chunk;
+  return PBFT_OK;
+}
+
+// The context stream (ev_done, the final bitmap export) follows stream2's last chunk too
+static int votes_join_streams(pbft_ctx* c) {
+  if (c->v_two) {
+    HIP_TRY(hipEventRecord(c->ev_s2, c->stream2));
+    HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+  }
+  return PBFT_OK;
+}
+
+static int votes_launch(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const uint16_t* K, const uint32_t* IDX,
+                        uint32_t rs_stride, uint64_t rows) {
+  const uint64_t N = c->v_n;
+  while (c->v_next < N && (rows >= N || votes_chunk_end(c, c->v_next, N) <= rows)) {
+    const uint64_t lo = c->v_next;
+    const int rc = votes_chunk(c, R, S, K, IDX, rs_stride, lo, votes_chunk_end(c, lo, N) - lo);
+    if (rc) return rc;
   }
   if (c->v_next >= N) {
     c->v_open = false;
-    if (c->v_two) {  // the context stream (ev_done, the final bitmap export) follows stream2's last chunk too
-      HIP_TRY(hipEventRecord(c->ev_s2, c->stream2));
-      HIP_TRY(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
-    }
+    return votes_join_streams(c);
   }
   return PBFT_OK;
 }
@@ -1050,6 +1078,7 @@ int pbft_verify_ctx_destroy(pbft_ctx* c) {
   (void)hipFree(c->d_work2);
   if (c->ev_comb) (void)hipEventDestroy(c->ev_comb);
   for (hipEvent_t e : c->ev_rows) (void)hipEventDestroy(e);
+  if (c->ev_envp) (void)hipEventDestroy(c->ev_envp);
   if (c->cstream) { (void)hipStreamSynchronize(c->cstream); (void)hipStreamDestroy(c->cstream); }
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
@@ -1488,6 +1517,106 @@ int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, 
 // GB/s (tools/microbench/pinned_write.cpp, numa_h2d.cpp; profiles/r05/pinned_h2d.txt).  One header page in front
 // holds the mapping's length for pbft_host_free.
 static constexpr size_t HOST_HDR = 4096;
+// ---- votes batch in pieces (pbft_verify_votes_open / _piece / _close): the caller's rows and envelopes are
+// written while earlier pieces are already being copied and verified (pbft_replica_push_many: r05) ----
+int pbft_verify_votes_open(pbft_ctx* c, uint64_t n_cap, uint32_t env_cap, uint64_t* out) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (n_cap == 0 || env_cap == 0 || !out) return set_err(PBFT_EINVAL, "empty batch or null bitmap");
+  if (c->n_keys == 0) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  c->staged = false;
+  HIP_TRY(hipSetDevice(c->device));
+  const uint64_t words = (n_cap + 63) / 64;
+  const size_t env_bytes = ((size_t)PBFT_ENVELOPE_LEN * env_cap + 64 + 255) & ~(size_t)255;
+  const votes_layout L(n_cap < VOTES_CHUNK ? n_cap : VOTES_CHUNK);
+  int rc = ensure_stage(c, env_bytes + VOTES_BUFS * L.bytes, words);
+  if (rc) return rc;
+  rc = ensure_wk(c, env_cap);
+  if (rc) return rc;
+  const bool two = c->two_streams;
+  if (two && !c->stream2) {
+    HIP_TRY(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_env, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming));
+  }
+  if (!c->ev_envp) HIP_TRY(hipEventCreateWithFlags(&c->ev_envp, hipEventDisableTiming));
+  c->v_short_tail = false;
+  c->v_ends.clear();
+  c->v_s2_ready = true;  // (stream2 waits for every piece's envelopes itself: votes_piece)
+  c->v_two = two;
+  c->v_n = n_cap;
+  c->v_next = 0;
+  c->v_chunk = 0;
+  c->v_env_bytes = env_bytes;
+  c->v_env = 0;
+  c->v_env_cap = env_cap;
+  c->v_wk = c->d_wk;
+  c->v_open = true;
+  c->v_readback = true;
+  c->rows_out = 0;
+  c->chunk_out = 0;
+  c->in_flight = true;
+  c->async_out = out;
+  c->async_words = words;
+  return PBFT_OK;
+}
+
+static int votes_drop(pbft_ctx* c, int rc) {  // a failed piece: drain what was launched, the batch is lost
+  (void)hipStreamSynchronize(c->stream);
+  if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+  (void)hipStreamSynchronize(c->cstream);
+  c->in_flight = false;
+  c->v_open = false;
+  c->v_env_cap = 0;
+  return rc;
+}
+
+int pbft_verify_votes_piece(pbft_ctx* c, const uint8_t* rows, uint64_t row_lo, uint64_t row_hi, const uint8_t* envs,
+                            uint32_t env_lo, uint32_t env_hi) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (!c->in_flight || !c->v_open || c->v_env_cap == 0) return set_err(PBFT_EINVAL, "no votes batch open in pieces");
+  if (!rows || row_lo != c->v_next || row_hi < row_lo || row_hi > c->v_n || (row_lo & 63) ||
+      env_lo != c->v_env || env_hi < env_lo || env_hi > c->v_env_cap || (env_hi > env_lo && !envs))
+    return set_err(PBFT_EINVAL, "piece out of order or out of the opened bounds");
+  HIP_TRY(hipSetDevice(c->device));
+  if (env_hi > env_lo) {  // the piece's new envelopes and their block-2 schedules, ahead of its rows' kernels
+    const uint32_t ne = env_hi - env_lo;
+    if (hipMemcpyAsync(c->d_stage + (size_t)PBFT_ENVELOPE_LEN * env_lo, envs + (size_t)PBFT_ENVELOPE_LEN * env_lo,
+                       (size_t)PBFT_ENVELOPE_LEN * ne, hipMemcpyHostToDevice, c->cstream) != hipSuccess ||
+        hipEventRecord(c->ev_envp, c->cstream) != hipSuccess || hipStreamWaitEvent(c->stream, c->ev_envp, 0) != hipSuccess)
+      return votes_drop(c, set_err(PBFT_EHIP, "piece envelopes"));
+    hipLaunchKernelGGL(env_sched_kernel, dim3((ne + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, c->stream,
+                       c->d_stage + (size_t)PBFT_ENVELOPE_LEN * env_lo, ne, c->d_wk + (size_t)SHA_ENV_WORDS * env_lo);
+    if (hipGetLastError() != hipSuccess) return votes_drop(c, set_err(PBFT_EHIP, "piece envelope schedule"));
+    if (c->v_two && (hipEventRecord(c->ev_env, c->stream) != hipSuccess ||
+                     hipStreamWaitEvent(c->stream2, c->ev_env, 0) != hipSuccess))
+      return votes_drop(c, set_err(PBFT_EHIP, "piece envelope event"));
+    c->v_env = env_hi;
+  }
+  for (uint64_t lo = row_lo; lo < row_hi;) {
+    const uint64_t n = row_hi - lo > VOTES_CHUNK ? VOTES_CHUNK : row_hi - lo;
+    const int rc = votes_chunk(c, rows, rows + 32, (const uint16_t*)(rows + PBFT_VOTES_ROW_KEY),
+                               (const uint32_t*)(rows + PBFT_VOTES_ROW_ENV), ROW, lo, n);
+    if (rc) return votes_drop(c, rc);
+    lo += n;
+  }
+  return PBFT_OK;
+}
+
+int pbft_verify_votes_close(pbft_ctx* c, uint64_t n) {
+  if (!c) return set_err(PBFT_EINVAL, "null context");
+  if (!c->in_flight || !c->v_open || c->v_env_cap == 0) return set_err(PBFT_EINVAL, "no votes batch open in pieces");
+  if (n != c->v_next || n == 0) return votes_drop(c, set_err(PBFT_EINVAL, "close: rows submitted differ"));
+  HIP_TRY(hipSetDevice(c->device));
+  c->v_open = false;
+  c->v_env_cap = 0;
+  c->v_n = n;
+  c->async_words = (n + 63) / 64;
+  int rc = votes_join_streams(c);
+  if (rc == PBFT_OK && hipEventRecord(c->ev_done, c->stream) != hipSuccess) rc = set_err(PBFT_EHIP, "event record");
+  return rc ? votes_drop(c, rc) : PBFT_OK;
+}
+
 int pbft_host_alloc(pbft_ctx* c, size_t bytes, void** out) {
   if (!out) return set_err(PBFT_EINVAL, "null argument");
   *out = nullptr;

@@ -66,7 +66,10 @@ struct FakeGpu {
   uint32_t n_env = 0, n_keys = 0;
   uint64_t* out = nullptr;
   bool staged = false, open = false, in_flight = false;
-  uint64_t batches = 0, chunk_launches = 0, direct_batches = 0, ext_hash = 0;
+  uint64_t batches = 0, chunk_launches = 0, direct_batches = 0, early_batches = 0, ext_hash = 0;
+  bool pieces = false;  // opened with pbft_verify_votes_open
+  uint32_t env_cap = 0;
+  std::vector<std::array<uint64_t, 3>> piece_hash;  // (lo, hi, hash of the rows when the piece was launched)
   uint32_t lag = 1, polls = 0;  // polls per chunk landing (3 contexts: each slice is one chunk of the schedule)
 };
 static uint64_t fnv(const uint8_t* p, size_t n) {
@@ -81,6 +84,8 @@ int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_
   if (!g) return PBFT_ENODEV;
   CHECK(!g->in_flight);
   g->ext = nullptr;
+  g->pieces = false;
+  g->piece_hash.clear();
   g->rows.assign((size_t)PBFT_VOTES_ROW_BYTES * N, 0);
   for (uint64_t i = 0; i < N; ++i) memset(&g->rows[(size_t)PBFT_VOTES_ROW_BYTES * i + PBFT_VOTES_ROW_KEY], 0xFF, 2);
   g->env.assign((size_t)PBFT_ENVELOPE_BYTES * n_env, 0);
@@ -113,7 +118,8 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   FakeGpu* g = (FakeGpu*)c;
   if (!g->in_flight) { *rows_done = g->N; return 1; }
   if (g->done < g->launched && ++g->polls % g->lag == 0) {  // one more chunk "lands"
-    const uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
+    uint64_t hi = PBFT_VOTES_CHUNK_END(g->done, g->N);
+    if (hi > g->launched) hi = g->launched;  // (a batch in pieces: only what was launched)
     for (uint64_t w = g->done / 64; w < (hi + 63) / 64; ++w) g->out[w] = 0;
     for (uint64_t i = g->done; i < hi; ++i) {
       CHECK(g->idx(i) < g->n_env);
@@ -126,7 +132,9 @@ int pbft_verify_poll_rows(pbft_ctx* c, uint64_t* rows_done) {
   }
   *rows_done = g->done;
   if (g->open || g->done < g->N) return 0;
-  if (g->ext) CHECK(fnv(g->ext, (size_t)PBFT_VOTES_ROW_BYTES * g->N) == g->ext_hash);  // untouched while in flight
+  if (g->ext && !g->pieces) CHECK(fnv(g->ext, (size_t)PBFT_VOTES_ROW_BYTES * g->N) == g->ext_hash);  // untouched while in flight
+  for (const auto& ph : g->piece_hash)  // every piece's rows untouched since it was launched
+    CHECK(fnv(g->ext + (size_t)PBFT_VOTES_ROW_BYTES * ph[0], (size_t)PBFT_VOTES_ROW_BYTES * (ph[1] - ph[0])) == ph[2]);
   g->in_flight = false;
   return 1;
 }
@@ -136,6 +144,8 @@ int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, 
   CHECK(g && !g->in_flight && rows && env && n_env && out && N);
   for (uint32_t e = 0; e < n_env; ++e) CHECK(memcmp(env + (size_t)PBFT_ENVELOPE_BYTES * e, "PBFT", 4) == 0);
   g->staged = false;
+  g->pieces = false;
+  g->piece_hash.clear();
   g->ext = rows;
   g->ext_hash = fnv(rows, (size_t)PBFT_VOTES_ROW_BYTES * N);
   g->N = N; g->n_env = n_env; g->out = out;
@@ -143,6 +153,36 @@ int pbft_verify_votes_submit_host(pbft_ctx* c, const uint8_t* rows, uint64_t N, 
   ++g->batches;
   ++g->direct_batches;
   for (uint64_t lo = 0; lo < N; lo = PBFT_VOTES_CHUNK_END(lo, N)) ++g->chunk_launches;
+  return 0;
+}
+int pbft_verify_votes_open(pbft_ctx* c, uint64_t n_cap, uint32_t env_cap, uint64_t* out) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && !g->in_flight && n_cap && env_cap && out);
+  g->staged = false; g->ext = nullptr; g->pieces = true; g->piece_hash.clear();
+  g->N = n_cap; g->n_env = 0; g->env_cap = env_cap; g->out = out;
+  g->open = true; g->in_flight = true; g->launched = 0; g->done = 0;
+  ++g->batches; ++g->direct_batches; ++g->early_batches;
+  return 0;
+}
+int pbft_verify_votes_piece(pbft_ctx* c, const uint8_t* rows, uint64_t lo, uint64_t hi, const uint8_t* env,
+                            uint32_t elo, uint32_t ehi) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && g->open && g->pieces && rows && lo == g->launched && lo % 64 == 0 && hi >= lo && hi <= g->N);
+  CHECK(elo == g->n_env && ehi >= elo && ehi <= g->env_cap);
+  CHECK(!g->ext || g->ext == rows);  // (one base pointer for every piece)
+  for (uint32_t e = elo; e < ehi; ++e) CHECK(memcmp(env + (size_t)PBFT_ENVELOPE_BYTES * e, "PBFT", 4) == 0);
+  g->ext = rows;
+  g->n_env = ehi;
+  g->launched = hi;
+  g->piece_hash.push_back({lo, hi, fnv(rows + (size_t)PBFT_VOTES_ROW_BYTES * lo, (size_t)PBFT_VOTES_ROW_BYTES * (hi - lo))});
+  ++g->chunk_launches;
+  return 0;
+}
+int pbft_verify_votes_close(pbft_ctx* c, uint64_t n) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && g->open && g->pieces && n == g->launched && n);
+  g->open = false;
+  g->N = n;
   return 0;
 }
 int pbft_host_alloc(pbft_ctx*, size_t bytes, void** out) {
@@ -162,6 +202,7 @@ int pbft_verify_poll(pbft_ctx* c) {
   return pbft_verify_poll_rows(c, &r);
 }
 int pbft_verify_wait(pbft_ctx* c) {
+  if (((FakeGpu*)c)->open) return PBFT_EBUSY;
   uint64_t r;
   while (pbft_verify_poll_rows(c, &r) == 0) {}
   return 0;
@@ -668,14 +709,16 @@ static void test_replica_progressive(uint32_t n_ctx, bool many) {
   }
   uint64_t rows = 0;
   CHECK(pbft_replica_flush_submit(r, 0, &rows) == 0 && rows == pushed + seqs);
-  uint64_t staged = 0, direct = 0;
+  uint64_t staged = 0, direct = 0, early = 0;
   for (const FakeGpu& x : gs) {
     CHECK(x.batches == 1 && x.chunk_launches >= (n_ctx > 1 ? 1u : 2u));  // every slice launched, in steps
     staged += x.N;
     direct += x.direct_batches;
+    early += x.early_batches;
   }
   // + the padding that 64-aligns each slice (staging fill), or push_many's unused rows (the arena as it is)
-  CHECK(staged >= rows && staged < rows + 64 * n_ctx + dups);
+  // (+ 64-row padding of each part of an early batch: 8 parts)
+  CHECK(staged >= rows && staged < rows + 64 * n_ctx + dups + (early ? 8 * 64 : 0));
   std::vector<pbft_round_event> ev(4 * seqs);
   uint32_t ne = 0;
   int polls = 0, st;
@@ -717,8 +760,68 @@ static void test_replica_progressive(uint32_t n_ctx, bool many) {
   CHECK(pbft_replica_flush(r, 0, ev2.data(), (uint32_t)ev2.size(), &ne) == 0 && ne == 120);
   pbft_replica_destroy(r);
   printf("replica progressive (%u contexts, %s): %llu rows in %llu launch steps on context 0, %d polls, %u commits, "
-         "%llu direct batches\n", n_ctx, many ? "push_many" : "push", (unsigned long long)rows,
-         (unsigned long long)g.chunk_launches, polls, committed, (unsigned long long)direct);
+         "%llu direct batches, %llu early\n", n_ctx, many ? "push_many" : "push", (unsigned long long)rows,
+         (unsigned long long)g.chunk_launches, polls, committed, (unsigned long long)direct,
+         (unsigned long long)early);
+}
+
+// ---- 6. push_many's early batch dropped: a PrePrepare pushed after it (the arena grew past what it covers), or a
+// key update between push_many and the flush; the flush then verifies the arena again (direct), same outcome -------
+static void test_replica_early_dropped(int how) {
+  const uint32_t n = 256, seqs = 600;  // 307,200 votes: an early batch
+  std::vector<uint8_t> keys(32 * (size_t)n);
+  for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = 7; }
+  FakeGpu g;
+  g.n_keys = n;
+  pbft_ctx* cx = (pbft_ctx*)&g;
+  pbft_replica* r = nullptr;
+  CHECK(pbft_replica_create_multi(&cx, 1, n, 0, keys.data(), &r) == 0);
+  pbft_replica_set_digest_fn(r, host_digest, nullptr);
+  pbft_replica_set_log_window(r, 4096);
+  const char op[] = "earlyOperation";
+  uint8_t d[64];
+  digest_padded(d, (const uint8_t*)op, strlen(op));
+  uint8_t sg[64] = {2};
+  for (uint32_t q = 1; q <= seqs; ++q)
+    CHECK(pbft_replica_on_pre_prepare(r, 1, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+  const uint64_t N = 2ull * n * seqs;
+  std::vector<uint8_t> mk(N), mdig(64 * N), msig(64 * N);
+  std::vector<uint64_t> mview(N, 1), mseq(N);
+  std::vector<uint32_t> msigner(N);
+  for (uint64_t i = 0; i < N; ++i) {
+    mk[i] = (i / n) % 2 ? PBFT_KIND_COMMIT : PBFT_KIND_PREPARE;
+    mseq[i] = 1 + i / (2 * n);
+    msigner[i] = (uint32_t)(i % n);
+    memcpy(&mdig[64 * i], d, 64);
+    msig[64 * i] = 1;
+    msig[64 * i + 1] = (uint8_t)i;
+    msig[64 * i + 2] = (uint8_t)(i >> 8);
+  }
+  uint64_t queued = 0;
+  CHECK(pbft_replica_push_many(r, N, mk.data(), mview.data(), mseq.data(), mdig.data(), msigner.data(), msig.data(),
+                               &queued) == 0 && queued == N);
+  CHECK(g.early_batches == 1 && g.in_flight);
+  if (how == 0) {
+    CHECK(pbft_replica_on_pre_prepare(r, 1, 1, seqs + 1, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+  } else {
+    const uint32_t idx = 5;
+    uint8_t A[32] = {5, 7};
+    uint8_t ok = 0;
+    CHECK(pbft_replica_update_keys(r, &idx, A, 1, &ok) == 0 && ok == 1);  // (the same key again)
+    CHECK(!g.in_flight);  // the early batch was finished first
+  }
+  std::vector<pbft_round_event> ev(4 * seqs);
+  uint32_t ne = 0;
+  CHECK(pbft_replica_flush(r, 0, ev.data(), (uint32_t)ev.size(), &ne) == 0);
+  uint32_t committed = 0;
+  for (uint32_t e = 0; e < ne; ++e) committed += ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL;
+  CHECK(committed == seqs);
+  CHECK(g.batches == 2 && g.early_batches == 1 && g.direct_batches == 2);  // the early one, then the flush's own
+  pbft_replica_stats st;
+  pbft_replica_get_stats(r, &st);
+  CHECK(st.batches == 1 && st.accepted == N + seqs + (how == 0 ? 1 : 0));
+  pbft_replica_destroy(r);
+  printf("replica early batch dropped (%s): %u commits\n", how == 0 ? "late PrePrepare" : "key update", committed);
 }
 
 int main() {
@@ -731,6 +834,10 @@ int main() {
   for (bool many : {false, true}) {
     test_replica_progressive(1, many);
     test_replica_progressive(3, many);
+  }
+  if (!(getenv("PBFT_REPLICA_DIRECT") && atoi(getenv("PBFT_REPLICA_DIRECT")) == 0)) {
+    test_replica_early_dropped(0);
+    test_replica_early_dropped(1);
   }
   printf("sanitized host run ok\n");
   return 0;
