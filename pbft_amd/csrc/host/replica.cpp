@@ -1633,7 +1633,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         for (const Run& u : runs) {
           if (u.owner != t) continue;
           for (uint64_t i = u.lo; i < u.hi; ++i) {
-            if (bad[i]) continue;
+            if (bad[i] || k >= P) continue;  // (k < P always: the quotas add up to the thread's good rows)
             sk.row = slot;
             sk.row_end = slot + 1;
             if (push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk) != 1)
