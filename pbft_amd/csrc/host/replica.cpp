@@ -1651,7 +1651,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     });
     if (early) {  // launch part k as soon as every thread has finished it (its 64-row padding written here first)
       for (size_t k = 0; k < P; ++k) {
-        while (parts_done[k].load(std::memory_order_acquire) < T) std::this_thread::yield();
+        // (sleeping, not spinning: the T workers have the host's cores; a 17th runnable thread slows one of them,
+        // and the pass waits for its slowest worker)
+        while (parts_done[k].load(std::memory_order_acquire) < T) std::this_thread::sleep_for(std::chrono::microseconds(20));
         for (uint64_t x = part_end[k]; x < piece_end[k]; ++x) put_row(A.rows + ROWB * x, zero_sig, 0, 0, false);
         if (launched) {
           const uint64_t lo = k ? piece_end[k - 1] : 0;
@@ -1684,9 +1686,13 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     }
     RTRACE(r, "push_done", q);
     if (g_push_trace && r->trace.size() >= 4) {  // PBFT_PUSH_TRACE (with PBFT_REPLICA_TRACE): pass times of this call
-      const size_t e = r->trace.size();
-      fprintf(stderr, "push-trace: checks %.3f windows %.3f rows %.3f ms\n", (r->trace[e - 3].ns - r->trace[e - 4].ns) / 1e6,
-              (r->trace[e - 2].ns - r->trace[e - 3].ns) / 1e6, (r->trace[e - 1].ns - r->trace[e - 2].ns) / 1e6);
+      auto at = [&](const char* what) {
+        for (size_t x = r->trace.size(); x-- > 0;)
+          if (!strcmp(r->trace[x].what, what)) return r->trace[x].ns;
+        return (uint64_t)0;
+      };
+      fprintf(stderr, "push-trace: checks %.3f windows %.3f rows %.3f ms\n", (at("push_checked") - at("push")) / 1e6,
+              (at("push_windows") - at("push_checked")) / 1e6, (at("push_done") - at("push_windows")) / 1e6);
       r->trace.clear();
     }
   }

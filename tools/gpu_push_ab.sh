@@ -3,7 +3,7 @@
 # prefetch distance, then the arena handed over as it is vs the staging fill.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
-for spec in ${SPECS:-PBFT_APPLY_OWNER=1,0 PBFT_REPLICA_DIRECT=1,0}; do
+for spec in ${SPECS:-PBFT_REPLICA_EARLY=1,0}; do
   tag=$(echo $spec | tr '=,' '__')
   timeout -k 10 300 python -u tools/replica_probe.py 24 1 $spec > gpurun_out/pab_$tag.json 2> gpurun_out/pab_$tag.err || exit 1
   python - gpurun_out/pab_$tag.json $spec <<'PY'
