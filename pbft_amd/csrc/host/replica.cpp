@@ -333,6 +333,7 @@ struct pbft_replica {
     uint32_t arena = 0;
     uint64_t rows = 0;
     uint32_t envs = 0;
+    std::vector<uint64_t> lo;  // context j (ctxs[j]) verifies rows [lo[j], lo[j + 1]) (one context: {0, rows})
   } eu;
   uint32_t busy_arena = 0;
   uint64_t applied_upto = 0;  // rows_done at the last progressive application
@@ -393,7 +394,11 @@ static bool early_enabled() {  // PBFT_REPLICA_EARLY=0: push_many never launches
 // wait for the early batch (the context is needed, or its arena is about to change); its bits stay adoptable
 static int eu_settle(pbft_replica* r) {
   if (!r->eu.active || r->eu.done) return PBFT_OK;
-  const int rc = pbft_verify_wait(r->ctx);
+  int rc = PBFT_OK;
+  for (size_t j = 0; j + 1 < r->eu.lo.size(); ++j) {
+    const int w = pbft_verify_wait(r->ctxs[j]);
+    if (w && !rc) rc = w;
+  }
   if (rc) {
     r->eu.active = false;  // lost: the flush verifies the rows again
     return rc;
@@ -1537,7 +1542,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     // window whose first run falls in it, + 8 per thread); rows of rejected pushes and the 64-row padding of a part
     // are rows no candidate references.
     constexpr size_t P = 8;
-    const bool early = early_enabled() && direct_enabled() && r->ctx && r->ctxs.size() == 1 && !r->verify_fn && !r->vsub &&
+    const bool early = early_enabled() && direct_enabled() && r->ctx && !r->verify_fn && !r->vsub &&
                        !r->in_flight && !r->eu.active && A.rows_pinned && A.envs_pinned &&
                        A.clean.load(std::memory_order_relaxed) && rows_all >= (1u << 17);
     std::vector<uint64_t> q_rows(early ? T * P : 0), q_envs(early ? T * P : 0);  // [t * P + k]
@@ -1586,9 +1591,25 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       for (size_t t = 0; t < T; ++t) sinks.push_back(Sink{&A, r->cur, 0, 0, 0, 0, false, g_stream_stores});
     }
     bool launched = false;
-    if (early) {  // the batch is opened before the threads start: envelope 0 and the rows pushed before this call
+    // several contexts (one per GPU): context j takes parts [j P / K, (j + 1) P / K) as one batch of its own -- the
+    // earlier parts to the first context, whose GPU starts first -- each batch's first piece carrying every envelope
+    // written so far (its rows may name any of them)
+    const size_t K = early ? std::min<size_t>(r->ctxs.size(), P) : 0;
+    std::vector<size_t> part0(K + 1);
+    std::vector<uint64_t> ctx_lo(K + 1);
+    for (size_t j = 0; j <= K; ++j) {
+      part0[j] = j * P / (K ? K : 1);
+      ctx_lo[j] = part0[j] == 0 ? 0 : piece_end[part0[j] - 1];
+    }
+    size_t opened = 0;
+    if (early) {  // the batches are opened before the threads start: envelope 0 and the rows pushed before this call
       r->bitmap.assign((piece_end[P - 1] + 63) / 64, 0);
-      launched = pbft_verify_votes_open(r->ctx, piece_end[P - 1], (uint32_t)env_end[P - 1], r->bitmap.data()) == PBFT_OK;
+      launched = true;
+      for (size_t j = 0; j < K && launched; ++j) {
+        launched = pbft_verify_votes_open(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j], (uint32_t)env_end[part0[j + 1] - 1],
+                                          r->bitmap.data() + ctx_lo[j] / 64) == PBFT_OK;
+        if (launched) opened = j + 1;
+      }
     }
     std::unique_ptr<std::atomic<uint32_t>[]> parts_done(new std::atomic<uint32_t>[P]);
     for (size_t k = 0; k < P; ++k) parts_done[k].store(0, std::memory_order_relaxed);
@@ -1656,10 +1677,14 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         while (parts_done[k].load(std::memory_order_acquire) < T) std::this_thread::sleep_for(std::chrono::microseconds(20));
         for (uint64_t x = part_end[k]; x < piece_end[k]; ++x) put_row(A.rows + ROWB * x, zero_sig, 0, 0, false);
         if (launched) {
-          const uint64_t lo = k ? piece_end[k - 1] : 0;
-          const uint32_t elo = k ? (uint32_t)env_end[k - 1] : 0;
-          launched = pbft_verify_votes_piece(r->ctx, A.rows, lo, piece_end[k], A.envs, elo, (uint32_t)env_end[k]) ==
-                     PBFT_OK;
+          size_t j = 0;
+          while (part0[j + 1] <= k) ++j;  // the context of part k
+          const uint64_t lo = (k ? piece_end[k - 1] : 0) - ctx_lo[j];
+          const uint32_t elo = k == part0[j] ? 0 : (uint32_t)env_end[k - 1];
+          launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], lo, piece_end[k] - ctx_lo[j], A.envs,
+                                             elo, (uint32_t)env_end[k]) == PBFT_OK;
+          if (launched && k + 1 == part0[j + 1])
+            launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
         }
       }
     }
@@ -1667,12 +1692,20 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     if (early) {
       A.n = piece_end[P - 1];
       A.ne = (uint32_t)env_end[P - 1];
-      if (launched && pbft_verify_votes_close(r->ctx, A.n) == PBFT_OK) {
+      if (launched) {
         r->eu.active = true;
         r->eu.done = false;
         r->eu.arena = r->cur;
         r->eu.rows = A.n;
         r->eu.envs = A.ne;
+        r->eu.lo = ctx_lo;
+      } else {
+        // (a failed open, piece or close dropped that context's batch; the other opened ones are dropped -- a close
+        // that does not match drops a batch still open -- or finished, and forgotten)
+        for (size_t j = 0; j < opened; ++j) {
+          (void)pbft_verify_votes_close(r->ctxs[j], 0);
+          (void)pbft_verify_wait(r->ctxs[j]);
+        }
       }
       RTRACE(r, "early", launched);
     } else {
@@ -1781,6 +1814,13 @@ static int adopt_early(pbft_replica* r, uint64_t N) {
     g.row_end = p.row_hi;
     p.n_flight = g.count;
     p.n_pending = 0;
+  }
+  if (r->eu.lo.size() > 2) {  // one slice per context (flush_poll: each context's own prefix)
+    const size_t S = r->eu.lo.size() - 1;
+    r->slice_lo = r->eu.lo;
+    r->slice_hi.assign(r->slice_lo.begin() + 1, r->slice_lo.end());
+    r->slice_end.assign(S, 0);
+    r->slice_fin.assign(S, 0);
   }
   A.busy = true;
   r->busy_arena = a;

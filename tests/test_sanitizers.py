@@ -55,5 +55,5 @@ def test_host_code_clean_under_asan_ubsan(direct):
         # the early batch launched piecewise while pushing, then adopted by the flush
         n_ctx = int(l.split("(")[1].split()[0])
         many = "push_many" in l
-        early = 1 if direct == "1" and many and n_ctx == 1 else 0
+        early = n_ctx if direct == "1" and many else 0
         assert l.endswith(f"{n_ctx if direct == '1' else 0} direct batches, {early} early"), l
