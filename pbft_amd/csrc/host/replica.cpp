@@ -1541,7 +1541,12 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     // the round run under push_many instead of after flush_submit.  Each part's envelopes are its own range (two per
     // window whose first run falls in it, + 8 per thread); rows of rejected pushes and the 64-row padding of a part
     // are rows no candidate references.
-    constexpr size_t P = 8;
+    // (PBFT_EARLY_PARTS: the part count, 2..32, default 8 -- read per call: A/B in one process)
+    const size_t P = [] {
+      const char* e = getenv("PBFT_EARLY_PARTS");
+      const long v = e ? strtol(e, nullptr, 10) : 8;
+      return (size_t)(v < 2 ? 2 : v > 32 ? 32 : v);
+    }();
     const bool early = early_enabled() && direct_enabled() && r->ctx && !r->verify_fn && !r->vsub &&
                        !r->in_flight && !r->eu.active && A.rows_pinned && A.envs_pinned &&
                        A.clean.load(std::memory_order_relaxed) && rows_all >= (1u << 17);
