@@ -205,7 +205,8 @@ int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq
  * flush, and a digest on the context (on_pre_prepare without a digest override), a key update or a verifier change
  * in between waits for the early batch first.  Environment (read per call, for A/B runs): PBFT_REPLICA_EARLY=0 (no
  * early batch), PBFT_EARLY_PARTS (parts, default 8), PBFT_REPLICA_DIRECT=0 (flush_submit fills the context's
- * staging instead of handing the arena over), PBFT_APPLY_PREFETCH=0, PBFT_REPLICA_THREADS (threads, default 16). */
+ * staging instead of handing the arena over), PBFT_APPLY_PREFETCH=0; read once: PBFT_REPLICA_THREADS (worker
+ * threads, default 16), PBFT_STREAM_STORES=0 (plain stores for the rows). */
 int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, const uint64_t *view, const uint64_t *seq,
                            const uint8_t *digests, const uint32_t *signer, const uint8_t *sigs, uint64_t *queued);
 
