@@ -331,10 +331,10 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     windows are recycled from round to round, as a running replica's are) receives each round's 2048 signed
     PrePrepares and 2^20 Prepare / Commit votes (pbft_replica_push_many: the per-row checks and window inserts on
     the worker pool, each window's rows on one thread, every vote's 72-byte staged row written into the replica's
-    pinned row arena as it is pushed), then ONE pbft_replica_flush_submit (the arena handed to the GPU as it is:
-    pbft_verify_votes_submit_host, each chunk's H2D straight from it; r05, VERDICT r04 item 6 -- before, the flush
-    filled the context's staging from the windows, a second pass over every vote) and pbft_replica_flush_poll from
-    the loop until the bitmap is applied and the events are out.  Timed: push_many -> last poll (`value`), and submit -> last poll (`flush_*`).  Round r
+    pinned row arena as it is pushed, and the arena's verification launched in parts while the threads push: r05,
+    VERDICT r04 item 6 -- before, the flush filled the context's staging from the windows, a second pass over every
+    vote, and only then copied it), then ONE pbft_replica_flush_submit (adopts that batch) and
+    pbft_replica_flush_poll from the loop until the bitmap is applied and the events are out.  Timed: push_many -> last poll (`value`), and submit -> last poll (`flush_*`).  Round r
     covers seqs r * 2048 + 1 .. (r + 1) * 2048 (every round re-signed on the GPU: new envelopes); its bitmap
     pattern is the headline round's.  n_ctx > 1: pbft_replica_create_multi over the context and n_ctx - 1 clones
     (each context stages, launches and returns its own slice of the batch; on a node they would
@@ -434,9 +434,10 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             "gpu_wait_ms": max(0.0, med["flush_ms"] - med["submit_ms"] - med["apply_ms"]),  # (medians of separate series)
             "polls_while_running": int(med["polls"]), "sigs": n + n_seq, "rounds": rounds, "contexts": n_ctx,
             "path": "one long-lived pbft_replica: push_many (2^20 votes, each one's 72-B staged row written into "
-                    "the replica's pinned row arena; + 2048 PrePrepares via on_pre_prepare, untimed) -> flush_submit "
-                    "(the arena handed to the GPU as it is: every chunk's H2D + kernels + bitmap words launched at "
-                    "once; PBFT_REPLICA_DIRECT=0: filled into the context's staging by worker threads instead) -> "
+                    "the replica's pinned row arena, the arena launched in 8 parts -- H2D + kernels -- as the worker "
+                    "threads finish them; + 2048 PrePrepares via on_pre_prepare, untimed) -> flush_submit (adopts that "
+                    "early batch; PBFT_REPLICA_EARLY=0: hands the arena over as it is, PBFT_REPLICA_DIRECT=0: fills "
+                    "the context's staging instead) -> "
                     "flush_poll loop applying each chunk's rows as its bitmap words land, until 2048 COMMITTED_LOCAL "
                     "events are out; value = votes / (push_many + flush); H2D 72 B/sig + 4096 envelopes; apply_ms = "
                     "time inside flush_poll applying, gpu_wait_ms = the rest of the polling"}
