@@ -185,17 +185,18 @@ static inline void stream_fence() {
 
 struct Window {
   Phase ph[3];  // [0] PrePrepare candidates, [1] Prepare, [2] Commit
+  uint64_t seq = 0;        // its (current-view) sequence number: the ring slot seq & ring_mask holds it
   uint64_t push_call = 0;  // the last push_many that routed rows here, and the thread it gave the window to
   uint32_t push_owner = 0;
   bool have_pre_prepare = false;
+  bool dirty = false;      // in pbft_replica::dirty (events to be re-evaluated)
   Digest digest{};
   bool pre_prepared_reported = false, prepared_reported = false, committed_reported = false;
   void reset() {
     for (Phase& p : ph) p.reset();
-    have_pre_prepare = pre_prepared_reported = prepared_reported = committed_reported = false;
+    have_pre_prepare = pre_prepared_reported = prepared_reported = committed_reported = dirty = false;
   }
 };
-using WindowMap = std::map<std::pair<uint64_t, uint64_t>, Window>;
 
 // One phase of the in-flight batch: rows [row0, row0 + count) are its first `count` candidates.
 struct Seg {
@@ -347,13 +348,25 @@ struct pbft_replica {
   uint64_t log_window = PBFT_DEFAULT_LOG_WINDOW;
   std::vector<uint8_t> keys;
   std::unordered_map<std::string, uint32_t> key_index;
-  WindowMap windows;
-  std::vector<WindowMap::node_type> spare;  // GC'd windows kept for reuse (no allocation per round)
-  std::set<Key> dirty;                    // windows whose events must be (re-)evaluated
+  // Window store (r06): every window is of the current view (the reference has no view change,
+  // src/view.rs) and its seq lies in (h, h + log_window], a dense range: a ring of 2^k >= log_window slots indexed by
+  // seq holds them, so a lookup, an insertion, the flush's ordered walk and the GC's committed-prefix step are O(1)
+  // per window instead of std::map operations.  Live windows' seqs are distinct modulo the ring size because h only
+  // moves in gc(), which drops every window <= h in the same call, and the ring never shrinks.
+  std::vector<Window*> ring;              // [seq & ring_mask]: the live window of that seq, or null
+  uint64_t ring_mask = 0;
+  std::vector<std::unique_ptr<Window>> win_pool;  // every window ever allocated (recycled through win_free)
+  std::vector<Window*> win_free;
+  size_t n_windows = 0;
+  uint64_t win_hi = 0;                    // every live window's seq is <= win_hi
+  uint64_t gc_h = 0;                      // every window <= gc_h has been dropped
+  std::vector<uint64_t> dirty;            // seqs of windows whose events must be (re-)evaluated
   std::deque<pbft_round_event> evq;       // decided, not yet delivered
   std::map<uint64_t, uint64_t> done;      // seqs of current_view committed locally and GC'd: [lo, hi]
-  Key last_key{~0ull, ~0ull};             // push fast path: the last window looked up
+  uint64_t last_seq = ~0ull;              // push fast path: the last window looked up
   Window* last_w = nullptr;
+  pbft_ctx* dctx = nullptr;               // the replica's own clone of ctx for request digests (r06): a digest
+                                          // never waits for the votes batch on ctx (nor pushes an open one out)
   pbft_batch_verify_fn verify_fn = nullptr;
   void* verify_user = nullptr;
   pbft_votes_submit_fn vsub = nullptr;
@@ -593,35 +606,58 @@ static bool commit_ready(const pbft_replica* r, const Window& w) {
 
 static std::string key_str(const uint8_t* A) { return std::string((const char*)A, 32); }
 
-static Window& window_at(pbft_replica* r, const Key& k) {
-  if (r->last_w && r->last_key == k) return *r->last_w;
-  // (rounds arrive in ascending (view, seq): a key above the last window's is new and goes at the end, no search)
-  const bool above = r->windows.empty() || r->windows.rbegin()->first < k;
-  auto it = above ? r->windows.end() : r->windows.find(k);
-  if (it == r->windows.end()) {
-    if (!r->spare.empty()) {
-      auto nh = std::move(r->spare.back());
-      r->spare.pop_back();
-      nh.key() = k;
-      nh.mapped().reset();
-      it = r->windows.insert(above ? r->windows.end() : r->windows.lower_bound(k), std::move(nh));
+// ---- window ring ----
+static constexpr uint64_t MAX_LOG_WINDOW = 1ull << 24;  // (pbft_replica_set_log_window; the ring's slots are 8 B)
+// room for live seqs (h, h + span]: the ring grows to a power of two >= span, re-slotting the live windows
+static void ring_reserve(pbft_replica* r, uint64_t span) {
+  uint64_t R = 1024;
+  while (R < span) R <<= 1;
+  if (R <= r->ring.size()) return;
+  std::vector<Window*> nr(R, nullptr);
+  for (Window* w : r->ring)
+    if (w) nr[w->seq & (R - 1)] = w;
+  r->ring.swap(nr);
+  r->ring_mask = R - 1;
+}
+// the live window of (view, seq), or null
+static inline Window* find_window(const pbft_replica* r, uint64_t view, uint64_t seq) {
+  if (view != r->current_view) return nullptr;
+  Window* w = r->ring[seq & r->ring_mask];
+  return w && w->seq == seq ? w : nullptr;
+}
+// the window of (current view, seq), created if absent; seq must be in the log (in_log)
+static Window& window_at(pbft_replica* r, uint64_t seq) {
+  if (r->last_w && r->last_seq == seq) return *r->last_w;
+  Window*& s = r->ring[seq & r->ring_mask];
+  if (!s) {
+    Window* w;
+    if (!r->win_free.empty()) {
+      w = r->win_free.back();
+      r->win_free.pop_back();
+      w->reset();
     } else {
-      it = r->windows.emplace_hint(above ? r->windows.end() : r->windows.lower_bound(k), k, Window());
+      r->win_pool.emplace_back(new Window());
+      w = r->win_pool.back().get();
     }
+    w->seq = seq;
+    s = w;
+    ++r->n_windows;
+    if (seq > r->win_hi) r->win_hi = seq;
   }
-  r->last_key = k;
-  r->last_w = &it->second;
-  return it->second;
+  r->last_seq = seq;
+  r->last_w = s;
+  return *s;
 }
 
-// erase a window, keeping its node (and every vector in it) for the next window
-static WindowMap::iterator drop_window(pbft_replica* r, WindowMap::iterator it) {
-  auto next = std::next(it);
+// erase a window, keeping it (and every vector in it) for the next window
+static void drop_window(pbft_replica* r, Window* w) {
   if (r->in_flight) r->erased_in_flight = true;
-  release_window(r, it->second);  // (an in-flight batch skips the window's rows: erased_in_flight)
-  if (r->spare.size() < 4096) r->spare.push_back(r->windows.extract(it));
-  else r->windows.erase(it);
-  return next;
+  release_window(r, *w);  // (an in-flight batch skips the window's rows: erased_in_flight)
+  r->ring[w->seq & r->ring_mask] = nullptr;
+  --r->n_windows;
+  w->seq = 0;  // (no seq in the log is 0: a recycled window matches no lookup until it is reused)
+  r->win_free.push_back(w);
+  if (r->last_w == w) r->last_w = nullptr;
 }
 
 // seqs of the current view committed locally whose windows are gone (interval set)
@@ -671,33 +707,36 @@ static bool is_done(const pbft_replica* r, uint64_t view, uint64_t seq) {
 
 static void gc(pbft_replica* r) {
   r->last_w = nullptr;  // windows may go away
-  // committed prefix: h advances over consecutive committed windows of the current view (one ordered walk:
-  // they are neighbours in the map)
+  // committed prefix: h advances over consecutive committed windows (ring slot h + 1, h + 2, ...)
   const uint64_t h0 = r->h;
-  for (auto it = r->windows.lower_bound({r->current_view, r->h + 1});
-       it != r->windows.end() && it->first.first == r->current_view && it->first.second == r->h + 1 &&
-       it->second.committed_reported;) {
-    if (!r->dirty.empty()) r->dirty.erase(it->first);
-    it = drop_window(r, it);
+  for (;;) {
+    Window* w = find_window(r, r->current_view, r->h + 1);
+    if (!w || !w->committed_reported) break;
+    drop_window(r, w);
     ++r->h;
     ++r->stats.windows_gc;
   }
   if (r->h > h0) record_done_range(r, h0 + 1, r->h);
-  // anything at or below h (stable checkpoint, or stale views); the in-flight rows of an erased window are
-  // skipped when the batch completes
-  for (auto it = r->windows.begin(); it != r->windows.end();) {
-    if (it->first.second <= r->h) {
-      if (it->second.committed_reported && it->first.first == r->current_view) record_done(r, it->first.second);
-      r->dirty.erase(it->first);
-      it = drop_window(r, it);
+  // anything else at or below h (a stable checkpoint moved it): seqs (gc_h, h], or every slot when that range is
+  // longer than the ring; the in-flight rows of an erased window are skipped when the batch completes (a dropped
+  // window's dirty entry finds no window at evaluate())
+  if (r->h > r->gc_h && r->n_windows) {
+    auto drop_low = [r](Window* w) {
+      if (w->committed_reported) record_done(r, w->seq);
+      drop_window(r, w);
       ++r->stats.windows_gc;
-    } else if (it->first.first == ~0ull) {
-      break;
+    };
+    if (r->h - r->gc_h <= r->ring.size()) {
+      for (uint64_t q = r->gc_h + 1; q <= r->h && r->n_windows; ++q) {
+        Window* w = r->ring[q & r->ring_mask];
+        if (w && w->seq == q) drop_low(w);
+      }
     } else {
-      // every later window of this view has a higher seq: on to the next view
-      it = r->windows.lower_bound({it->first.first + 1, 0});
+      for (Window* w : std::vector<Window*>(r->ring))
+        if (w && w->seq <= r->h) drop_low(w);
     }
   }
+  if (r->h > r->gc_h) r->gc_h = r->h;
 }
 
 // The events one window's state now decides (pre-prepared, prepared :177-182, committed_local :214-223), appended
@@ -723,17 +762,21 @@ static void evaluate_window(const pbft_replica* r, uint64_t view, uint64_t seq, 
 // or not the caller has room for it.  (Windows completed by a batch are evaluated as they are applied,
 // apply_range; `dirty` holds the rest.)
 static void evaluate(pbft_replica* r) {
-  auto wi = r->windows.begin();
-  for (const Key& k : r->dirty) {
-    // both sorted by key: advance (a lookup when the next dirty key is far ahead)
-    if (wi != r->windows.end() && wi->first < k) {
-      auto nx = std::next(wi);
-      wi = (nx != r->windows.end() && nx->first >= k) ? nx : r->windows.lower_bound(k);
-    }
-    if (wi == r->windows.end() || wi->first != k) continue;
-    evaluate_window(r, k.first, k.second, wi->second, r->evq);
+  if (r->dirty.empty()) return;
+  std::sort(r->dirty.begin(), r->dirty.end());
+  for (uint64_t q : r->dirty) {
+    Window* w = find_window(r, r->current_view, q);
+    if (!w || !w->dirty) continue;  // (gone, or already evaluated: a duplicate entry)
+    w->dirty = false;
+    evaluate_window(r, r->current_view, q, *w, r->evq);
   }
   r->dirty.clear();
+}
+static void mark_window_dirty(pbft_replica* r, Window& w) {
+  if (!w.dirty) {
+    w.dirty = true;
+    r->dirty.push_back(w.seq);
+  }
 }
 
 static void drain(pbft_replica* r, pbft_round_event* events, uint32_t max_events, uint32_t* n_events) {
@@ -750,9 +793,9 @@ static void mark_dirty(pbft_replica* r);
 static void revert_segs(pbft_replica* r) {
   for (size_t gi = r->seg_next; gi < r->segs.size(); ++gi) {  // (segments applied before the failure stay)
     const Seg& g = r->segs[gi];
-    auto wi = r->windows.find(g.key);
-    if (wi == r->windows.end()) continue;
-    Phase& p = wi->second.ph[g.kind];
+    Window* wp = find_window(r, g.key.first, g.key.second);
+    if (!wp) continue;
+    Phase& p = wp->ph[g.kind];
     const uint32_t back = std::min<uint32_t>(p.n_flight, (uint32_t)p.size());  // (the batch's: the first ones)
     p.n_pending += back;
     p.n_flight = 0;
@@ -800,9 +843,8 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
     if (pf && gi + 1 < s1 && !r->erased_in_flight) prefetch_phase(r->segs[gi + 1].w->ph[r->segs[gi + 1].kind]);
     Window* wp = g.w;
     if (r->erased_in_flight) {
-      auto wi = r->windows.find(g.key);
-      if (wi == r->windows.end()) continue;  // window erased (stable checkpoint) while the batch was in flight
-      wp = &wi->second;
+      wp = find_window(r, g.key.first, g.key.second);
+      if (!wp) continue;  // window erased (stable checkpoint) while the batch was in flight
     }
     Window& w = *wp;
     Phase& p = w.ph[g.kind];
@@ -940,8 +982,11 @@ static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
 
 // the batch is done: its windows with accepted candidates are evaluated next
 static void mark_dirty(pbft_replica* r) {
-  for (size_t gi = 0; gi < r->seg_next; ++gi)  // segments come in window (key) order: O(1) hinted inserts
-    if (r->touched[gi]) r->dirty.emplace_hint(r->dirty.end(), r->segs[gi].key);
+  for (size_t gi = 0; gi < r->seg_next; ++gi)
+    if (r->touched[gi]) {
+      Window* w = find_window(r, r->segs[gi].key.first, r->segs[gi].key.second);
+      if (w) mark_window_dirty(r, *w);
+    }
 }
 
 static void finish_batch(pbft_replica* r) {
@@ -1223,6 +1268,7 @@ int pbft_replica_create_multi(pbft_ctx* const* ctxs, uint32_t n_ctx, uint32_t n,
   r->self = self_id;
   r->keys.assign(keys, keys + 32 * (size_t)n);
   for (uint32_t i = 0; i < n; ++i) r->key_index.emplace(key_str(keys + 32 * (size_t)i), i);  // first index wins
+  ring_reserve(r, r->log_window);
   *out = r;
   return PBFT_OK;
 }
@@ -1323,7 +1369,8 @@ int pbft_replica_set_digest_fn(pbft_replica* r, pbft_digest_fn fn, void* user) {
 }
 
 int pbft_replica_set_log_window(pbft_replica* r, uint64_t log_window) {
-  if (!r || log_window == 0) return PBFT_EINVAL;
+  if (!r || log_window == 0 || log_window > MAX_LOG_WINDOW) return PBFT_EINVAL;
+  ring_reserve(r, log_window);
   r->log_window = log_window;
   return PBFT_OK;
 }
@@ -1359,7 +1406,7 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
   if (memcmp(d, claimed_digest, 64) != 0) { ++r->stats.rejected_digest; return 0; }  // validate_digest :139-145
   if (view != r->current_view) { ++r->stats.rejected_view; return 0; }                // :134-141
   if (!in_log(r, seq)) { ++r->stats.rejected_watermark; return 0; }                   // h/H TODO :154
-  Window& w = window_at(r, {view, seq});
+  Window& w = window_at(r, seq);
   if (w.have_pre_prepare) {                                                           // :144-151
     if (memcmp(w.digest.data(), d, 64) != 0) ++r->stats.rejected_digest; else ++r->stats.duplicates;
     return 0;
@@ -1444,7 +1491,7 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
   else if (!in_log(r, seq)) ++c.rejected_watermark;
   else {
     Sink sk = single_sink(r);
-    rc = push_into(r, window_at(r, {view, seq}), kind, view, seq, digest, signer, sig, c, sk);
+    rc = push_into(r, window_at(r, seq), kind, view, seq, digest, signer, sig, c, sk);
     sink_done(sk);
   }
   add_counts(r, c);
@@ -1520,7 +1567,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     const uint64_t call = ++r->push_calls;
     std::vector<uint64_t> t_rows(T, 0), t_envs(T, 64);
     for (Run& u : runs) {
-      Window& w = window_at(r, {r->current_view, u.seq});
+      Window& w = window_at(r, u.seq);
       u.w = &w;
       u.first = w.push_call != call;
       if (u.first) {  // the window's first run in this call: its owner
@@ -1859,15 +1906,17 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   r->segs.clear();
   uint64_t N = 0;
   uint32_t E = 0;
-  for (auto& kv : r->windows) {
-    Window& w = kv.second;
-    const uint64_t view = kv.first.first;
+  const uint64_t view = r->current_view;
+  for (uint64_t q = r->h + 1; q <= r->win_hi && r->n_windows; ++q) {  // (the ring in seq order)
+    Window* wp = r->ring[q & r->ring_mask];
+    if (!wp || wp->seq != q) continue;
+    Window& w = *wp;
     const bool rd[3] = {w.ph[0].n_pending > 0, force ? w.ph[1].n_pending > 0 : prepare_ready(r, view, w),
                         force ? w.ph[2].n_pending > 0 : commit_ready(r, w)};
     for (int kind = 0; kind < 3; ++kind) {
       if (!rd[kind]) continue;
       Phase& p = w.ph[kind];
-      r->segs.push_back({&w, kv.first, N, N + p.size(), (uint32_t)p.size(), E, (uint8_t)kind});
+      r->segs.push_back({&w, Key{view, q}, N, N + p.size(), (uint32_t)p.size(), E, (uint8_t)kind});
       N += p.size();
       E += (uint32_t)p.digs.size();
     }
@@ -2047,7 +2096,7 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
     RTRACE(r, "evaluate", r->evq.size());
     gc(r);
     r->stats.apply_ns += ns_since(t0);
-    RTRACE(r, "gc", r->windows.size());
+    RTRACE(r, "gc", r->n_windows);
     if (g_trace && !r->trace.empty()) {
       const uint64_t t_0 = r->trace.front().ns;
       fprintf(stderr, "replica-trace:");
@@ -2152,22 +2201,20 @@ int pbft_replica_stable_checkpoint(pbft_replica* r, uint64_t seq) {
 // moves h without deciding anything here).
 int pbft_replica_prepared(pbft_replica* r, uint64_t view, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
-  auto it = r->windows.find({view, seq});
-  if (it != r->windows.end()) return is_prepared(r, view, it->second) ? 1 : 0;
+  if (const Window* w = find_window(r, view, seq)) return is_prepared(r, view, *w) ? 1 : 0;
   return is_done(r, view, seq) ? 1 : 0;
 }
 
 int pbft_replica_committed_local(pbft_replica* r, uint64_t view, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
-  auto it = r->windows.find({view, seq});
-  if (it != r->windows.end()) return is_committed_local(r, view, it->second) ? 1 : 0;
+  if (const Window* w = find_window(r, view, seq)) return is_committed_local(r, view, *w) ? 1 : 0;
   return is_done(r, view, seq) ? 1 : 0;
 }
 
 int pbft_replica_get_stats(pbft_replica* r, pbft_replica_stats* out) {
   if (!r || !out) return PBFT_EINVAL;
   r->stats.low_watermark = r->h;
-  r->stats.live_windows = r->windows.size();
+  r->stats.live_windows = r->n_windows;
   *out = r->stats;
   return PBFT_OK;
 }
