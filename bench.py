@@ -180,8 +180,11 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
     for c in ctxs:  # warm: workspace / staging allocation
         c.wait(c.submit(batches[0]))
     period = batch / offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else 0.0
-    pending = [None] * n_ctx  # (ticket, scheduled time)
+    pending = [None] * n_ctx  # (ticket, scheduled time, submit start, submit end)
     lat, done = [], 0
+    rec = []  # per batch: (latency, queue delay, submit, wait, largest gap between polls while waiting) in ms
+    gap_since = [0.0] * n_ctx  # per context: the largest gap between consecutive poll passes while it was pending
+    last_pass = time.perf_counter()
     import gc
     gc.collect()
     gc.disable()  # no collector pause inside the timed loop (a host-side tail, not the verifier's)
@@ -189,10 +192,16 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
     k = 0
     while True:
         now = time.perf_counter()
+        gap = now - last_pass
+        last_pass = now
         for ci, p in enumerate(pending):
+            if p is not None:
+                gap_since[ci] = max(gap_since[ci], gap)
             if p is not None and ctxs[ci].poll(p[0]) is not None:
                 t = time.perf_counter()
                 lat.append((t - p[1]) * 1e3)
+                rec.append(((t - p[1]) * 1e3, (p[2] - p[1]) * 1e3, (p[3] - p[2]) * 1e3, (t - p[3]) * 1e3,
+                            gap_since[ci] * 1e3))
                 pending[ci] = None
                 done += 1
         if now - t0 >= duration_s:
@@ -203,17 +212,30 @@ def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int 
         if now >= t_sched:
             ci = k % n_ctx
             if pending[ci] is not None:  # backlog: this stream is still busy
-                ctxs[ci].wait(pending[ci][0])
-                lat.append((time.perf_counter() - pending[ci][1]) * 1e3)
+                p = pending[ci]
+                ctxs[ci].wait(p[0])
+                t = time.perf_counter()
+                lat.append((t - p[1]) * 1e3)
+                rec.append(((t - p[1]) * 1e3, (p[2] - p[1]) * 1e3, (p[3] - p[2]) * 1e3, (t - p[3]) * 1e3,
+                            gap_since[ci] * 1e3))
                 done += 1
-            pending[ci] = (ctxs[ci].submit(batches[k % len(batches)]), t_sched if period else time.perf_counter())
+            ts = time.perf_counter()
+            tk = ctxs[ci].submit(batches[k % len(batches)])
+            pending[ci] = (tk, t_sched if period else ts, ts, time.perf_counter())
+            gap_since[ci] = 0.0
             k += 1
     wall = time.perf_counter() - t0
     gc.enable()
     for c in ctxs:
         c.close()
     lat = np.array(lat)
-    return {"batch": batch, "streams": n_ctx,
+    worst = max(rec, key=lambda x: x[0]) if rec else (0, 0, 0, 0, 0)
+    # the slowest batch's phases: queue (its scheduled arrival -> the submit call: the loop was busy elsewhere),
+    # submit (the host call: staging / import kernel / launches), wait (submit return -> the poll that saw its bitmap:
+    # GPU time + wake-up), and the largest gap between two poll passes meanwhile (> ~0.1 ms: this Python thread was
+    # descheduled, a host-side stall, not the verifier)
+    max_batch = dict(zip(("latency_ms", "queue_ms", "submit_ms", "wait_ms", "max_poll_gap_ms"), map(float, worst)))
+    return {"batch": batch, "streams": n_ctx, "max_batch": max_batch,
             "offered_sigs_per_s": offered_sigs_per_s if np.isfinite(offered_sigs_per_s) else None,
             "achieved_sigs_per_s": done * batch / wall, "batches": int(done),
             "p50_ms": float(np.median(lat)), "p99_ms": float(np.percentile(lat, 99)),
@@ -355,6 +377,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     primary = 1 % n_rep
     bad = ~expect
     res = {k: [] for k in ("push_ms", "submit_ms", "flush_ms", "total_ms", "polls", "apply_ms")}
+    phases = []  # per timed round: the replica's own phase timings (pbft_replica_get_timings)
     ev = (Event * 16384)()
     rep = ctypes.c_void_p()
     clones = [v.clone() for _ in range(n_ctx - 1)]
@@ -413,6 +436,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             res["total_ms"].append((t2 - t) * 1e3)
             res["polls"].append(polls)
             res["apply_ms"].append((st.apply_ns - st_prev.apply_ns) * 1e-6)
+            phases.append(replica_timings(L, rep))
             mode_of.append(modes[r % len(modes)] if modes else None)
         st_prev = st
     if modes:
@@ -421,6 +445,9 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     for c in clones:
         c.close()
     med = {k: float(np.median(x)) for k, x in res.items()}
+    worst = int(np.argmax(res["total_ms"]))  # the slowest round, with its phases
+    max_round = {"total_ms": res["total_ms"][worst], "push_many_ms": res["push_ms"][worst],
+                 "flush_ms": res["flush_ms"][worst], "phases": phases[worst]}
     by_mode = None
     if modes:
         by_mode = {m: {k: float(np.median([x for x, mm in zip(v_, mode_of) if mm == m])) for k, v_ in res.items()}
@@ -428,6 +455,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     return {"value": n / (med["total_ms"] * 1e-3), "unit": "verifies/s", "ms_per_round": med["total_ms"],
             **({"by_mode": by_mode} if by_mode else {}),
             "ms_per_round_min_max": [float(np.min(res["total_ms"])), float(np.max(res["total_ms"]))],
+            "ms_per_round_mean": float(np.mean(res["total_ms"])), "max_round": max_round,
             "push_many_ms": med["push_ms"], "flush_ms": med["flush_ms"],
             "flush_verifies_per_s": n / (med["flush_ms"] * 1e-3),
             "flush_submit_ms": med["submit_ms"], "apply_ms": med["apply_ms"],
@@ -441,6 +469,144 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
                     "flush_poll loop applying each chunk's rows as its bitmap words land, until 2048 COMMITTED_LOCAL "
                     "events are out; value = votes / (push_many + flush); H2D 72 B/sig + 4096 envelopes; apply_ms = "
                     "time inside flush_poll applying, gpu_wait_ms = the rest of the polling"}
+
+
+TIMING_FIELDS = ("push_checks_ns", "push_windows_ns", "push_rows_ns", "submit_segs_ns", "submit_launch_ns", "wait_ns",
+                 "apply_partial_ns", "apply_final_ns", "gc_ns", "polls", "early_pieces", "early_piece_ns",
+                 "early_last_rows")
+
+
+def replica_timings(L, rep):
+    """pbft_replica_get_timings of the last push_many / flush (include/pbft_replica.h), in ms (counts as they are)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from replica_sim import Timings
+    tm = Timings()
+    assert L.pbft_replica_get_timings(rep, ctypes.byref(tm)) == 0
+    return {k.replace("_ns", "_ms"): (getattr(tm, k) * 1e-6 if k.endswith("_ns") else int(getattr(tm, k)))
+            for k in TIMING_FIELDS}
+
+
+def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
+    """config #4's round delivered to ONE long-lived pbft_replica the way the reference's caller
+    delivers it -- one message at a time on ONE thread (the swarm's poll loop -> Pbft::inject_node_event,
+    /root/reference/src/behavior.rs:304, arms :340-412) -- then flush_submit -> flush_poll.
+    The loops run natively (tools/ingress/ingress_driver.cpp) and time themselves around the calls into the product:
+      push         one pbft_replica_push per vote, in arrival order;
+      records_1    each of the 256 connections' byte stream of 160-B binary records (built untimed with
+                   pbft_amd.wire.records_pack), the loop visiting the connections round-robin and handing ONE record
+                   per visit to pbft_replica_push_records;
+      records_64   the same, 64 records (10 KiB, one socket read's worth) per visit;
+      json_1       each connection's UviBytes/JSON frames (pbft_amd.wire.encode_votes), one frame per visit to
+                   pbft_replica_push_frames.
+    Round-robin visits deliver the round in time order: for seq, for kind, every peer's vote.  The signed PrePrepares
+    (on_pre_prepare, GPU digest) are delivered first, untimed.  With a flush behind it (the first rounds) the
+    single-message path opens the arena as a batch in pieces on the GPU while the votes arrive (r06), so the flush is
+    the last piece, the GPU's tail and the application.  Per mode: ingress votes/s (the loop alone), end to end
+    ((ingress + flush)), and the replica's own phase timings of its slowest round (pbft_replica_get_timings)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from replica_sim import Event, Stats, lib
+    from pbft_amd import wire
+    from pbft_amd.native_build import INGRESS_LIB
+    L = lib()
+    D = ctypes.CDLL(INGRESS_LIB)
+    vp = ctypes.c_void_p
+    D.ingress_push.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp]
+    D.ingress_streams.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
+    n_rep = len(pub)
+    n = 2 * n_rep * n_seq
+    modes = modes or [("push", 2, True), ("push", 3, False), ("records_1", 3, False), ("records_64", 2, False),
+                      ("json_1", 1, False)]
+    primary = 1 % n_rep
+    ev = (Event * 16384)()
+    rep = ctypes.c_void_p()
+    assert L.pbft_replica_create(v._ctx.value, n_rep, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+    kind = np.tile(np.repeat(np.array([1, 2], np.uint8), n_rep), n_seq)
+    signer = np.tile(np.arange(n_rep, dtype=np.uint32), 2 * n_seq)
+    view = np.ones(n, np.uint64)
+    key_idx = signer.astype(np.uint16)
+    res = {}
+    st_prev = Stats()
+    L.pbft_replica_get_stats(rep, ctypes.byref(st_prev))
+    rnd = 0
+    try:
+        for mode, rounds, warm in modes:
+            out = res.setdefault(mode, {"ingress_ms": [], "flush_ms": [], "timings": []}) if not warm else None
+            for _ in range(rounds):
+                seq0 = 1 + (1 << 20) + rnd * n_seq  # (seqs past the replica_flush leg's)
+                rnd += 1
+                m, _ = envelopes(seq0, n_seq, n_rep)
+                Rr, Sr, _ = v.sign(seeds, key_idx, m, ENVELOPE)
+                Sr[bad] = S_bad[bad]
+                seq = np.repeat(np.arange(seq0, seq0 + n_seq, dtype=np.uint64), 2 * n_rep)
+                digs = np.ascontiguousarray(m[:, 21:85])
+                sigs = np.ascontiguousarray(np.concatenate([Rr, Sr], axis=1))
+                pp_env = m[::2 * n_rep].copy()
+                pp_env[:, 4] = 0
+                pR, pS, _ = v.sign(seeds, np.full(n_seq, primary, np.uint16), pp_env, ENVELOPE)
+                for q in range(n_seq):
+                    op = b"op-" + str(seq0 + q).encode()
+                    assert L.pbft_replica_on_pre_prepare(rep, primary, 1, seq0 + q, op, len(op),
+                                                         digs[2 * n_rep * q].tobytes(),
+                                                         pR[q].tobytes() + pS[q].tobytes(), None) == 1
+                sec = ctypes.c_double()
+                if mode == "push":
+                    qd = ctypes.c_uint64()
+                    assert D.ingress_push(rep, n, kind.ctypes.data, view.ctypes.data, seq.ctypes.data,
+                                          digs.ctypes.data, signer.ctypes.data, sigs.ctypes.data, ctypes.byref(qd),
+                                          ctypes.byref(sec)) == 0 and qd.value == n
+                else:
+                    binary, per_visit = mode.startswith("records"), int(mode.split("_")[1])
+                    streams = []
+                    for c in range(n_rep):
+                        sel = slice(c, None, n_rep)  # peer c's votes in (seq, kind) order
+                        if binary:
+                            streams.append(wire.records_pack(Rr[sel], Sr[sel], key_idx[sel], m[sel]).reshape(-1))
+                        else:
+                            streams.append(wire.encode_votes(kind[sel], view[sel], seq[sel], digs[sel], signer[sel],
+                                                             sigs[sel]))
+                    ptrs = (ctypes.c_void_p * n_rep)(*[s_.ctypes.data for s_ in streams])
+                    lens = (ctypes.c_uint64 * n_rep)(*[len(s_) for s_ in streams])
+                    pushed, dropped, calls = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+                    assert D.ingress_streams(rep, int(binary), n_rep, ptrs, lens, per_visit, ctypes.byref(pushed),
+                                             ctypes.byref(dropped), ctypes.byref(calls), ctypes.byref(sec)) == 0
+                    assert pushed.value == n and dropped.value == 0, (pushed.value, dropped.value)
+                rows = ctypes.c_uint64()
+                ne = ctypes.c_uint32()
+                t0 = time.perf_counter()
+                assert L.pbft_replica_flush_submit(rep, 0, ctypes.byref(rows)) == 0
+                while True:
+                    rc = L.pbft_replica_flush_poll(rep, ev, len(ev), ctypes.byref(ne))
+                    assert rc >= 0
+                    if rc == 1:
+                        break
+                t1 = time.perf_counter()
+                assert rows.value == n + n_seq
+                st = Stats()
+                L.pbft_replica_get_stats(rep, ctypes.byref(st))
+                assert st.rejected_sig - st_prev.rejected_sig == int(bad.sum()), "ingress round: rejected votes differ"
+                assert sum(1 for e in ev[: ne.value] if e.kind == 2) == n_seq, "ingress round: not every seq committed"
+                st_prev = st
+                if out is not None:
+                    out["ingress_ms"].append(sec.value * 1e3)
+                    out["flush_ms"].append((t1 - t0) * 1e3)
+                    out["timings"].append(replica_timings(L, rep))
+    finally:
+        L.pbft_replica_destroy(rep)
+    legs = {}
+    for mode, o in res.items():
+        ing, fl = np.array(o["ingress_ms"]), np.array(o["flush_ms"])
+        tot = ing + fl
+        worst = int(np.argmax(tot))
+        legs[mode] = {"ingress_votes_per_s": n / (np.median(ing) * 1e-3), "ingress_ms": float(np.median(ing)),
+                      "flush_ms": float(np.median(fl)), "flush_ms_max": float(fl.max()),
+                      "end_to_end_votes_per_s": n / (np.median(tot) * 1e-3), "rounds": len(ing),
+                      "max_round": {"ingress_ms": float(ing[worst]), "flush_ms": float(fl[worst]),
+                                    "phases": o["timings"][worst]}}
+    return {"votes": n, "prepreprares_untimed": n_seq, "thread": "one (the caller's)", "modes": legs,
+            "path": "tools/ingress/ingress_driver.cpp loops -> pbft_replica_push / _push_records / _push_frames "
+                    "(one message, or one 64-record read, per call; connections round-robin) -> flush_submit -> "
+                    "flush_poll until every seq is COMMITTED_LOCAL; the single-message early batch launched in "
+                    "2^16-row pieces while the votes arrive"}
 
 
 def plan_legs(v, pub, d, n, stream, torch):
@@ -964,6 +1130,8 @@ def main():
         # the same round through pbft_replica_create_multi over this context + 1 clone (one slice each; on a node the
         # contexts would be two GPUs with a PCIe link each -- here both share this GPU and its link)
         extras["replica_flush_2^20_2ctx"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, n_ctx=2)
+        # the reference-shaped ingress: one message at a time on one thread
+        extras["replica_ingress_2^20"] = replica_ingress_leg(v, seeds, pub, S, ~expect, n_seq)
         extras["shuffled_2^20"] = shuffled_leg(v, d, n, stream, torch, dev, expect)
         # the C ABI's single-process multi-GPU form on this process's one GPU (a 1-rank RCCL communicator): its
         # bitmap must equal the headline path's; unmeasured on 8 GPUs in this pipeline

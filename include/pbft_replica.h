@@ -17,7 +17,8 @@
  *                                the signer is the AUTHENTICATED peer (the reference
  *                                keys votes by the connection's peer_id, :346, :380)
  *   pbft_replica_push_frames     PbftHandler -> message_to_handler_event
- *                                src/handler.rs:533-548 for one connection
+ *   pbft_replica_push_records    src/handler.rs:533-548 for one connection (UviBytes/
+ *                                JSON frames, or 160-byte binary records)
  *   pbft_replica_flush_submit    the batched validation, non-blocking: every ready
  *   pbft_replica_flush_poll      sub-window's signatures in ONE GPU batch (votes
  *                                form, written into the verifier's pinned staging),
@@ -114,6 +115,24 @@ typedef struct {
   uint64_t submit_ns;          /* host time inside pbft_replica_flush_submit (batch build + launch), summed */
   uint64_t apply_ns;           /* host time applying finished batches (bitmap -> votes, quorums, GC), summed */
 } pbft_replica_stats;
+
+/* Where the last push_many and the last flush spent their time (host clock, ns), so that a slow round can be
+ * attributed from the record that shows it.  pbft_replica_get_timings copies them. */
+typedef struct {
+  uint64_t push_checks_ns;   /* the last pbft_replica_push_many: per-row checks (worker threads)                 */
+  uint64_t push_windows_ns;  /*   the windows of its runs (serial, on the calling thread)                         */
+  uint64_t push_rows_ns;     /*   the rows pushed (worker threads; with the early batch, its launches)            */
+  uint64_t submit_segs_ns;   /* the last flush_submit that launched: the walk over the windows (segments)         */
+  uint64_t submit_launch_ns; /*   the rest of it: adoption of an early batch, or the fill / copies / launches      */
+  uint64_t wait_ns;          /* its batch: from the end of flush_submit to the flush_poll that found it complete  */
+  uint64_t apply_partial_ns; /*   chunks applied by flush_poll while it ran                                       */
+  uint64_t apply_final_ns;   /*   the rest applied once complete                                                  */
+  uint64_t gc_ns;            /*   the evaluation of dirty windows and the GC after it                             */
+  uint64_t polls;            /*   flush_poll calls that found it running                                          */
+  uint64_t early_pieces;     /* single pushes before that flush_submit: early-batch pieces launched...            */
+  uint64_t early_piece_ns;   /*   ...and the pushing thread's time inside those launches                          */
+  uint64_t early_last_rows;  /* rows flush_submit launched as the early batch's last piece                        */
+} pbft_replica_timings;
 
 /* Optional verifier override (tests without a GPU): same SoA contract as
  * pbft_verify_batch; returns 0 and fills bitmap_out. */
@@ -219,6 +238,14 @@ int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, con
  * read).  Returns 0, or PBFT_EINVAL on a framing error. */
 int pbft_replica_push_frames(pbft_replica *r, uint32_t peer_idx, const uint8_t *stream, size_t len,
                              uint64_t *consumed, uint64_t *pushed, uint64_t *dropped);
+/* The same from one connection's stream of 160-byte binary records (PBFT_RECORD_BYTES, include/pbft_wire.h:
+ * R || S, the 85-byte signed envelope, the signer's key index LE at byte 150), the zero-copy alternative to JSON
+ * frames: Prepare / Commit records whose key index equals peer_idx are pushed, others counted
+ * in *dropped (a record whose key index is not the connection's peer also in rejected_signer; PrePrepares need
+ * their operation bytes: on_pre_prepare or a JSON frame).  *consumed = bytes of whole records.  Returns 0 or the
+ * first negative code of a push (then *consumed stops before that record). */
+int pbft_replica_push_records(pbft_replica *r, uint32_t peer_idx, const uint8_t *stream, size_t len,
+                              uint64_t *consumed, uint64_t *pushed, uint64_t *dropped);
 
 /* Non-blocking flush.  _submit: collect every READY sub-window (force = every pending candidate) into one
  * batch and launch it; *n_rows = its signatures (0: nothing launched); PBFT_EBUSY while a batch is in flight.
@@ -244,6 +271,7 @@ int pbft_replica_stable_checkpoint(pbft_replica *r, uint64_t seq);
 int pbft_replica_prepared(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_committed_local(pbft_replica *r, uint64_t view, uint64_t seq);
 int pbft_replica_get_stats(pbft_replica *r, pbft_replica_stats *out);
+int pbft_replica_get_timings(pbft_replica *r, pbft_replica_timings *out);
 
 /* libp2p PeerId <-> Ed25519 key.  A PeerId of an Ed25519 identity is the
  * identity multihash of the protobuf-encoded public key: 00 24 08 01 12 20 || A.

@@ -79,6 +79,13 @@ int pbft_verify_set_keys(pbft_ctx *ctx, const uint8_t *A, uint32_t n, uint8_t *k
  * unchanged; otherwise the m slots' key_ok is cleared in the shared set (every
  * context holding it rejects signatures under them; the other keys work). */
 int pbft_verify_update_keys(pbft_ctx *ctx, const uint32_t *idx, const uint8_t *A, uint32_t m, uint8_t *key_ok);
+/* Slots idx[0..m) of the installed set reject every signature from now on (key_ok cleared in the shared set; the
+ * tables stay) until a later set_keys / update_keys installs them again -- a replica whose key update failed on
+ * one of its contexts revokes the slots on all of them (pbft_replica_update_keys).  Synchronises the device. */
+int pbft_verify_revoke_keys(pbft_ctx *ctx, const uint32_t *idx, uint32_t m);
+/* *id = an identity of the key set the context verifies against, equal for contexts sharing one
+ * (pbft_verify_ctx_clone); 0 without a key set. */
+int pbft_verify_key_set_id(pbft_ctx *ctx, uint64_t *id);
 
 /* Phases of the last pbft_verify_set_keys / pbft_verify_update_keys on this
  * context (host wall time, ms). */

@@ -109,6 +109,14 @@ int pbft_wire_decode_votes(const uint8_t *stream, size_t len, uint32_t n_replica
                            uint8_t *msg, uint8_t *kind, uint64_t *view, uint64_t *seq, uint64_t *n_frames,
                            uint64_t *n_rows, uint64_t *consumed);
 
+/* N signed votes (kind[i] Prepare / Commit, view, seq, digest[64], replica, sig = R || S) as consecutive UviBytes
+ * frames of their JSON Messages -- what a replica's connection carries when it multicasts its votes (the egress side
+ * of pbft_replica_push_frames).  *len = the stream's full length; returns 0, or PBFT_EINVAL if cap is too small
+ * (then *len still tells the length needed) or a kind is not a vote. */
+int pbft_wire_encode_votes(uint64_t N, const uint8_t *kind, const uint64_t *view, const uint64_t *seq,
+                           const uint8_t *digests, const uint32_t *replica, const uint8_t *sigs, uint8_t *out,
+                           size_t cap, size_t *len);
+
 /* Pack SoA rows into 160-byte binary records (layout above) and back. */
 int pbft_records_pack(const uint8_t *R, const uint8_t *S, const uint16_t *key_idx, const uint8_t *msg,
                       uint32_t msg_stride, uint64_t N, uint8_t *records);

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("PBFT_VERIFY_LIB") or os.path.join(_HERE, "libpbft_ver
 # every symbol include/pbft_verify.h declares
 EXPORTS = (
     "pbft_verify_ctx_create", "pbft_verify_ctx_destroy", "pbft_verify_ctx_clone", "pbft_verify_set_keys",
-    "pbft_verify_update_keys", "pbft_verify_key_stats",
+    "pbft_verify_update_keys", "pbft_verify_key_stats", "pbft_verify_revoke_keys", "pbft_verify_key_set_id",
     "pbft_verify_batch", "pbft_verify_batch_multi", "pbft_verify_batch_async", "pbft_verify_poll", "pbft_verify_wait",
     "pbft_verify_batch_device", "pbft_verify_reserve", "pbft_digest_blake2b512", "pbft_digest_sha256",
     "pbft_sign_batch", "pbft_last_error", "pbft_build_info", "pbft_last_kernel_ms", "pbft_verify_ctx_info",
@@ -25,7 +25,7 @@ EXPORTS = (
     # include/pbft_wire.h
     "pbft_uvi_encode", "pbft_uvi_decode", "pbft_wire_encode_json", "pbft_wire_encode_frame",
     "pbft_wire_decode_json", "pbft_wire_decode_votes", "pbft_records_pack", "pbft_verify_records_device",
-    "pbft_verify_records",
+    "pbft_verify_records", "pbft_wire_encode_votes",
 )
 
 ERRORS = {0: "PBFT_OK", -1: "PBFT_EINVAL", -2: "PBFT_EHIP", -3: "PBFT_ENOKEYS",
@@ -109,6 +109,9 @@ def load() -> ctypes.CDLL:
         "pbft_wire_decode_votes": (i32, [u8p, ctypes.c_size_t, u32, u64, u64, vp, vp, vp, vp, vp, vp, vp, vp,
                                          vp, vp, vp]),
         "pbft_records_pack": (i32, [vp, vp, vp, vp, u32, u64, vp]),
+        "pbft_wire_encode_votes": (i32, [u64, vp, vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp]),
+        "pbft_verify_revoke_keys": (i32, [vp, vp, u32]),
+        "pbft_verify_key_set_id": (i32, [vp, ctypes.POINTER(u64)]),
         "pbft_verify_records_device": (i32, [vp, vp, u64, vp, vp]),
         "pbft_verify_records": (i32, [vp, vp, u64, vp]),
     }

@@ -331,11 +331,17 @@ struct pbft_replica {
   struct {
     bool active = false;  // a batch covers arena `arena` rows [0, rows) and envelopes [0, envs); bits -> bitmap
     bool done = false;    // waited for: every bit is in r->bitmap
+    bool open = false;    // (single pushes, r06) still open on ctx: pieces [0, rows) launched, more may follow
     uint32_t arena = 0;
     uint64_t rows = 0;
     uint32_t envs = 0;
     std::vector<uint64_t> lo;  // context j (ctxs[j]) verifies rows [lo[j], lo[j + 1]) (one context: {0, rows})
   } eu;
+  pbft_replica_timings tm{};      // phases of the last push_many / flush (pbft_replica_get_timings)
+  uint64_t early_pieces = 0, early_piece_ns = 0;  // the single pushes' early batch since the last flush_submit
+  std::chrono::steady_clock::time_point t_submit_end{};
+  uint64_t peak_rows = 0;  // the largest arena a flush has taken, and its envelopes (the single pushes' early batch
+  uint32_t peak_envs = 0;  // sizes the arena for a whole round before it opens: pieces read it in place)
   uint32_t busy_arena = 0;
   uint64_t applied_upto = 0;  // rows_done at the last progressive application
   bool adopted = false;       // the batch in flight is push_many's early batch: applied once, when done (its rows
@@ -407,6 +413,12 @@ static bool early_enabled() {  // PBFT_REPLICA_EARLY=0: push_many never launches
 // wait for the early batch (the context is needed, or its arena is about to change); its bits stay adoptable
 static int eu_settle(pbft_replica* r) {
   if (!r->eu.active || r->eu.done) return PBFT_OK;
+  if (r->eu.open) {  // an open batch cannot be waited for: dropped (a close that does not match drains and drops it)
+    (void)pbft_verify_votes_close(r->ctx, 0);
+    r->eu.open = false;
+    r->eu.active = false;
+    return PBFT_OK;
+  }
   int rc = PBFT_OK;
   for (size_t j = 0; j + 1 < r->eu.lo.size(); ++j) {
     const int w = pbft_verify_wait(r->ctxs[j]);
@@ -529,14 +541,15 @@ struct Sink {
 };
 static Sink single_sink(pbft_replica* r) {
   Arena& a = push_arena(r);
-  return Sink{&a, r->cur, a.n, ~0ull, a.ne, ~0u, true, false};
+  return Sink{&a, r->cur, a.n, ~0ull, a.ne, ~0u, true, g_stream_stores};
 }
 static void sink_done(Sink& s) {  // (single sinks) the arena's counts
   if (s.grow) {
     s.a->n = s.row;
     s.a->ne = s.env;
   }
-  s.a->live.fetch_add(s.added, std::memory_order_relaxed);
+  // (single pushes run on the caller's thread with no worker touching the counts: a plain update, not an RMW)
+  s.a->live.store(s.a->live.load(std::memory_order_relaxed) + s.added, std::memory_order_relaxed);
   s.added = 0;
 }
 static uint32_t sink_env(pbft_replica* r, Sink& s, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t* d) {
@@ -564,6 +577,62 @@ static bool sink_row(pbft_replica* r, Sink& s, uint64_t* idx) {
   }
   *idx = s.row++;
   return true;
+}
+
+// ---- the single-message path's early batch (r06) ----
+// Messages delivered one at a time (pbft_replica_push, _push_frames, _push_records, on_pre_prepare: the reference's
+// inject_node_event, one message per call on its swarm thread, src/behavior.rs:304) write their rows into the current
+// arena in arrival order.  Once a piece's worth of rows is in, the arena is opened as a batch in pieces on the context
+// (pbft_verify_votes_open) and every further piece is launched (pbft_verify_votes_piece) while the caller keeps
+// pushing, so at the flush only the last < piece + 64 rows are left to copy and verify: flush_submit launches them,
+// closes the batch and adopts it (one context; a replica over several contexts hands its arena over at the flush).
+// PBFT_EARLY_PIECE: rows per piece (default 2^16; read once -- this runs on every push).
+static uint64_t early_piece_rows() {
+  static const uint64_t rows = [] {
+    const char* e = getenv("PBFT_EARLY_PIECE");
+    const long long v = e ? strtoll(e, nullptr, 10) : (1 << 16);
+    return (uint64_t)(v < 4096 ? 4096 : v > (1 << 22) ? (1 << 22) : v) & ~(uint64_t)63;
+  }();
+  return rows;
+}
+static void early_single(pbft_replica* r) {
+  if (r->eu.active && !r->eu.open) return;  // push_many's batch (closed): nothing to add
+  Arena& A = r->arena[r->cur];
+  const uint64_t piece = early_piece_rows();
+  if (!r->eu.active) {
+    // (not before a flush has shown the round's size: the arena is sized for the round before it opens)
+    if (A.n < piece || r->peak_rows == 0 || !early_enabled() || !direct_enabled() || !r->ctx || r->ctxs.size() != 1 || r->verify_fn ||
+        r->vsub || r->in_flight || A.busy || !A.rows_pinned || !A.envs_pinned || !A.clean.load(std::memory_order_relaxed))
+      return;
+    // room for the whole round first (the pieces read the arena in place: it must not move while the batch is open)
+    const uint64_t want = std::max<uint64_t>(2 * A.n, r->peak_rows + r->peak_rows / 8);
+    const uint64_t want_e = std::max<uint64_t>(2 * (uint64_t)A.ne + 256, r->peak_envs + r->peak_envs / 8);
+    if (!arena_reserve(r, A, want - A.n, want_e > A.ne ? want_e - A.ne : 0) || !A.rows_pinned || !A.envs_pinned)
+      return;
+    r->bitmap.assign((A.cap + 63) / 64, 0);
+    if (pbft_verify_votes_open(r->ctx, A.cap, A.ecap, r->bitmap.data()) != PBFT_OK) return;
+    r->eu.active = true;
+    r->eu.open = true;
+    r->eu.done = false;
+    r->eu.arena = r->cur;
+    r->eu.rows = 0;
+    r->eu.envs = 0;
+    r->eu.lo.assign({0, A.cap});
+    RTRACE(r, "early_open", A.n);
+  }
+  if (r->eu.arena != r->cur || A.n - r->eu.rows < piece) return;
+  const uint64_t hi = A.n & ~(uint64_t)63;
+  const uint64_t t0 = now_ns();
+  stream_fence();  // (the rows' streaming stores are visible before the copy engine reads them)
+  const int rc = pbft_verify_votes_piece(r->ctx, A.rows, r->eu.rows, hi, A.envs, r->eu.envs, A.ne);
+  r->early_piece_ns += now_ns() - t0;
+  ++r->early_pieces;
+  if (rc != PBFT_OK) {
+    r->eu.active = r->eu.open = false;  // (a failing piece drops the batch; the flush verifies the arena again)
+    return;
+  }
+  r->eu.rows = hi;
+  r->eu.envs = A.ne;
 }
 
 static bool in_log(const pbft_replica* r, uint64_t seq) { return seq > r->h && seq - r->h <= r->log_window; }
@@ -1187,18 +1256,28 @@ static int fill_and_launch_multi(pbft_replica* r, size_t T, uint32_t E, size_t* 
   for (size_t k = 1; k < K; ++k) memcpy(st[k].envelopes, env0, (size_t)PBFT_ENVELOPE_BYTES * E);
   RTRACE(r, "envs", E);
   int rc = PBFT_OK;
+  size_t failed = K;  // the context whose call failed (its batch is dropped by that call, or was never opened)
   for (size_t k = 0; k < K && rc == PBFT_OK; ++k) {
     rc = pbft_verify_votes_submit_begin(r->ctxs[k], r->slice_lo[k + 1] - r->slice_lo[k], E,
                                         r->bitmap.data() + r->slice_lo[k] / 64);
     if (rc == PBFT_OK) *opened = k + 1;
+    else failed = k;
   }
   RTRACE(r, "begin", r->rows_span);
   for (size_t q = 0; q < S && rc == PBFT_OK; ++q) {
     while (done[q].load(std::memory_order_acquire) < T) std::this_thread::yield();
     rc = pbft_verify_votes_submit_rows(r->ctxs[steps[q].k], steps[q].launch_rows);
+    if (rc) failed = steps[q].k;
     RTRACE(r, "launched", q);
   }
   WorkerPool::get().wait();
+  if (rc) {
+    // the other opened contexts' batches may still be open (not every chunk launched), and
+    // pbft_verify_wait refuses an open batch -- they would stay in flight for good.  Their staging is complete now
+    // (the workers have joined): launch the rest of each, so the caller's waits drain them.
+    for (size_t k = 0; k < *opened; ++k)
+      if (k != failed) (void)pbft_verify_votes_submit_rows(r->ctxs[k], r->slice_lo[k + 1] - r->slice_lo[k]);
+  }
   return rc;
 }
 
@@ -1291,9 +1370,25 @@ int pbft_replica_update_keys(pbft_replica* r, const uint32_t* idx, const uint8_t
   }
   if (r->ctx && m) {
     eu_drop(r);  // (its bits were computed under the old keys)
-    for (size_t k = 0; k < r->ctxs.size(); ++k) {  // every GPU's key set (a clone listed twice: rebuilt twice)
-      const int rc = pbft_verify_update_keys(r->ctxs[k], idx, A, m, key_ok);
-      if (rc) return rc;
+    // every GPU's key set, once per set (clones share one: ADVICE r05, it used to be rebuilt per context)
+    std::vector<uint64_t> sets;
+    int rc = PBFT_OK;
+    for (size_t k = 0; k < r->ctxs.size() && rc == PBFT_OK; ++k) {
+      uint64_t id = 0;
+      if (pbft_verify_key_set_id(r->ctxs[k], &id) == PBFT_OK && id &&
+          std::find(sets.begin(), sets.end(), id) != sets.end())
+        continue;
+      rc = pbft_verify_update_keys(r->ctxs[k], idx, A, m, key_ok);
+      if (rc == PBFT_OK) sets.push_back(id);
+    }
+    if (rc) {
+      // All or nothing across the replica's contexts (contexts 0..k-1 held the new keys, context
+      // k the old or a cleared slot, and the PeerId map the old identity -- a vote's bit depended on its slice): the
+      // updated slots are revoked on EVERY context, rebuilt or not, and keys / key_index keep the old identity, so
+      // every context rejects the slots' votes until a retry installs the new keys everywhere.
+      for (pbft_ctx* c : r->ctxs) (void)pbft_verify_revoke_keys(c, idx, m);
+      if (key_ok) memset(key_ok, 0, m);
+      return rc;
     }
   } else if (key_ok) {
     memset(key_ok, 1, m);  // (no GPU context: the installed verifier override judges the keys)
@@ -1335,6 +1430,7 @@ int pbft_replica_destroy(pbft_replica* r) {
     host_mem_free(r, a.rows, a.rows_pinned);
     host_mem_free(r, a.envs, a.envs_pinned);
   }
+  if (r->dctx) (void)pbft_verify_ctx_destroy(r->dctx);
   delete r;
   return PBFT_OK;
 }
@@ -1394,11 +1490,16 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
     rc = r->digest_fn(r->digest_user, op, op_len, d);
   } else {
     if (!r->ctx) return PBFT_ENODEV;
-    rc = eu_settle(r);  // (the context must be idle)
-    if (rc) return rc;
+    // on the replica's own clone of the context (its stream, the shared tables): never behind, nor in the way of,
+    // the votes batch on ctx -- an early batch still open or running (the digest used to wait for it and
+    // fail with its error)
+    if (!r->dctx && (rc = pbft_verify_ctx_clone(r->ctx, &r->dctx)) != PBFT_OK) {
+      r->dctx = nullptr;
+      return rc;
+    }
     const uint64_t off = 0;
     const uint8_t empty = 0;
-    rc = pbft_digest_blake2b512(r->ctx, op_len ? op : &empty, &off, &op_len, 1, d);
+    rc = pbft_digest_blake2b512(r->dctx, op_len ? op : &empty, &off, &op_len, 1, d);
   }
   if (rc) return rc;
   if (digest_out) memcpy(digest_out, d, 64);
@@ -1422,10 +1523,11 @@ int pbft_replica_on_pre_prepare(pbft_replica* r, uint32_t peer_idx, uint64_t vie
   const uint32_t env = j >= 0 && p.dgen[(size_t)j] == s.a->gen ? p.denv[(size_t)j] : sink_env(r, s, 0, view, seq, d);
   uint64_t ri;
   if (!sink_row(r, s, &ri)) { sink_done(s); return PBFT_ENOMEM; }
-  put_row(s.a->rows + ROWB * ri, primary_sig, prim, env, false);
+  put_row(s.a->rows + ROWB * ri, primary_sig, prim, env, s.nt);
   p.append(d, j, prim, s.aid << 31 | (uint32_t)ri, env, s.a->gen);
   ++s.added;
   sink_done(s);
+  early_single(r);
   return 1;
 }
 
@@ -1481,9 +1583,62 @@ static void add_counts(pbft_replica* r, const PushCounts& c) {
 }
 
 // inject_node_event Prepare / Commit arms (src/behavior.rs:340-412): enqueue into the round window
+static inline bool eq64(const uint8_t* a, const uint8_t* b) {  // 64 bytes, branch-free
+  uint64_t x = 0;
+  for (int q = 0; q < 8; ++q) {
+    uint64_t u, v;
+    memcpy(&u, a + 8 * q, 8);
+    memcpy(&v, b + 8 * q, 8);
+    x |= u ^ v;
+  }
+  return x == 0;
+}
+
+// The common single push in one branch-light pass (r06, VERDICT r05 item 1: the reference's ingress is one message
+// per call on one thread, so the per-vote cost of this call bounds a replica's ingest): the window is the last one
+// looked up or in the ring, its phase already holds exactly this digest with an envelope in the current arena, the
+// signer has neither a candidate nor an accepted vote there, and the arena and the phase's columns have room.  The
+// outcome is the general path's (push_into) for the same vote; anything else takes the general path.
+static inline int push_fast(pbft_replica* r, uint8_t kind, uint64_t seq, const uint8_t* digest, uint32_t signer,
+                            const uint8_t* sig) {
+  Window* w = r->last_w && r->last_seq == seq ? r->last_w : nullptr;
+  if (!w) {
+    Window* x = r->ring[seq & r->ring_mask];
+    if (!x || x->seq != seq) return -1;
+    r->last_seq = seq;
+    r->last_w = w = x;
+  }
+  if (w->committed_reported) return -1;
+  Phase& p = w->ph[kind];
+  if (p.cnt.empty() || p.digs.size() != 1 || p.cnt[signer] || p.acc[signer] || p.row.size() == p.row.capacity() ||
+      !eq64(p.digs[0].data(), digest))
+    return -1;
+  Arena& A = r->arena[r->cur];
+  if (A.gen == 0 || A.n >= A.cap || p.dgen[0] != A.gen || (A.n > 0 && A.live.load(std::memory_order_relaxed) == 0))
+    return -1;
+  const uint64_t ri = A.n++;
+  put_row(A.rows + ROWB * ri, sig, signer, p.denv[0], g_stream_stores);
+  A.live.store(A.live.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+  p.row.push_back(r->cur << 31 | (uint32_t)ri);
+  p.who.push_back((uint16_t)signer);
+  p.dix.push_back(0);
+  ++p.n_pending;
+  if (ri + 1 > p.row_hi) p.row_hi = ri + 1;
+  ++p.distinct;
+  ++p.cnt[signer];
+  return 1;
+}
+
 int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]) {
   if (!r || !digest || !sig || (kind != PBFT_KIND_PREPARE && kind != PBFT_KIND_COMMIT)) return PBFT_EINVAL;
+  if (signer < r->n && view == r->current_view && in_log(r, seq) && push_fast(r, kind, seq, digest, signer, sig) == 1) {
+    ++r->stats.pushed;
+    const uint64_t n = r->arena[r->cur].n;  // (the early batch's next step is due: every piece's worth of rows)
+    if (r->eu.open ? n - r->eu.rows >= early_piece_rows() : (!r->eu.active && n >= early_piece_rows() && r->peak_rows))
+      early_single(r);
+    return 1;
+  }
   PushCounts c;
   ++c.pushed;
   int rc = 0;
@@ -1493,6 +1648,7 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
     Sink sk = single_sink(r);
     rc = push_into(r, window_at(r, seq), kind, view, seq, digest, signer, sig, c, sk);
     sink_done(sk);
+    if (rc == 1) early_single(r);
   }
   add_counts(r, c);
   return rc;
@@ -1526,6 +1682,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //     one (view, seq); rejected rows are flagged and do not break a run;
     struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; bool first; };
     RTRACE(r, "push", n_ok);
+    const uint64_t tp0 = now_ns();
     std::vector<std::vector<Run>> slice_runs(T);
     std::vector<uint8_t> bad(n_ok);
     std::vector<PushCounts> cnt(T);
@@ -1562,6 +1719,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //     owner: the thread whose share of the rows its first run starts in; each thread's range of the arena:
     //     a row per row it may push, two envelopes per window it owns (one per kind: honest rounds) + 64
     RTRACE(r, "push_checked", T);
+    const uint64_t tp1 = now_ns();
     std::vector<Run> runs;
     for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
     const uint64_t call = ++r->push_calls;
@@ -1666,6 +1824,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     std::unique_ptr<std::atomic<uint32_t>[]> parts_done(new std::atomic<uint32_t>[P]);
     for (size_t k = 0; k < P; ++k) parts_done[k].store(0, std::memory_order_relaxed);
     RTRACE(r, "push_windows", runs.size());
+    const uint64_t tp2 = now_ns();
     //  3. (threads) every thread pushes the rows of the windows it owns, in input order, into its range; the range's
     //     unused rows (rejected pushes) become rows no candidate references (key 0, envelope 0), its unused
     //     envelopes copies of envelope 0
@@ -1770,6 +1929,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       q += c.queued;
     }
     RTRACE(r, "push_done", q);
+    r->tm.push_checks_ns = tp1 - tp0;
+    r->tm.push_windows_ns = tp2 - tp1;
+    r->tm.push_rows_ns = now_ns() - tp2;
     if (g_push_trace && r->trace.size() >= 4) {  // PBFT_PUSH_TRACE (with PBFT_REPLICA_TRACE): pass times of this call
       auto at = [&](const char* what) {
         for (size_t x = r->trace.size(); x-- > 0;)
@@ -1890,8 +2052,19 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows);
 int pbft_replica_flush_submit(pbft_replica* r, int force, uint64_t* n_rows) {
   if (!r) return PBFT_EINVAL;
   const auto t0 = std::chrono::steady_clock::now();
+  const bool busy = r->in_flight;
+  const uint64_t pieces = r->early_pieces, piece_ns = r->early_piece_ns;
   const int rc = flush_submit_impl(r, force, n_rows);
-  r->stats.submit_ns += ns_since(t0);
+  const uint64_t dt = ns_since(t0);
+  r->stats.submit_ns += dt;
+  if (!busy) {  // (the phases of the batch this call launched; a PBFT_EBUSY call leaves the running one's)
+    r->tm.submit_launch_ns = dt > r->tm.submit_segs_ns ? dt - r->tm.submit_segs_ns : 0;
+    r->tm.early_pieces = pieces;
+    r->tm.early_piece_ns = piece_ns;
+    r->early_pieces = r->early_piece_ns = 0;
+    r->tm.wait_ns = r->tm.apply_partial_ns = r->tm.apply_final_ns = r->tm.gc_ns = r->tm.polls = 0;
+    r->t_submit_end = std::chrono::steady_clock::now();
+  }
   RTRACE(r, "submit_end", rc);
   return rc;
 }
@@ -1900,6 +2073,10 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   if (n_rows) *n_rows = 0;
   if (r->in_flight) return PBFT_EBUSY;
   RTRACE(r, "submit", 0);
+  stream_fence();  // (single pushes write their rows with streaming stores: drained before any batch reads them)
+  const uint64_t ts0 = now_ns();
+  r->tm.submit_segs_ns = 0;
+  r->tm.early_last_rows = 0;
   if (!r->verify_fn && !r->vsub && !r->ctx) return PBFT_ENODEV;
   // 1. one segment per ready phase: its candidates (all pending between batches) and its envelopes, one per
   //    distinct (kind, view, seq, digest)
@@ -1925,6 +2102,7 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   r->rows_span = N;
   r->slice_lo.clear();
   RTRACE(r, "segs", r->segs.size());
+  r->tm.submit_segs_ns = now_ns() - ts0;
   if (n_rows) *n_rows = N;
   if (N == 0) { r->segs.clear(); return PBFT_OK; }
   r->applied_upto = 0;
@@ -1935,6 +2113,27 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
     const bool direct = direct_enabled() && r->ctx && !r->verify_fn && !r->vsub && A.rows_pinned && A.envs_pinned &&
                         A.clean.load() && A.gen && B.live.load() == 0 && !B.busy &&
                         (int64_t)N == A.live.load() && A.n <= N + std::max<uint64_t>(4096, N / 16);
+    if (direct) {
+      r->peak_rows = std::max<uint64_t>(r->peak_rows, A.n);
+      r->peak_envs = std::max<uint32_t>(r->peak_envs, A.ne);
+    }
+    if (r->eu.active && r->eu.open && direct && r->eu.arena == r->cur) {
+      // the single pushes' early batch: its last piece (the rows and envelopes since), closed, then adopted
+      int rc = PBFT_OK;
+      if (A.n > r->eu.rows || A.ne > r->eu.envs)
+        rc = pbft_verify_votes_piece(r->ctx, A.rows, r->eu.rows, A.n, A.envs, r->eu.envs, A.ne);
+      RTRACE(r, "early_last", A.n - r->eu.rows);
+      r->tm.early_last_rows = A.n - r->eu.rows;
+      if (rc == PBFT_OK) rc = pbft_verify_votes_close(r->ctx, A.n);
+      r->eu.open = false;
+      if (rc == PBFT_OK) {
+        r->eu.rows = A.n;
+        r->eu.envs = A.ne;
+        r->eu.lo.assign({0, A.n});
+        return adopt_early(r, N);
+      }
+      r->eu.active = false;  // (the failing call dropped the batch: the arena goes over as it is below)
+    }
     if (r->eu.active) {  // push_many's early batch: adopted when it covers exactly this arena as it is now
       if (direct && r->eu.arena == r->cur && A.n == r->eu.rows && A.ne == r->eu.envs) return adopt_early(r, N);
       eu_drop(r);
@@ -2085,16 +2284,22 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
         if (s1 > r->seg_next) r->applied_upto = rows_done;
         apply_segs(r, r->seg_next, s1);
         r->stats.apply_ns += ns_since(t0);
+        r->tm.apply_partial_ns += ns_since(t0);
         RTRACE(r, "applied", s1);
       }
+      ++r->tm.polls;
       return 0;
     }
     RTRACE(r, "done", rows_done);
+    r->tm.wait_ns = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(t0 - r->t_submit_end).count();
     finish_batch(r);
     RTRACE(r, "finish_batch", 0);
+    r->tm.apply_final_ns = ns_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
     evaluate(r);
     RTRACE(r, "evaluate", r->evq.size());
     gc(r);
+    r->tm.gc_ns = ns_since(t1);
     r->stats.apply_ns += ns_since(t0);
     RTRACE(r, "gc", r->n_windows);
     if (g_trace && !r->trace.empty()) {
@@ -2190,6 +2395,43 @@ int pbft_replica_push_frames(pbft_replica* r, uint32_t peer_idx, const uint8_t* 
   return rc;
 }
 
+// One connection's stream of 160-byte binary records (include/pbft_wire.h: R || S, the 85-byte signed envelope, the
+// signer's key index) -- the zero-copy alternative to the UviBytes/JSON frames above: no
+// parsing, the envelope's fields are read in place.  Same rules as the frames: a vote is pushed only when its key index
+// is the authenticated connection's peer; a record that is not a Prepare / Commit envelope is dropped (a PrePrepare
+// needs its operation bytes: pbft_replica_on_pre_prepare or a JSON frame).
+int pbft_replica_push_records(pbft_replica* r, uint32_t peer_idx, const uint8_t* stream, size_t len,
+                              uint64_t* consumed, uint64_t* pushed, uint64_t* dropped) {
+  if (!r || !consumed || (!stream && len)) return PBFT_EINVAL;
+  const size_t n = len / PBFT_RECORD_BYTES;
+  uint64_t np = 0, nd = 0;
+  int rc = 0;
+  size_t i = 0;
+  for (; i < n; ++i) {
+    const uint8_t* rec = stream + (size_t)PBFT_RECORD_BYTES * i;
+    const uint8_t* env = rec + 64;
+    uint16_t key;
+    memcpy(&key, rec + 150, 2);
+    int got = 0;
+    if (memcmp(env, "PBFT", 4) != 0 || (env[4] != PBFT_KIND_PREPARE && env[4] != PBFT_KIND_COMMIT)) {
+      got = 0;
+    } else if (key != peer_idx) {
+      ++r->stats.rejected_signer;  // (the signer is the connection, src/behavior.rs:346, :380)
+    } else {
+      uint64_t view, seq;
+      memcpy(&view, env + 5, 8);
+      memcpy(&seq, env + 13, 8);
+      got = pbft_replica_push(r, env[4], view, seq, env + 21, peer_idx, rec);
+    }
+    if (got < 0) { rc = got; break; }
+    if (got == 1) ++np; else ++nd;
+  }
+  *consumed = (uint64_t)PBFT_RECORD_BYTES * i;
+  if (pushed) *pushed = np;
+  if (dropped) *dropped = nd;
+  return rc;
+}
+
 int pbft_replica_stable_checkpoint(pbft_replica* r, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
   if (seq > r->h) r->h = seq;
@@ -2209,6 +2451,12 @@ int pbft_replica_committed_local(pbft_replica* r, uint64_t view, uint64_t seq) {
   if (!r) return PBFT_EINVAL;
   if (const Window* w = find_window(r, view, seq)) return is_committed_local(r, view, *w) ? 1 : 0;
   return is_done(r, view, seq) ? 1 : 0;
+}
+
+int pbft_replica_get_timings(pbft_replica* r, pbft_replica_timings* out) {
+  if (!r || !out) return PBFT_EINVAL;
+  *out = r->tm;
+  return PBFT_OK;
 }
 
 int pbft_replica_get_stats(pbft_replica* r, pbft_replica_stats* out) {

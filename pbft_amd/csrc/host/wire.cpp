@@ -511,6 +511,35 @@ int pbft_wire_decode_votes(const uint8_t* stream, size_t len, uint32_t n_replica
   return 0;
 }
 
+int pbft_wire_encode_votes(uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
+                           const uint8_t* digests, const uint32_t* replica, const uint8_t* sigs, uint8_t* out,
+                           size_t cap, size_t* len) {
+  if (!len || (N && (!kind || !view || !seq || !digests || !replica || !sigs))) return PBFT_EINVAL;
+  size_t off = 0;
+  int rc = 0;
+  for (uint64_t i = 0; i < N; ++i) {
+    pbft_wire_msg m;
+    memset(&m, 0, sizeof m);
+    m.kind = kind[i];
+    m.view = view[i];
+    m.seq = seq[i];
+    memcpy(m.digest, digests + 64 * i, 64);
+    m.digest_ok = 1;
+    m.has_sig = 1;
+    m.replica = replica[i];
+    memcpy(m.sig, sigs + 64 * i, 64);
+    if (m.kind != PBFT_MSG_PREPARE && m.kind != PBFT_MSG_COMMIT) return PBFT_EINVAL;
+    size_t fl = 0;
+    const bool room = out && off <= cap;
+    const int e = pbft_wire_encode_frame(&m, room ? out + off : nullptr, room ? cap - off : 0, &fl);
+    if (fl == 0) return PBFT_EINVAL;
+    if (e) rc = PBFT_EINVAL;  // (no room: keep counting the length)
+    off += fl;
+  }
+  *len = off;
+  return rc;
+}
+
 int pbft_records_pack(const uint8_t* R, const uint8_t* S, const uint16_t* key_idx, const uint8_t* msg,
                       uint32_t msg_stride, uint64_t N, uint8_t* records) {
   if (N && (!R || !S || !key_idx || !msg || !records || msg_stride < PBFT_ENVELOPE_BYTES)) return PBFT_EINVAL;

@@ -1253,6 +1253,41 @@ int pbft_verify_update_keys(pbft_ctx* c, const uint32_t* idx, const uint8_t* A, 
   return PBFT_OK;
 }
 
+// Slots idx[0..m) of the context's key set reject every signature from now on (key_ok cleared; the tables stay):
+// pbft_replica_update_keys uses it to leave no context of a replica verifying a key its PeerId map does not hold
+// after an update failed on one of them.  A later set_keys / update_keys of a slot admits it again.
+int pbft_verify_revoke_keys(pbft_ctx* c, const uint32_t* idx, uint32_t m) {
+  if (!c || (m && !idx)) return set_err(PBFT_EINVAL, "null argument");
+  if (c->in_flight) return set_err(PBFT_EBUSY, "async batch in flight");
+  if (!c->ks) return set_err(PBFT_ENOKEYS, "pbft_verify_set_keys not called");
+  for (uint32_t i = 0; i < m; ++i)
+    if (idx[i] >= c->n_keys) return set_err(PBFT_EINVAL, "key index out of range");
+  if (m == 0) return PBFT_OK;
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipDeviceSynchronize());  // (no launch of a clone is reading key_ok while it changes)
+  uint32_t* d_idx = nullptr;
+  HIP_TRY(hipMalloc(&d_idx, 4 * (size_t)m));
+  int rc = PBFT_OK;
+  if (hipMemcpyAsync(d_idx, idx, 4 * (size_t)m, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    rc = set_err(PBFT_EHIP, "revoke upload");
+  if (!rc) {
+    hipLaunchKernelGGL(clear_key_ok_kernel, dim3((m + 255) / 256), dim3(256), 0, c->stream, c->ks->d_key_ok,
+                       (const uint32_t*)d_idx, m);
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess)
+      rc = set_err(PBFT_EHIP, "revoke kernel");
+  }
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(d_idx);
+  return rc;
+}
+
+// An identity of the key set the context verifies against (shared by its clones: pbft_verify_ctx_clone); 0 = none.
+int pbft_verify_key_set_id(pbft_ctx* c, uint64_t* id) {
+  if (!c || !id) return set_err(PBFT_EINVAL, "null argument");
+  *id = (uint64_t)(uintptr_t)c->ks;
+  return PBFT_OK;
+}
+
 int pbft_verify_key_stats(pbft_ctx* c, pbft_key_stats* out) {
   if (!c || !out) return set_err(PBFT_EINVAL, "null argument");
   *out = c->kstats;

@@ -72,5 +72,18 @@ def build_library(out: str = LIB, defines=(), objdir: str | None = None, jobs: i
             f.result()
     objs = hip_objs + host_objs
     if todo or _stale(out, objs):
-        _run([HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-o", out] + objs)
+        _run([HIPCC, "--offload-arch=gfx950", "-fPIC", "-shared", "-Wl,-soname,libpbft_verify.so", "-o", out] + objs)
     return out
+
+
+INGRESS_SRC = os.path.join(ROOT, "tools", "ingress", "ingress_driver.cpp")
+INGRESS_LIB = os.path.join(ROOT, "tools", "ingress", "libingress.so")
+
+
+def build_ingress_driver() -> str:
+    """Bench infrastructure: the single-threaded ingress loops of bench.py's replica_ingress leg
+    (tools/ingress/ingress_driver.cpp), linked against the in-tree library."""
+    if _stale(INGRESS_LIB, [INGRESS_SRC, LIB] + _headers()):
+        _run(["g++"] + HOST_FLAGS + ["-shared", "-o", INGRESS_LIB, INGRESS_SRC, "-L" + os.path.dirname(LIB),
+                                     "-lpbft_verify", "-Wl,-rpath,$ORIGIN/../../pbft_amd"])
+    return INGRESS_LIB

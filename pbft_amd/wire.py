@@ -145,3 +145,19 @@ def records_pack(R, S, key_idx, msg, msg_stride: int = ENVELOPE) -> np.ndarray:
     check(load().pbft_records_pack(R.ctypes.data, S.ctypes.data, K.ctypes.data, M.ctypes.data, msg_stride, n,
                                    out.ctypes.data))
     return out
+
+
+def encode_votes(kind, view, seq, digests, replica, sigs) -> np.ndarray:
+    """N signed votes as one stream of UviBytes/JSON frames (include/pbft_wire.h pbft_wire_encode_votes): what one
+    connection carries (uint8 array)."""
+    lib = load()
+    k = np.ascontiguousarray(kind, np.uint8)
+    v, q = np.ascontiguousarray(view, np.uint64), np.ascontiguousarray(seq, np.uint64)
+    d, s = np.ascontiguousarray(digests, np.uint8), np.ascontiguousarray(sigs, np.uint8)
+    r = np.ascontiguousarray(replica, np.uint32)
+    n = ctypes.c_size_t()
+    args = (len(k), k.ctypes.data, v.ctypes.data, q.ctypes.data, d.ctypes.data, r.ctypes.data, s.ctypes.data)
+    lib.pbft_wire_encode_votes(*args, None, 0, ctypes.byref(n))
+    out = np.zeros(max(1, n.value), np.uint8)
+    check(lib.pbft_wire_encode_votes(*args, out.ctypes.data, n.value, ctypes.byref(n)))
+    return out[: n.value]

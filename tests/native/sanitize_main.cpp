@@ -43,10 +43,11 @@ int pbft_verify_batch(pbft_ctx*, const uint8_t*, const uint8_t*, const uint16_t*
 int pbft_digest_blake2b512(pbft_ctx*, const uint8_t*, const uint64_t*, const uint32_t*, uint64_t, uint8_t*) {
   return PBFT_ENODEV;
 }
-int pbft_verify_update_keys(pbft_ctx*, const uint32_t*, const uint8_t*, uint32_t m, uint8_t* key_ok) {
-  if (key_ok) memset(key_ok, 1, m);
-  return PBFT_OK;
+int pbft_verify_ctx_clone(pbft_ctx*, pbft_ctx** out) {  // (the replica's digest clone: the tests install digest_fn)
+  *out = nullptr;
+  return PBFT_ENODEV;
 }
+int pbft_verify_ctx_destroy(pbft_ctx*) { return PBFT_OK; }
 }
 
 // A fake GPU context for the replica's progressive votes path (pbft_verify_votes_stage / _submit_begin / _rows /
@@ -66,11 +67,17 @@ struct FakeGpu {
   uint32_t n_env = 0, n_keys = 0;
   uint64_t* out = nullptr;
   bool staged = false, open = false, in_flight = false;
-  uint64_t batches = 0, chunk_launches = 0, direct_batches = 0, early_batches = 0, ext_hash = 0;
+  uint64_t batches = 0, chunk_launches = 0, direct_batches = 0, early_batches = 0, ext_hash = 0, dropped = 0;
   bool pieces = false;  // opened with pbft_verify_votes_open
   uint32_t env_cap = 0;
   std::vector<std::array<uint64_t, 3>> piece_hash;  // (lo, hi, hash of the rows when the piece was launched)
   uint32_t lag = 1, polls = 0;  // polls per chunk landing (3 contexts: each slice is one chunk of the schedule)
+  // fault injection: the next submit_begin fails / the submit_rows call that launches chunk `fail_rows_at` fails
+  // (dropping the batch) / the next update_keys fails; key set identity (contexts sharing one: equal ids)
+  bool fail_begin = false, fail_update = false;
+  int fail_rows_at = -1;
+  uint64_t set_id = 0, updates = 0;
+  std::vector<uint32_t> revoked;
 };
 static uint64_t fnv(const uint8_t* p, size_t n) {
   uint64_t h = 1469598103934665603ull;
@@ -98,6 +105,11 @@ int pbft_verify_votes_stage(pbft_ctx* c, uint64_t N, uint32_t n_env, pbft_votes_
 int pbft_verify_votes_submit_begin(pbft_ctx* c, uint64_t N, uint32_t n_env, uint64_t* out) {
   FakeGpu* g = (FakeGpu*)c;
   CHECK(g && g->staged && N == g->N && n_env == g->n_env && out);
+  if (g->fail_begin) {
+    g->fail_begin = false;
+    g->staged = false;
+    return PBFT_EHIP;
+  }
   for (uint32_t e = 0; e < n_env; ++e) CHECK(memcmp(&g->env[(size_t)PBFT_ENVELOPE_BYTES * e], "PBFT", 4) == 0);
   g->staged = false; g->open = true; g->in_flight = true; g->out = out; g->launched = g->done = 0;
   ++g->batches;
@@ -105,7 +117,14 @@ int pbft_verify_votes_submit_begin(pbft_ctx* c, uint64_t N, uint32_t n_env, uint
 }
 int pbft_verify_votes_submit_rows(pbft_ctx* c, uint64_t rows) {
   FakeGpu* g = (FakeGpu*)c;
-  CHECK(g && g->open);
+  CHECK(g);
+  if (!g->open) return PBFT_EINVAL;  // (as the library: no progressive batch open)
+  if (g->fail_rows_at >= 0 && (uint64_t)g->fail_rows_at <= g->chunk_launches) {
+    g->fail_rows_at = -1;
+    g->open = false;
+    g->in_flight = false;  // (a failing _submit_rows drops the batch)
+    return PBFT_EHIP;
+  }
   uint64_t upto = g->launched;  // every whole chunk of the library's schedule inside [0, rows)
   while (upto < g->N && PBFT_VOTES_CHUNK_END(upto, g->N) <= (rows >= g->N ? g->N : rows))
     upto = PBFT_VOTES_CHUNK_END(upto, g->N);
@@ -180,10 +199,37 @@ int pbft_verify_votes_piece(pbft_ctx* c, const uint8_t* rows, uint64_t lo, uint6
 }
 int pbft_verify_votes_close(pbft_ctx* c, uint64_t n) {
   FakeGpu* g = (FakeGpu*)c;
-  CHECK(g && g->open && g->pieces && n == g->launched && n);
+  CHECK(g && g->open && g->pieces);
+  if (n != g->launched || n == 0) {  // (as the library: a close that does not match drops the batch)
+    g->open = false;
+    g->in_flight = false;
+    ++g->dropped;
+    return PBFT_EINVAL;
+  }
   g->open = false;
   g->N = n;
   return 0;
+}
+int pbft_verify_update_keys(pbft_ctx* c, const uint32_t*, const uint8_t*, uint32_t m, uint8_t* key_ok) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && !g->in_flight);
+  if (g->fail_update) {
+    g->fail_update = false;
+    return PBFT_EHIP;
+  }
+  ++g->updates;
+  if (key_ok) memset(key_ok, 1, m);
+  return PBFT_OK;
+}
+int pbft_verify_revoke_keys(pbft_ctx* c, const uint32_t* idx, uint32_t m) {
+  FakeGpu* g = (FakeGpu*)c;
+  CHECK(g && !g->in_flight);
+  g->revoked.insert(g->revoked.end(), idx, idx + m);
+  return PBFT_OK;
+}
+int pbft_verify_key_set_id(pbft_ctx* c, uint64_t* id) {
+  *id = ((FakeGpu*)c)->set_id;
+  return PBFT_OK;
 }
 int pbft_host_alloc(pbft_ctx*, size_t bytes, void** out) {
   *out = malloc(bytes);
@@ -824,6 +870,160 @@ static void test_replica_early_dropped(int how) {
   printf("replica early batch dropped (%s): %u commits\n", how == 0 ? "late PrePrepare" : "key update", committed);
 }
 
+// ---- 7. the single-message path's early batch (r06): rounds delivered one vote at a time (pbft_replica_push, and
+// binary records through pbft_replica_push_records) -- the first round sizes the arena (no early batch), later ones
+// open the arena as a batch in pieces while the votes arrive and the flush adopts it; one round drops it half-way by
+// a key update, one by outgrowing the arena; every round commits every seq (forged votes rejected) ------------------
+static void test_replica_single_early() {
+  const uint32_t n = 64, seqs = 600;  // 76,800 votes + 600 PrePrepares per round: pieces of 2^16 rows
+  std::vector<uint8_t> keys(32 * (size_t)n);
+  for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = 9; }
+  FakeGpu g;
+  g.n_keys = n;
+  pbft_ctx* cx = (pbft_ctx*)&g;
+  pbft_replica* r = nullptr;
+  CHECK(pbft_replica_create_multi(&cx, 1, n, 0, keys.data(), &r) == 0);
+  pbft_replica_set_digest_fn(r, host_digest, nullptr);
+  pbft_replica_set_log_window(r, 8192);
+  const char op[] = "singleOperation";
+  uint8_t d[64];
+  digest_padded(d, (const uint8_t*)op, strlen(op));
+  uint64_t seq0 = 0;
+  auto round = [&](uint32_t S, int how) {  // how: 0 push, 1 records, 2 key update half-way, 3 records per connection
+    const uint64_t batches0 = g.batches, early0 = g.early_batches, dropped0 = g.dropped;
+    uint8_t sg[64] = {3};
+    for (uint32_t q = 1; q <= S; ++q)
+      CHECK(pbft_replica_on_pre_prepare(r, 1, 1, seq0 + q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+    std::vector<uint8_t> rec(PBFT_RECORD_BYTES);
+    uint64_t forged = 0, k = 0;
+    for (uint32_t q = 1; q <= S; ++q)
+      for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})
+        for (uint32_t i = 0; i < n; ++i, ++k) {
+          const bool bad = k % 1009 == 7;  // scattered forgeries (never a quorum's worth)
+          forged += bad;
+          sg[0] = bad ? 0xEE : 3;
+          sg[1] = (uint8_t)i;
+          sg[2] = (uint8_t)q;
+          if (how == 2 && k == 70000) {
+            CHECK(g.early_batches == early0 + 1 && g.in_flight);  // the early batch is open...
+            const uint32_t idx = 5;
+            uint8_t A[32] = {5, 9};
+            uint8_t ok = 0;
+            CHECK(pbft_replica_update_keys(r, &idx, A, 1, &ok) == 0 && ok == 1);  // (the same key again)
+            CHECK(!g.in_flight && g.dropped == dropped0 + 1);                     // ...dropped first
+          }
+          if (how == 1 || how == 3) {
+            memcpy(rec.data(), sg, 64);
+            pbft_envelope(rec.data() + 64, kind, 1, seq0 + q, d);
+            rec[149] = 0;
+            const uint16_t ki = (uint16_t)i;
+            memcpy(rec.data() + 150, &ki, 2);
+            uint64_t used = 0, np = 0, nd = 0;
+            CHECK(pbft_replica_push_records(r, i, rec.data(), rec.size(), &used, &np, &nd) == 0 &&
+                  used == PBFT_RECORD_BYTES && np == 1 && nd == 0);
+            if (k % 5000 == 0) {  // the wrong connection, a PrePrepare record, half a record: dropped / kept
+              CHECK(pbft_replica_push_records(r, (i + 1) % n, rec.data(), rec.size(), &used, &np, &nd) == 0 &&
+                    np == 0 && nd == 1);
+              rec[68] = PBFT_KIND_PREPREPARE;
+              CHECK(pbft_replica_push_records(r, i, rec.data(), rec.size(), &used, &np, &nd) == 0 && np == 0 && nd == 1);
+              CHECK(pbft_replica_push_records(r, i, rec.data(), 100, &used, &np, &nd) == 0 && used == 0 && np == 0);
+            }
+          } else {
+            CHECK(pbft_replica_push(r, kind, 1, seq0 + q, d, i, sg) == 1);
+          }
+        }
+    pbft_replica_timings tm{};
+    std::vector<pbft_round_event> ev(4 * S + 16);
+    uint32_t ne = 0;
+    CHECK(pbft_replica_flush(r, 0, ev.data(), (uint32_t)ev.size(), &ne) == 0);
+    CHECK(pbft_replica_get_timings(r, &tm) == 0);
+    uint32_t committed = 0;
+    for (uint32_t e = 0; e < ne; ++e) committed += ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL;
+    CHECK(committed == S);
+    CHECK(g.batches == batches0 + 1 + (g.dropped - dropped0));  // (every opened batch: adopted or dropped)
+    seq0 += S;
+    printf("replica single pushes (%s, %u seqs): early batches %llu, dropped %llu, pieces %llu, last piece %llu rows\n",
+           how == 0 ? "push" : how == 2 ? "push, key update" : "records", S,
+           (unsigned long long)(g.early_batches - early0), (unsigned long long)(g.dropped - dropped0),
+           (unsigned long long)tm.early_pieces, (unsigned long long)tm.early_last_rows);
+    return g.early_batches - early0;
+  };
+  CHECK(round(seqs, 0) == 0);      // sizes the arena: no early batch yet
+  CHECK(round(seqs, 1) == 1);      // records, one message per call: early batch, adopted
+  CHECK(round(seqs, 0) == 1);
+  CHECK(round(seqs, 2) == 2);      // dropped by the key update, reopened
+  CHECK(round(2 * seqs, 3) >= 2);  // outgrows the sized arena: dropped at the growth, reopened
+  pbft_replica_destroy(r);
+}
+
+// ---- 8. failures across several contexts: a multi-context staging flush whose begin or rows call fails
+// on context k > 0 leaves no context in flight (the next flush works), and a key update that fails on one context is
+// revoked on all of them with the replica's PeerId map unchanged; clones sharing a key set are updated once --------
+static void test_replica_multi_failures() {
+  const uint32_t n = 64, seqs = 520;  // 66,560 votes: one slice per context
+  std::vector<uint8_t> keys(32 * (size_t)n);
+  for (uint32_t i = 0; i < n; ++i) { keys[32 * (size_t)i] = (uint8_t)i; keys[32 * (size_t)i + 1] = 11; }
+  std::vector<FakeGpu> gs(3);
+  std::vector<pbft_ctx*> cs(3);
+  for (int k = 0; k < 3; ++k) { gs[k].n_keys = n; cs[k] = (pbft_ctx*)&gs[k]; }
+  gs[0].set_id = gs[1].set_id = 1;  // a context and its clone
+  gs[2].set_id = 2;                 // a second GPU's context
+  pbft_replica* r = nullptr;
+  CHECK(pbft_replica_create_multi(cs.data(), 3, n, 0, keys.data(), &r) == 0);
+  pbft_replica_set_digest_fn(r, host_digest, nullptr);
+  const char op[] = "multiFail";
+  uint8_t d[64];
+  digest_padded(d, (const uint8_t*)op, strlen(op));
+  const char* prev = getenv("PBFT_REPLICA_DIRECT");
+  const std::string keep = prev ? prev : "";
+  setenv("PBFT_REPLICA_DIRECT", "0", 1);  // (the staging fill, one slice per context)
+  {
+    uint8_t sg[64] = {4};
+    for (uint32_t q = 1; q <= seqs; ++q)
+      CHECK(pbft_replica_on_pre_prepare(r, 1, 1, q, (const uint8_t*)op, (uint32_t)strlen(op), d, sg, nullptr) == 1);
+    for (uint32_t q = 1; q <= seqs; ++q)
+      for (uint8_t kind : {(uint8_t)PBFT_KIND_PREPARE, (uint8_t)PBFT_KIND_COMMIT})
+        for (uint32_t i = 0; i < n; ++i) {
+          sg[1] = (uint8_t)i;
+          CHECK(pbft_replica_push(r, kind, 1, q, d, i, sg) == 1);
+        }
+  }
+  for (int fail = 0; fail < 3; ++fail) {  // 0: begin fails on context 1, 1: rows fail on context 2, 2: none
+    if (fail == 0) gs[1].fail_begin = true;
+    if (fail == 1) gs[2].fail_rows_at = 0;
+    uint64_t rows = 0;
+    const int rc = pbft_replica_flush_submit(r, 0, &rows);
+    CHECK(fail < 2 ? rc == PBFT_EHIP : rc == 0);
+    if (fail < 2) {  // nothing left open or running; the candidates are pending again
+      for (const FakeGpu& g : gs) CHECK(!g.in_flight && !g.open);
+      CHECK(pbft_replica_in_flight(r) == 0);
+      continue;
+    }
+    std::vector<pbft_round_event> ev(4 * seqs);
+    uint32_t ne = 0;
+    CHECK(pbft_replica_flush(r, 0, ev.data(), (uint32_t)ev.size(), &ne) == 0);
+    uint32_t committed = 0;
+    for (uint32_t e = 0; e < ne; ++e) committed += ev[e].kind == PBFT_EVENT_COMMITTED_LOCAL;
+    CHECK(committed == seqs);
+  }
+  if (prev) setenv("PBFT_REPLICA_DIRECT", keep.c_str(), 1); else unsetenv("PBFT_REPLICA_DIRECT");
+  // key updates: the clone's shared set once; a failure on the second GPU revokes the slot everywhere
+  const uint32_t idx = 9;
+  uint8_t A2[32] = {200, 11}, ok = 7;
+  uint8_t pid_old[PBFT_PEER_ID_BYTES], pid_new[PBFT_PEER_ID_BYTES];
+  pbft_peer_id_from_key(&keys[32 * 9], pid_old);
+  pbft_peer_id_from_key(A2, pid_new);
+  gs[2].fail_update = true;
+  CHECK(pbft_replica_update_keys(r, &idx, A2, 1, &ok) == PBFT_EHIP && ok == 0);
+  for (const FakeGpu& g : gs) CHECK(g.revoked.size() == 1 && g.revoked[0] == 9);
+  CHECK(pbft_replica_peer_index(r, pid_old, sizeof pid_old) == 9 && pbft_replica_peer_index(r, pid_new, sizeof pid_new) < 0);
+  CHECK(pbft_replica_update_keys(r, &idx, A2, 1, &ok) == 0 && ok == 1);  // the retry installs it everywhere
+  CHECK(gs[0].updates == 2 && gs[1].updates == 0 && gs[2].updates == 1);  // (set 1 once per call; set 2 once)
+  CHECK(pbft_replica_peer_index(r, pid_new, sizeof pid_new) == 9 && pbft_replica_peer_index(r, pid_old, sizeof pid_old) < 0);
+  pbft_replica_destroy(r);
+  printf("replica multi-context failures: begin / rows failures drained, key update revoked on 3 contexts\n");
+}
+
 int main() {
   std::mt19937_64 rng(0x5EED);
   Keys k = make_keys(4, rng);
@@ -838,7 +1038,9 @@ int main() {
   if (!(getenv("PBFT_REPLICA_DIRECT") && atoi(getenv("PBFT_REPLICA_DIRECT")) == 0)) {
     test_replica_early_dropped(0);
     test_replica_early_dropped(1);
+    test_replica_single_early();
   }
+  test_replica_multi_failures();
   printf("sanitized host run ok\n");
   return 0;
 }

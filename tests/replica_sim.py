@@ -27,6 +27,12 @@ class Stats(ctypes.Structure):
                                                 "live_windows", "submit_ns", "apply_ns")]
 
 
+class Timings(ctypes.Structure):  # include/pbft_replica.h pbft_replica_timings
+    _fields_ = [(n, ctypes.c_uint64) for n in ("push_checks_ns", "push_windows_ns", "push_rows_ns", "submit_segs_ns",
+                                                "submit_launch_ns", "wait_ns", "apply_partial_ns", "apply_final_ns",
+                                                "gc_ns", "polls", "early_pieces", "early_piece_ns", "early_last_rows")]
+
+
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p)
 DIGEST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p)
@@ -50,6 +56,8 @@ def lib():
     L.pbft_replica_on_pre_prepare.argtypes = [vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_char_p,
                                               ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
     L.pbft_replica_push_frames.argtypes = [vp, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t, vp, vp, vp]
+    L.pbft_replica_push_records.argtypes = [vp, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t, vp, vp, vp]
+    L.pbft_replica_get_timings.argtypes = [vp, ctypes.POINTER(Timings)]
     L.pbft_replica_set_log_window.argtypes = [vp, ctypes.c_uint64]
     L.pbft_replica_stable_checkpoint.argtypes = [vp, ctypes.c_uint64]
     L.pbft_replica_peer_index.argtypes = [vp, ctypes.c_char_p, ctypes.c_size_t]

@@ -193,3 +193,175 @@ def test_gpu_replica_2p20_round(gpu_cluster, n_ctx, direct, monkeypatch):
         c.close()
     print(f"replica 2^20 ({n_ctx} contexts): submit {(t1 - t0) * 1e3:.1f} ms, submit->done {(t2 - t0) * 1e3:.1f} ms, "
           f"{polls} polls")
+
+
+def _signed_round(v, seeds, n, seq0, seqs, primary=1):
+    """(PrePrepare R||S per seq, vote sigs [N][64], kind, seq, signer, digests [N][64], ops) of a round of n replicas
+    over seqs seq0 .. seq0 + seqs - 1, votes in (seq, kind, signer) order, signed on the GPU."""
+    import hashlib
+    from replica_sim import KIND_COMMIT, KIND_PREPARE
+    qs = np.arange(seq0, seq0 + seqs, dtype=np.uint64)
+    ops = [b"op-" + str(int(q)).encode() for q in qs]
+    dig = np.stack([np.frombuffer(hashlib.blake2b(o, digest_size=64).digest(), np.uint8) for o in ops])
+    env = lambda k, q, d: np.frombuffer(b"PBFT" + bytes([k]) + (1).to_bytes(8, "little") +  # noqa: E731
+                                        int(q).to_bytes(8, "little") + d.tobytes(), np.uint8)
+    N = seqs * 2 * n
+    seq = np.repeat(qs, 2 * n)
+    kind = np.tile(np.repeat(np.array([KIND_PREPARE, KIND_COMMIT], np.uint8), n), seqs)
+    signer = np.tile(np.arange(n, dtype=np.uint32), 2 * seqs)
+    base = np.stack([np.stack([env(k, q, dig[j]) for k in (0, 1, 2)]) for j, q in enumerate(qs)])
+    msg = base[(seq - seq0).astype(np.int64), kind.astype(np.int64)]
+    R, S, _ = v.sign(seeds, signer.astype(np.uint16), msg, 85)
+    pR, pS, _ = v.sign(seeds, np.full(seqs, primary, np.uint16), base[:, 0], 85)
+    digs = np.ascontiguousarray(dig[(seq - seq0).astype(np.int64)])
+    return np.concatenate([pR, pS], 1), np.concatenate([R, S], 1), kind, seq, signer, digs, dig, ops, msg
+
+
+def test_gpu_replica_single_pushes_early_batch(gpu_cluster):
+    """r06: rounds delivered the reference's way -- one message per call: each seq's PrePrepare
+    (pbft_replica_on_pre_prepare, its digest by the GPU Blake2b on the replica's own clone of the context) and then its
+    votes one pbft_replica_push / one 160-byte record (pbft_replica_push_records) at a time.  From the second round on
+    the arena is verified in pieces on the GPU while the votes arrive (the single-message early batch); a PrePrepare's
+    digest runs while that batch is open.  Every seq commits but the one whose Prepare quorum was forged away, the
+    forged votes are the rejected ones, and the events come in seq order."""
+    import ctypes
+    import hashlib
+    from replica_sim import EV_PREPARED, Event, Stats, Timings, lib
+    from pbft_amd import wire
+    v = gpu_cluster
+    L = lib()
+    n, seqs = 64, 600                       # 76,800 votes + 600 PrePrepares per round: 2^16-row pieces
+    seeds = np.stack([np.frombuffer(hashlib.sha512(b"pbft-key" + (31).to_bytes(8, "little") +
+                                                   i.to_bytes(8, "little")).digest()[:32], np.uint8) for i in range(n)])
+    _, _, pub = v.sign(seeds, np.arange(n, dtype=np.uint16), np.zeros((n, 85), np.uint8), 85)
+    assert v.set_keys(pub).all()
+    rep = ctypes.c_void_p()
+    assert L.pbft_replica_create(v._ctx, n, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+    ev = (Event * 4096)()
+    ne = ctypes.c_uint32()
+    st0 = Stats()
+    try:
+        for rnd, how in enumerate(["push", "push", "records"]):
+            seq0 = 1 + rnd * seqs
+            pps, sigs, kind, seq, signer, digs, dig, ops, msg = _signed_round(v, seeds, n, seq0, seqs)
+            bad = ((seq == seq0 + 7) & (kind == 1) & (signer >= 2) & (signer < 50)) | (np.arange(len(seq)) % 991 == 3)
+            sigs[bad, 40] ^= 1
+            recs = wire.records_pack(sigs[:, :32], sigs[:, 32:], signer.astype(np.uint16), msg) if how == "records" \
+                else None
+            used, a, b = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+            for j in range(seqs):
+                q = seq0 + j
+                assert L.pbft_replica_on_pre_prepare(rep, 1, 1, q, ops[j], len(ops[j]), dig[j].tobytes(),
+                                                     pps[j].tobytes(), None) == 1
+                for i in range(2 * n * j, 2 * n * (j + 1)):
+                    if recs is None:
+                        assert L.pbft_replica_push(rep, int(kind[i]), 1, int(seq[i]), digs[i].tobytes(),
+                                                   int(signer[i]), sigs[i].tobytes()) == 1
+                    else:
+                        assert L.pbft_replica_push_records(rep, int(signer[i]), recs[i].ctypes.data, 160,
+                                                           ctypes.byref(used), ctypes.byref(a), ctypes.byref(b)) == 0
+                        assert used.value == 160 and a.value == 1
+            rows = ctypes.c_uint64()
+            assert L.pbft_replica_flush_submit(rep, 0, ctypes.byref(rows)) == 0 and rows.value == len(seq) + seqs
+            evs = []
+            while True:
+                rc = L.pbft_replica_flush_poll(rep, ev, len(ev), ctypes.byref(ne))
+                assert rc >= 0
+                evs += [(e.seq, e.kind) for e in ev[: ne.value]]
+                if rc == 1:
+                    break
+            tm = Timings()
+            assert L.pbft_replica_get_timings(rep, ctypes.byref(tm)) == 0
+            if rnd:
+                assert tm.early_pieces >= 1 and tm.early_last_rows < (1 << 16) + 64, (rnd, tm.early_pieces)
+            else:
+                assert tm.early_pieces == 0  # (the first round sizes the arena)
+            allq = set(range(seq0, seq0 + seqs))
+            assert [x for x, _ in evs] == sorted(x for x, _ in evs)
+            assert {x for x, k in evs if k == EV_PREPARED} == allq - {seq0 + 7}
+            assert {x for x, k in evs if k == EV_COMMITTED} == allq - {seq0 + 7}
+            st = Stats()
+            L.pbft_replica_get_stats(rep, ctypes.byref(st))
+            assert st.rejected_sig - st0.rejected_sig == int(bad.sum())
+            assert st.accepted - st0.accepted == len(seq) + seqs - int(bad.sum())
+            st0 = st
+    finally:
+        L.pbft_replica_destroy(rep)
+
+
+def test_gpu_replica_update_keys_all_or_nothing(gpu_cluster):
+    """VERDICT r05 item 4 / ADVICE r05: a replica over two independently created contexts (two key sets, as two GPUs
+    of a node); pbft_replica_update_keys fails on the second (PBFT_OPT_FAULT_INJECT 2: after its tables were written).
+    Afterwards EVERY context rejects the slot's signatures under the old and the new key (revoked everywhere), the
+    PeerId map keeps the old identity, and the other slots verify; a retry installs the new key on both contexts and
+    maps its PeerId; a flush over both contexts then accepts the slot's new-key votes in both slices."""
+    import ctypes
+    import hashlib
+    from pbft_amd import GpuBatchVerifier, SigBatch, bitmap_to_bool
+    from replica_sim import Event, Stats, lib
+    L = lib()
+    n, slot = 16, 5
+    seeds = np.stack([np.frombuffer(hashlib.sha512(b"pbft-key" + (41).to_bytes(8, "little") +
+                                                   i.to_bytes(8, "little")).digest()[:32], np.uint8) for i in range(n)])
+    v0 = gpu_cluster
+    v1 = GpuBatchVerifier(0)
+    rep = ctypes.c_void_p()
+    try:
+        _, _, pub = v0.sign(seeds, np.arange(n, dtype=np.uint16), np.zeros((n, 85), np.uint8), 85)
+        assert v0.set_keys(pub).all() and v1.set_keys(pub).all()
+        ctxs = (ctypes.c_void_p * 2)(v0._ctx.value, v1._ctx.value)
+        assert L.pbft_replica_create_multi(ctxs, 2, n, 0, pub.tobytes(), ctypes.byref(rep)) == 0
+        seeds_new = seeds.copy()
+        seeds_new[slot] = np.frombuffer(hashlib.sha512(b"new-key").digest()[:32], np.uint8)
+        msg = np.tile(np.frombuffer(b"PBFT\x01" + bytes(80), np.uint8), (4 * n, 1))
+        K = np.tile(np.arange(n, dtype=np.uint16), 4)
+        Ro, So, _ = v0.sign(seeds, K, msg, 85)
+        Rn, Sn, pub_new = v0.sign(seeds_new, K, msg, 85)
+        hit = K == slot
+
+        def bits(v, R, S):
+            return bitmap_to_bool(v.verify(SigBatch(R, S, K, msg, 85)), len(K))
+        v1.set_option(v1.OPT_FAULT_INJECT, 2)
+        ok = np.zeros(1, np.uint8)
+        idx = np.array([slot], np.uint32)
+        assert L.pbft_replica_update_keys(rep, idx.ctypes.data, pub_new[slot].tobytes(), 1, ok.ctypes.data) < 0
+        assert ok[0] == 0
+        for v in (v0, v1):  # revoked on both: neither key verifies for the slot, every other slot does
+            for R, S in ((Ro, So), (Rn, Sn)):
+                b = bits(v, R, S)
+                assert not b[hit].any() and b[~hit].all()
+        pid = ctypes.create_string_buffer(38)
+        L.pbft_peer_id_from_key(pub[slot].tobytes(), pid)
+        assert L.pbft_replica_peer_index(rep, pid.raw, 38) == slot          # the old identity kept
+        L.pbft_peer_id_from_key(pub_new[slot].tobytes(), pid)
+        assert L.pbft_replica_peer_index(rep, pid.raw, 38) < 0
+        assert L.pbft_replica_update_keys(rep, idx.ctypes.data, pub_new[slot].tobytes(), 1, ok.ctypes.data) == 0
+        assert ok[0] == 1
+        assert L.pbft_replica_peer_index(rep, pid.raw, 38) == slot
+        for v in (v0, v1):
+            assert bits(v, Rn, Sn).all()
+            b = bits(v, Ro, So)
+            assert not b[hit].any() and b[~hit].all()
+        # a round over both contexts: 2 x 2^16 votes, the slot voting with its new key in both slices
+        pub2 = pub.copy()
+        pub2[slot] = pub_new[slot]
+        seqs = 2100
+        pps, sigs, kind, seq, signer, digs, dig, ops, _ = _signed_round(v0, seeds_new, n, 1, seqs)
+        for j in range(seqs):
+            assert L.pbft_replica_on_pre_prepare(rep, 1, 1, 1 + j, ops[j], len(ops[j]), dig[j].tobytes(),
+                                                 pps[j].tobytes(), None) == 1
+        view = np.ones(len(seq), np.uint64)
+        qd = ctypes.c_uint64()
+        assert L.pbft_replica_push_many(rep, len(seq), kind.ctypes.data, view.ctypes.data, seq.ctypes.data,
+                                        digs.ctypes.data, signer.ctypes.data, sigs.ctypes.data, ctypes.byref(qd)) == 0
+        ev = (Event * 8192)()
+        ne = ctypes.c_uint32()
+        assert L.pbft_replica_flush(rep, 0, ev, 8192, ctypes.byref(ne)) == 0
+        assert sum(1 for e in ev[: ne.value] if e.kind == EV_COMMITTED) == seqs
+        st = Stats()
+        L.pbft_replica_get_stats(rep, ctypes.byref(st))
+        assert st.rejected_sig == 0 and st.accepted == len(seq) + seqs
+    finally:
+        if rep:
+            L.pbft_replica_destroy(rep)
+        v1.close()

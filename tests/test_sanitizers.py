@@ -57,3 +57,8 @@ def test_host_code_clean_under_asan_ubsan(direct):
         many = "push_many" in l
         early = n_ctx if direct == "1" and many else 0
         assert l.endswith(f"{n_ctx if direct == '1' else 0} direct batches, {early} early"), l
+    # r06: one vote per call (push / binary records): early batches opened while the votes arrive, adopted by the
+    # flush, dropped by a key update or an outgrown arena; multi-context begin / rows / key-update failures
+    single = [l for l in p.stdout.splitlines() if l.startswith("replica single pushes")]
+    assert len(single) == (5 if direct == "1" else 0), p.stdout[-2000:]
+    assert "replica multi-context failures" in p.stdout

@@ -1,0 +1,90 @@
+// BENCH INFRASTRUCTURE (not the product): the reference-shaped caller of the replica's ingress, for bench.py's
+// replica_ingress_2^20 leg.  The reference receives every message on ONE thread -- the libp2p
+// swarm's poll loop hands each decoded message to Pbft::inject_node_event (src/behavior.rs:304, arms :340-412) one at
+// a time -- so these loops run on the calling thread only and time themselves around the calls into the product:
+//   ingress_push     one pbft_replica_push per vote, in the given order (inject_node_event's Prepare / Commit arms);
+//   ingress_streams  per-connection byte streams (PbftHandler -> message_to_handler_event, src/handler.rs:533-548):
+//                    the loop visits the connections round-robin and hands each visit's next `per_visit` messages
+//                    (UviBytes/JSON frames -> pbft_replica_push_frames, or 160-byte binary records ->
+//                    pbft_replica_push_records) to the replica, the connection being the authenticated peer.
+// Built by __graft_entry__.build() next to the library it links (tools/ingress/libingress.so).
+#include <time.h>
+
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#include "../../include/pbft_replica.h"
+#include "../../include/pbft_wire.h"
+
+static double now_s() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+// bytes of the next k whole UviBytes frames of buf[0, len) (fewer if the buffer ends first)
+static size_t frames_bytes(const uint8_t* buf, size_t len, uint32_t k) {
+  size_t off = 0;
+  for (uint32_t i = 0; i < k && off < len; ++i) {
+    uint64_t fl;
+    size_t hn;
+    if (pbft_uvi_decode(buf + off, len - off, &fl, &hn) != 0 || len - off - hn < fl) break;
+    off += hn + (size_t)fl;
+  }
+  return off;
+}
+
+extern "C" {
+
+int ingress_push(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
+                 const uint8_t* digests, const uint32_t* signer, const uint8_t* sigs, uint64_t* queued,
+                 double* seconds) {
+  uint64_t q = 0;
+  int rc = 0;
+  const double t0 = now_s();
+  for (uint64_t i = 0; i < N; ++i) {
+    const int p = pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
+    if (p < 0) { rc = p; break; }
+    q += (uint64_t)p;
+  }
+  *seconds = now_s() - t0;
+  *queued = q;
+  return rc;
+}
+
+int ingress_streams(pbft_replica* r, int binary, uint32_t n_conn, const uint8_t* const* streams,
+                    const uint64_t* lens, uint32_t per_visit, uint64_t* pushed, uint64_t* dropped, uint64_t* calls,
+                    double* seconds) {
+  std::vector<uint64_t> off(n_conn, 0);
+  uint64_t np = 0, nd = 0, nc = 0;
+  int rc = 0;
+  const double t0 = now_s();
+  for (bool more = true; more && rc == 0;) {
+    more = false;
+    for (uint32_t c = 0; c < n_conn && rc == 0; ++c) {
+      const uint64_t left = lens[c] - off[c];
+      if (!left) continue;
+      const uint8_t* p = streams[c] + off[c];
+      const size_t n = binary ? (size_t)(left < (uint64_t)PBFT_RECORD_BYTES * per_visit ? left
+                                                                                     : (uint64_t)PBFT_RECORD_BYTES * per_visit)
+                              : frames_bytes(p, left, per_visit);
+      uint64_t used = 0, a = 0, b = 0;
+      rc = binary ? pbft_replica_push_records(r, c, p, n, &used, &a, &b)
+                  : pbft_replica_push_frames(r, c, p, n, &used, &a, &b);
+      ++nc;
+      if (rc == 0 && used == 0) rc = PBFT_EINVAL;  // (a stream that makes no progress: malformed)
+      off[c] += used;
+      np += a;
+      nd += b;
+      more = more || off[c] < lens[c];
+    }
+  }
+  *seconds = now_s() - t0;
+  *pushed = np;
+  *dropped = nd;
+  *calls = nc;
+  return rc;
+}
+
+}  // extern "C"
