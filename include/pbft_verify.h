@@ -321,11 +321,6 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
  *   PBFT_OPT_KERNEL_TIMING        1: two HIP events bracket every launch for pbft_last_kernel_ms; 0 (default since
  *                                 r05: the two event records cost ~7.5 us per launch, 4.5 % of an 8-GPU shard): none,
  *                                 and pbft_last_kernel_ms returns -1
- *                                 (pbft_last_kernel_ms returns -1; ~3 us less per launch for latency-bound callers)
- *   PBFT_OPT_VOTES_ZERO_COPY      1: votes rows that sit in the context's pinned staging (pbft_verify_votes_stage
- *                                 / _submit_begin, the replica's flush, pageable inputs copied there) are read by
- *                                 the kernels in place over PCIe; 0 (default; env PBFT_VOTES_ZERO_COPY): copied
- *                                 to HBM chunk by chunk first (faster on MI355X: DESIGN.md section 5)
  *   PBFT_OPT_COMB_PAIR            1: one-lane batches run the comb with two waves per 64 signatures (a hashing
  *                                 wave and a base-point wave, joined by one extended addition); 0: one wave per
  *                                 64 signatures; any other value = by batch size (pairs up to 98,304 signatures,
@@ -338,28 +333,16 @@ int pbft_sign_batch(pbft_ctx *ctx, const uint8_t *seeds, uint32_t n_seeds, const
 #define PBFT_OPT_LAT_SPLIT 5
 #define PBFT_OPT_KERNEL_TIMING 7
 #define PBFT_OPT_FINISH_WAVES 8
-#define PBFT_OPT_VOTES_ZERO_COPY 9
+/* (9, 12, 14, 15: options of variants measured slower and removed in r06 -- now PBFT_EINVAL) */
 #define PBFT_OPT_COMB_PAIR 10
 /* Testing: the next pbft_verify_update_keys on this context fails at a chosen point -- 1: before anything is written
  * (as if its scratch allocation failed: the key set is unchanged), 2: after the updated keys' tables were written
  * (their key_ok is cleared in the shared key set, so every context holding it rejects them); 0: off. */
 #define PBFT_OPT_FAULT_INJECT 11
-/* 1 (default; env PBFT_COMB_SPREAD): a one-lane comb launch of fewer than 4 blocks per CU (e.g. the 131k shard of
- * an 8-GPU round) asks for enough LDS that no CU takes more than its even share of the blocks; 0: the kernels'
- * own LDS (the dispatcher then packs up to 4 blocks on some CUs). */
-#define PBFT_OPT_COMB_SPREAD 12
 /* 1: the one-lane comb (chain form, 85-byte messages, >= 2^16 signatures) runs 8-wave blocks whose two waves per
  * SIMD trade priorities so that they progress together (instead of oldest-first); 0: 4-wave blocks; any other
  * value (default; env PBFT_COMB_PRIO) = by batch size: 8-wave blocks where they fit one per CU (the 131k shard). */
 #define PBFT_OPT_COMB_PRIO 13
-/* 1: the chain-form comb (85-byte messages, >= 2^16 signatures, not pipelined) runs the finish in the same launch:
- * the last block of each group of comb blocks to finish verifies the group's signatures; 0 (default; env
- * PBFT_COMB_FUSE): a separate finish launch. */
-#define PBFT_OPT_COMB_FUSE 14
-/* 1: 8-wave comb launches (PBFT_OPT_COMB_PRIO) stagger the two waves of a SIMD -- one hashes before its base-point
- * positions, the other after them -- so one's latency-bound SHA-512 runs under the other's multiplications;
- * 0 (default; env PBFT_COMB_STAGGER): both hash first. */
-#define PBFT_OPT_COMB_STAGGER 15
 int pbft_verify_set_option(pbft_ctx *ctx, int option, uint64_t value);
 
 /* Diagnostics */

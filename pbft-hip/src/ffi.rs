@@ -51,13 +51,9 @@ pub const PBFT_OPT_FINISH_TREE: c_int = 4;
 pub const PBFT_OPT_LAT_SPLIT: c_int = 5;
 pub const PBFT_OPT_KERNEL_TIMING: c_int = 7;
 pub const PBFT_OPT_FINISH_WAVES: c_int = 8;
-pub const PBFT_OPT_VOTES_ZERO_COPY: c_int = 9;
 pub const PBFT_OPT_COMB_PAIR: c_int = 10;
 pub const PBFT_OPT_FAULT_INJECT: c_int = 11;
-pub const PBFT_OPT_COMB_SPREAD: c_int = 12;
 pub const PBFT_OPT_COMB_PRIO: c_int = 13;
-pub const PBFT_OPT_COMB_FUSE: c_int = 14;
-pub const PBFT_OPT_COMB_STAGGER: c_int = 15;
 pub const PBFT_MAX_REPLICA_CTX: u32 = 16;
 
 pub const PBFT_KIND_PREPREPARE: u8 = 0;
@@ -97,6 +93,25 @@ pub struct pbft_replica_stats {
     pub live_windows: u64,
     pub submit_ns: u64,
     pub apply_ns: u64,
+}
+
+/// Phases of the last push_many / flush (pbft_replica_get_timings; host clock, ns).
+#[repr(C)]
+#[derive(Debug, Default, Clone, Copy)]
+pub struct pbft_replica_timings {
+    pub push_checks_ns: u64,
+    pub push_windows_ns: u64,
+    pub push_rows_ns: u64,
+    pub submit_segs_ns: u64,
+    pub submit_launch_ns: u64,
+    pub wait_ns: u64,
+    pub apply_partial_ns: u64,
+    pub apply_final_ns: u64,
+    pub gc_ns: u64,
+    pub polls: u64,
+    pub early_pieces: u64,
+    pub early_piece_ns: u64,
+    pub early_last_rows: u64,
 }
 
 /// Phases of the last pbft_verify_set_keys / pbft_verify_update_keys (host wall time, ms).
@@ -163,6 +178,8 @@ extern "C" {
     pub fn pbft_verify_update_keys(ctx: *mut pbft_ctx, idx: *const u32, a: *const u8, m: u32,
                                    key_ok: *mut u8) -> c_int;
     pub fn pbft_verify_key_stats(ctx: *mut pbft_ctx, out: *mut pbft_key_stats) -> c_int;
+    pub fn pbft_verify_revoke_keys(ctx: *mut pbft_ctx, idx: *const u32, m: u32) -> c_int;
+    pub fn pbft_verify_key_set_id(ctx: *mut pbft_ctx, id: *mut u64) -> c_int;
     pub fn pbft_verify_ctx_clone(parent: *mut pbft_ctx, out: *mut *mut pbft_ctx) -> c_int;
     pub fn pbft_verify_batch(ctx: *mut pbft_ctx, r: *const u8, s: *const u8, key_idx: *const u16, msg: *const u8,
                              msg_len: u32, msg_stride: u32, n: u64, bitmap_out: *mut u64) -> c_int;
@@ -245,6 +262,8 @@ extern "C" {
                              sig: *const u8) -> c_int;
     pub fn pbft_replica_push_frames(r: *mut pbft_replica, peer_idx: u32, stream: *const u8, len: usize,
                                     consumed: *mut u64, pushed: *mut u64, dropped: *mut u64) -> c_int;
+    pub fn pbft_replica_push_records(r: *mut pbft_replica, peer_idx: u32, stream: *const u8, len: usize,
+                                     consumed: *mut u64, pushed: *mut u64, dropped: *mut u64) -> c_int;
     pub fn pbft_replica_push_many(r: *mut pbft_replica, n: u64, kind: *const u8, view: *const u64, seq: *const u64,
                                   digests: *const u8, signer: *const u32, sigs: *const u8,
                                   queued: *mut u64) -> c_int;
@@ -258,6 +277,7 @@ extern "C" {
     pub fn pbft_replica_prepared(r: *mut pbft_replica, view: u64, seq: u64) -> c_int;
     pub fn pbft_replica_committed_local(r: *mut pbft_replica, view: u64, seq: u64) -> c_int;
     pub fn pbft_replica_get_stats(r: *mut pbft_replica, out: *mut pbft_replica_stats) -> c_int;
+    pub fn pbft_replica_get_timings(r: *mut pbft_replica, out: *mut pbft_replica_timings) -> c_int;
     pub fn pbft_key_from_peer_id(peer_id: *const u8, len: usize, a: *mut u8) -> c_int;
     pub fn pbft_peer_id_from_key(a: *const u8, peer_id: *mut u8);
     pub fn pbft_key_from_peer_id_b58(text: *const c_char, len: usize, a: *mut u8) -> c_int;
@@ -274,6 +294,9 @@ extern "C" {
                                   status: *mut u8, r: *mut u8, s: *mut u8, key_idx: *mut u16, msg: *mut u8,
                                   kind: *mut u8, view: *mut u64, seq: *mut u64, n_frames: *mut u64,
                                   n_rows: *mut u64, consumed: *mut u64) -> c_int;
+    pub fn pbft_wire_encode_votes(n: u64, kind: *const u8, view: *const u64, seq: *const u64, digests: *const u8,
+                                  replica: *const u32, sigs: *const u8, out: *mut u8, cap: usize,
+                                  len: *mut usize) -> c_int;
     pub fn pbft_records_pack(r: *const u8, s: *const u8, key_idx: *const u16, msg: *const u8, msg_stride: u32,
                              n: u64, records: *mut u8) -> c_int;
     pub fn pbft_verify_records_device(ctx: *mut pbft_ctx, d_records: *const u8, n: u64, d_bitmap: *mut u64,

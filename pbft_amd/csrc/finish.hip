@@ -50,7 +50,7 @@ __global__ void __launch_bounds__(BLOCK, W) finish_kernel(const uint8_t* __restr
   const uint64_t* ds_tab = nullptr;
 #endif
   if (wave * FM * 64 >= N) return;
-  finish_wave<FM, LV, PRE, true, false>(wave, lane, R, rs_stride, xyz, flags, N, bitmap, ds_tab);
+  finish_wave<FM, LV, PRE, true>(wave, lane, R, rs_stride, xyz, flags, N, bitmap, ds_tab);
 }
 
 

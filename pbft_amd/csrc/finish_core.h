@@ -1,6 +1,5 @@
-// Batch-inversion finish of the one-lane-per-signature verify, as a per-wave device function: run by
-// finish_kernel (finish.hip, after comb_kernel) and by the last-arriving block of each group in the fused comb
-// (comb_kernel<..., FUSE>, verify_kernels.h).
+// Batch-inversion finish of the one-lane-per-signature verify, as a per-wave device function run by finish_kernel
+// (finish.hip, after comb_kernel).
 #pragma once
 #include "verify_core.h"
 
@@ -80,9 +79,8 @@ __device__ __forceinline__ uint32_t tree_partner(uint32_t v) {
 // One wave of the finish: signatures i = (wave * FM + m) * 64 + lane, m < FM; writes their bitmap words.
 // PRE: X, Y, Z loaded up front (register budget permitting).  SYNC: meet the block's barrier (the divstep table's
 // copy to LDS) right before the inversion -- every wave of the block, past N included, must then reach one
-// __syncthreads() (finish_kernel); without SYNC the table is in LDS already.  FUSED: comb_kernel<..., FUSE>'s
-// workspace (flag in bit 31 of X limb 0, no flags array).
-template <int FM, int LV, bool PRE, bool SYNC, bool FUSED>
+// __syncthreads() (finish_kernel); without SYNC the table is in LDS already.
+template <int FM, int LV, bool PRE, bool SYNC>
 __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8_t* __restrict__ R, uint32_t rs_stride,
                                             const uint32_t* __restrict__ xyz, const uint8_t* __restrict__ flags,
                                             uint64_t N, uint64_t* __restrict__ bitmap, const uint64_t* ds_tab) {
@@ -183,13 +181,7 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
       load_fe(X, Xb, N, ii);
       load_fe(Y, Yb, N, ii);
     }
-    bool fl;
-    if constexpr (FUSED) {  // comb_kernel<..., FUSE>: the flag rides in bit 31 of X limb 0 (no flags array)
-      fl = X.v[0] >> 31;
-      X.v[0] &= 0x7FFFFFFFu;
-    } else {
-      fl = flags[ii];
-    }
+    const bool fl = flags[ii];
     fe_mul(x, X, zi);
     fe_mul(y, Y, zi);
     uint32_t xw[8], yw[8], r[8], ry[8];

@@ -128,15 +128,6 @@ static void keyset_release(keyset* k) {
   }
 }
 
-// 1: votes rows in the context's pinned staging (the replica's flush, pbft_verify_votes_stage, pageable votes
-// inputs) are read by the comb kernel straight from host memory over PCIe instead of being copied to HBM first
-// (env PBFT_VOTES_ZERO_COPY, option PBFT_OPT_VOTES_ZERO_COPY).  Measured slower, so off by default: a 2^20 staged
-// round 2.69 ms against 1.97 ms with chunked copies (profiles/r04/zc_probe.json) -- every wave generation waits
-// for its rows at its start, so PCIe and the arithmetic take turns instead of overlapping.
-#ifndef PBFT_VOTES_ZERO_COPY
-#define PBFT_VOTES_ZERO_COPY 0
-#endif
-
 // device staging buffers of the votes chunks (chunk c uses buffer c % VOTES_BUFS; its copy waits for the kernels
 // of chunk c - VOTES_BUFS)
 static constexpr int VOTES_BUFS = 4;
@@ -161,12 +152,8 @@ struct pbft_ctx {
   int fin_waves = 0;                   // product-tree finish compiled for 1 or 2 waves per SIMD (0 = by batch size)
   int lat_split = 0;                   // latency-mode lanes per signature (4 / 8; 0 = by batch size)
   int comb_pair = -1;                  // comb_pair_kernel: 1 on, 0 off, -1 by batch size (PBFT_OPT_COMB_PAIR)
-  int comb_spread = 1;                 // even block placement of one-generation comb launches (PBFT_OPT_COMB_SPREAD)
   int comb_prio = -1;                  // 8-wave comb blocks with paired wave priorities: 1, 0, -1 by batch size
                                        // (PBFT_OPT_COMB_PRIO)
-  int comb_stagger = 0;                // 8-wave comb launches stagger their waves' hashes (PBFT_OPT_COMB_STAGGER)
-  int comb_fuse = 0;                   // the finish inside the chain-form comb launch: 1, 0, -1 by size
-                                       // (PBFT_OPT_COMB_FUSE)
   int cus = 0;                         // compute units of the device
   // ev0 / ev1 around every launch (pbft_last_kernel_ms).  Off by default since r05: the two event records cost 7.5 us
   // per comb + finish pair, 4.5 % of the 131k shard (profiles/r05/shard/timing_events.txt)
@@ -221,9 +208,8 @@ struct pbft_ctx {
   // pinned host staging of the non-blocking host-buffer forms (pageable caller buffers are copied here,
   // then DMA'd asynchronously; pbft_verify_votes_stage hands it out for in-place filling)
   uint8_t* h_stage = nullptr;
-  uint8_t* h_stage_dev = nullptr;  // the same memory as the kernels address it (zero-copy votes)
+  uint8_t* h_stage_dev = nullptr;  // the same memory as the kernels address it (the import kernels)
   size_t h_stage_cap = 0;
-  bool zero_copy = PBFT_VOTES_ZERO_COPY;  // votes rows in the staging: kernels read them in place (no H2D)
   uint64_t staged_n = 0;   // pbft_verify_votes_stage: the batch the staging is laid out for
   uint32_t staged_env = 0;
   bool staged = false;
@@ -470,21 +456,17 @@ static bool launch_trace() { return launch_trace_ms() >= 0; }
 
 // second xyz/flags half (pipelined form) after the entry-index region
 static inline size_t half1_offset(uint64_t N) { return eidx_offset(N) + eidx_bytes(N); }
-// R copy [W][32] of a launch whose R is read from host memory (launch_verify r_host), after both halves
-static inline size_t rcopy_offset(uint64_t W, bool two) {
+// the whole workspace: half 0, the entry indices and (pipelined form) half 1
+static inline size_t work_bytes(uint64_t W, bool two) {
   return ((two ? half1_offset(W) + eidx_offset(W) : half1_offset(W)) + 255) & ~(size_t)255;
 }
-// the fused comb's per-group arrival counters (comb_kernel<..., FG>: zero between launches -- zeroed here when the
-// workspace is allocated, and by the last arriver of each group in every launch), after the R copy
-static inline size_t ctr_offset(uint64_t W, bool two) { return (rcopy_offset(W, two) + 32 * (size_t)W + 255) & ~(size_t)255; }
-static inline size_t ctr_bytes(uint64_t W) { return 4 * ((W + BLOCK - 1) / BLOCK + 64); }
 // The layout is a function of c->work_n only, never of the batch at hand: a smaller batch must not move
 // the entry-index region onto the xyz/flags half a pipelined finish may still be reading.
 static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   if (N <= c->work_n && (!two_halves || c->work_two)) return PBFT_OK;
   const uint64_t W = N > c->work_n ? N : c->work_n;
   const bool two = two_halves || c->work_two;
-  const size_t need = ctr_offset(W, two) + ctr_bytes(W);
+  const size_t need = work_bytes(W, two);
   // nothing may still read the old workspace: the finishes of earlier pipelined launches, then this stream
   for (int h = 0; h < 2; ++h)
     if (c->fin_pending[h]) { HIP_TRY(hipEventSynchronize(c->ev_fin[h])); c->fin_pending[h] = false; }
@@ -496,7 +478,6 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
   c->work_n = 0;
   c->work_two = false;
   if (hipMalloc(&c->d_work, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
-  HIP_TRY(hipMemset(c->d_work + ctr_offset(W, two), 0, ctr_bytes(W)));
   c->work_cap = need;
   c->work_n = W;
   c->work_two = two;
@@ -507,7 +488,7 @@ static int ensure_work(pbft_ctx* c, uint64_t N, bool two_halves = false) {
 static int ensure_work2(pbft_ctx* c, uint64_t N) {
   if (N <= c->work2_n) return PBFT_OK;
   const uint64_t W = N;
-  const size_t need = ctr_offset(W, false) + ctr_bytes(W);
+  const size_t need = work_bytes(W, false);
   if (c->d_work2) {
     HIP_TRY(hipStreamSynchronize(c->stream2));
     HIP_TRY(hipFree(c->d_work2));
@@ -516,7 +497,6 @@ static int ensure_work2(pbft_ctx* c, uint64_t N) {
   c->work2_cap = 0;
   c->work2_n = 0;
   if (hipMalloc(&c->d_work2, need) != hipSuccess) return set_err(PBFT_ENOMEM, "verify workspace alloc");
-  HIP_TRY(hipMemset(c->d_work2 + ctr_offset(W, false), 0, ctr_bytes(W)));
   c->work2_cap = need;
   c->work2_n = W;
   return PBFT_OK;
@@ -529,14 +509,13 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
                          uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t* dB, hipStream_t st,
                          uint32_t rs_stride = 32, uint32_t k_stride = 2, hipStream_t fst = nullptr,
                          const uint32_t* dMI = nullptr, uint32_t n_msg = 0, const uint64_t* dWK = nullptr,
-                         bool r_host = false, uint32_t mi_stride = 1, int slot = 0) {
+                         uint32_t mi_stride = 1, int slot = 0) {
   if (N == 0) return PBFT_OK;
   const uint64_t blocks = (N + BLOCK - 1) / BLOCK;
   if (blocks > 0x7fffffffull) return set_err(PBFT_EINVAL, "N too large for one launch");
   int rc = slot ? ensure_work2(c, N) : ensure_work(c, N, fst != nullptr);
   if (rc) return rc;
   uint8_t* const wbase = slot ? c->d_work2 : c->d_work;
-  const bool wtwo = slot ? false : c->work_two;
   const bool timing = c->timing && slot == 0;
   int h = 0;
   if (fst) {
@@ -558,15 +537,8 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
   a.bitmap = dB; a.msg_idx = dMI; a.n_msg = n_msg; a.mi_stride = mi_stride; a.latency_mode = latency_mode; a.lat_split = c->lat_split; a.st = st;
   a.pair = c->comb_pair;
   a.cus = c->cus;
-  a.spread = c->comb_spread;
   a.prio = c->comb_prio;
-  // the finish inside the comb launch: not in the pipelined form (its finish runs on the second stream)
-  a.fuse = fst ? 0 : c->comb_fuse;
-  a.stagger = c->comb_stagger;
-  a.group_ctr = (uint32_t*)(wbase + ctr_offset(W, wtwo));
   a.wk = (PBFT_ENV_SCHED && dMI && msg_len == PBFT_ENVELOPE_LEN) ? dWK : nullptr;
-  // R in host memory: the comb leaves an HBM copy for the finish (the latency kernel reads R itself)
-  if (r_host && !latency_mode) a.r_copy = (uint32_t*)(wbase + rcopy_offset(W, wtwo));
   uint32_t* xyz = a.xyz;
   uint8_t* flags = a.flags;
   LT("comb", HIP_TRY(c->pa == PLA_HUGE::P  ? launch_comb_huge(a)
@@ -580,7 +552,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     HIP_TRY(hipStreamWaitEvent(fst, c->ev_comb, 0));
     st = fst;
   }
-  if (!latency_mode && !comb_fused(a)) {  // (the latency kernel, and the fused comb, write the bitmap themselves)
+  if (!latency_mode) {  // (the latency kernel writes the bitmap itself)
     // signatures per finish lane, product tree and waves per SIMD by batch size (PBFT_FIN_* above)
     const bool big = N >= ((uint64_t)1 << 19);
     int fm = big ? PBFT_FIN_FM_BIG : N > PBFT_FIN_SMALL_UPTO ? PBFT_FIN_FM_MID
@@ -592,8 +564,7 @@ static int launch_verify(pbft_ctx* c, const uint8_t* dR, const uint8_t* dS, cons
     if (c->fin_m) fm = c->fin_m;
     if (c->fin_tree >= 0) lv = c->fin_tree;
     const int fw = c->fin_waves ? c->fin_waves : (big ? PBFT_FIN_W_BIG : 1);
-    const uint8_t* fR = a.r_copy ? (const uint8_t*)a.r_copy : dR;
-    LT("finish", HIP_TRY(launch_finish(fm, lv, fw, fR, a.r_copy ? 32 : rs_stride, xyz, flags, N, dB, st)));
+    LT("finish", HIP_TRY(launch_finish(fm, lv, fw, dR, rs_stride, xyz, flags, N, dB, st)));
     HIP_TRY(hipGetLastError());
   }
   if (fst) {
@@ -743,15 +714,7 @@ struct votes_layout {
   }
 };
 
-// The kernels' address of [p, p + bytes) when it lies in the context's mapped staging and zero-copy reads are on,
-// else null (the rows are then copied to HBM first).
-static const uint8_t* zc_dev(const pbft_ctx* c, const void* p, size_t bytes) {
-  const uint8_t* q = (const uint8_t*)p;
-  if (!c->zero_copy || !c->h_stage_dev || q < c->h_stage || q + bytes > c->h_stage + c->h_stage_cap) return nullptr;
-  return c->h_stage_dev + (q - c->h_stage);
-}
-
-// The kernels' address of [p, p + bytes) in the context's mapped staging, else null (whatever the zero-copy option).
+// The kernels' address of [p, p + bytes) in the context's mapped staging, else null.
 static const uint8_t* zc_map(const pbft_ctx* c, const void* p, size_t bytes) {
   const uint8_t* q = (const uint8_t*)p;
   if (!c->h_stage_dev || q < c->h_stage || q + bytes > c->h_stage + c->h_stage_cap) return nullptr;
@@ -854,25 +817,7 @@ static int votes_chunk(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const ui
   }
   c->v_ends.push_back(lo + n);
   const bool rows_form = rs_stride == ROW;
-  const uint8_t* zR = zc_dev(c, R + (size_t)rs_stride * lo, (size_t)rs_stride * n);
-  const uint8_t* zS = rows_form ? zR + 32 : zc_dev(c, S + 32 * lo, 32 * n);
-  const uint8_t* zK = rows_form ? zR + PBFT_VOTES_ROW_KEY : zc_dev(c, K + lo, 2 * n);
-  const uint8_t* zI = rows_form ? zR + PBFT_VOTES_ROW_ENV : zc_dev(c, IDX + lo, 4 * n);
   const uint32_t ks = rows_form ? ROW : 2, mis = rows_form ? ROW / 4 : 1;
-  if (zR && zS && zK && zI) {  // rows in the mapped staging: the kernels read them in place, nothing to copy
-    int rc = 0;
-    LT("kernels", rc = launch_verify(c, zR, zS, (const uint16_t*)zK, c->d_stage, PBFT_ENVELOPE_LEN,
-                                     PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st, rs_stride, ks, nullptr,
-                                     (const uint32_t*)zI, c->v_env, c->v_wk, true, mis, slot));
-    if (rc) return rc;
-    if (c->v_readback) {
-      LT("export_bitmap", HIP_TRY(export_words(c, lo / 64, (n + 63) / 64, st)));
-      LT("rec_rows", HIP_TRY(hipEventRecord(c->ev_rows[c->v_chunk], st)));
-    }
-    c->v_next += n;
-    ++c->v_chunk;
-    return PBFT_OK;
-  }
   uint8_t* base = c->d_stage + c->v_env_bytes + (size_t)b * L.bytes;
   if (c->v_chunk >= VOTES_BUFS) LT("wait_consumed", HIP_TRY(hipStreamWaitEvent(c->cstream, c->ev_consumed[b], 0)));
   if (rows_form) {  // the chunk's rows: one copy
@@ -892,7 +837,7 @@ static int votes_chunk(pbft_ctx* c, const uint8_t* R, const uint8_t* S, const ui
                                    PBFT_ENVELOPE_LEN, PBFT_ENVELOPE_LEN, n, c->d_bitmap + lo / 64, st,
                                    rs_stride, ks, nullptr,
                                    (const uint32_t*)(base + (rows_form ? PBFT_VOTES_ROW_ENV : L.offI)), c->v_env,
-                                   c->v_wk, false, mis, slot));
+                                   c->v_wk, mis, slot));
   if (rc) return rc;
   LT("rec_consumed", HIP_TRY(hipEventRecord(c->ev_consumed[b], st)));
   if (c->v_readback) {  // this chunk's bitmap words (a few KB) back on their own, for the caller to apply early
@@ -1008,19 +953,12 @@ int pbft_verify_ctx_create(int device, pbft_ctx** out) {
   pbft_ctx* c = new pbft_ctx();
   c->device = device;
   c->cus = prop.multiProcessorCount;
-  if (const char* e = getenv("PBFT_COMB_SPREAD")) c->comb_spread = strtol(e, nullptr, 10) != 0;
-  if (const char* e = getenv("PBFT_COMB_STAGGER")) c->comb_stagger = strtol(e, nullptr, 10) != 0;
-  if (const char* e = getenv("PBFT_COMB_FUSE")) {
-    const long v = strtol(e, nullptr, 10);
-    c->comb_fuse = (v == 0 || v == 1) ? (int)v : -1;
-  }
   if (const char* e = getenv("PBFT_COMB_PRIO")) {
     const long v = strtol(e, nullptr, 10);
     c->comb_prio = (v == 0 || v == 1) ? (int)v : -1;
   }
   HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   if (const char* e = getenv("PBFT_SPLIT_BELOW")) c->split_below = strtoull(e, nullptr, 10);
-  if (const char* e = getenv("PBFT_VOTES_ZERO_COPY")) c->zero_copy = strtol(e, nullptr, 10) != 0;
   if (const char* e = getenv("PBFT_VOTES_TWO_STREAMS")) c->two_streams = strtol(e, nullptr, 10) != 0;
   if (const char* e = getenv("PBFT_COMB_PAIR")) {
     const long v = strtol(e, nullptr, 10);
@@ -1311,13 +1249,9 @@ int pbft_verify_ctx_clone(pbft_ctx* parent, pbft_ctx** out) {
   c->fin_waves = parent->fin_waves;
   c->lat_split = parent->lat_split;
   c->timing = parent->timing;
-  c->zero_copy = parent->zero_copy;
   c->two_streams = parent->two_streams;
   c->comb_pair = parent->comb_pair;
-  c->comb_spread = parent->comb_spread;
   c->comb_prio = parent->comb_prio;
-  c->comb_fuse = parent->comb_fuse;
-  c->comb_stagger = parent->comb_stagger;
   c->key_budget_mb = parent->key_budget_mb;
   *out = c;
   return PBFT_OK;
@@ -2105,13 +2039,9 @@ int pbft_verify_set_option(pbft_ctx* c, int option, uint64_t value) {
     case PBFT_OPT_FINISH_WAVES: c->fin_waves = (value == 1 || value == 2) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_LAT_SPLIT: c->lat_split = (value == 4 || value == 8) ? (int)value : 0; return PBFT_OK;
     case PBFT_OPT_KERNEL_TIMING: c->timing = value != 0; return PBFT_OK;
-    case PBFT_OPT_VOTES_ZERO_COPY: c->zero_copy = value != 0; return PBFT_OK;
     case PBFT_OPT_COMB_PAIR: c->comb_pair = value <= 1 ? (int)value : -1; return PBFT_OK;
     case PBFT_OPT_KEY_TABLE_BUDGET_MB: c->key_budget_mb = value; return PBFT_OK;
-    case PBFT_OPT_COMB_SPREAD: c->comb_spread = value != 0; return PBFT_OK;
     case PBFT_OPT_COMB_PRIO: c->comb_prio = value <= 1 ? (int)value : -1; return PBFT_OK;
-    case PBFT_OPT_COMB_FUSE: c->comb_fuse = value <= 1 ? (int)value : -1; return PBFT_OK;
-    case PBFT_OPT_COMB_STAGGER: c->comb_stagger = value != 0; return PBFT_OK;
     case PBFT_OPT_FAULT_INJECT:
       if (value > 2) return set_err(PBFT_EINVAL, "fault injection point");
       c->fault_inject = (int)value;

@@ -270,19 +270,7 @@ static __device__ uint64_t g_comb_stamp[COMB_STAMP_WAVES][8];
 // round) one wave ran as fast as it runs alone (194k cycles, 105 us) and its partner finished ~55 us later on
 // its own, latency-bound (profiles/r05/spread/: lifetimes 193k vs 293k cycles on every SIMD).
 static constexpr uint32_t COMB_PRIO_LDS = 64;  // 8 progress words (+ pad) after the 8 entry buffers
-// FG > 0 (PBFT_OPT_COMB_FUSE): the finish runs inside this launch.  Blocks form groups of FG consecutive blocks;
-// each block publishes its R' (X, Y, Z limbs, written through to memory: agent-scope stores, the flag in bit 31
-// of X limb 0), drains them, and adds one to its group's arrival counter; the block that arrives last runs the
-// finish of the whole group (finish_core.h, FG signatures per lane) after one agent-scope acquire, and resets the
-// counter for the next launch.  Nobody waits for anybody (no spin, whatever the dispatch order or placement), so
-// a group's finish starts as soon as its last comb block is done and overlaps the other blocks' combs -- the
-// separate finish launch, its launch gap and the SIMDs the comb's tail leaves idle are what it takes back.
-// The divstep table (40 KB) goes into the finishing block's LDS once its entry buffers are dead.
-#ifndef PBFT_FUSE_G
-#define PBFT_FUSE_G 2
-#endif
-static constexpr uint32_t FUSE_LDS = DS_TAB_ENTRIES * 8;  // the block's LDS in the fused form: >= the table
-template <int LEN, class PLA, bool CHAIN = false, int WPB = 4, int FG = 0>
+template <int LEN, class PLA, bool CHAIN = false, int WPB = 4>
 __global__ void __launch_bounds__(64 * WPB, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
     uint32_t rs_stride, uint32_t k_stride,
@@ -290,8 +278,7 @@ __global__ void __launch_bounds__(64 * WPB, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
     uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
-    const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy, uint64_t* __restrict__ bitmap,
-    uint32_t* __restrict__ group_ctr) {
+    const uint64_t* __restrict__ wk) {
   using ST = steps<PLB, PLA>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int lane = threadIdx.x & 63;
@@ -332,11 +319,6 @@ __global__ void __launch_bounds__(64 * WPB, PBFT_COMB_WAVES_PER_EU) comb_kernel(
     uint32_t r[8], s[8], a[8];
     load32(r, R + (size_t)rs_stride * ii);
     load32(s, S + (size_t)rs_stride * ii);
-    if (r_copy && live) {  // R read from host memory (zero-copy votes): the finish reads this HBM copy instead
-      uint4* rc = (uint4*)(r_copy + 8 * i);
-      rc[0] = uint4{r[0], r[1], r[2], r[3]};
-      rc[1] = uint4{r[4], r[5], r[6], r[7]};
-    }
     uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
     kok = ki < n_keys;
     if (!kok) ki = 0;
@@ -465,303 +447,6 @@ __global__ void __launch_bounds__(64 * WPB, PBFT_COMB_WAVES_PER_EU) comb_kernel(
 #endif
 #undef COMB_WAIT_VM
 #undef COMB_WAIT_LGKM
-  if constexpr (FG == 1) {
-    // own-block finish: this block's waves finish its own signatures (one per lane): no hand-off between blocks,
-    // so plain stores and the workgroup barrier suffice
-    (void)flags; (void)group_ctr;
-    if (live) {
-#pragma unroll
-      for (int t = 0; t < 10; ++t) {
-        xyz[(size_t)t * N + i] = t == 0 ? (P.X.v[0] | ((s_ok && kok) ? 0x80000000u : 0u)) : P.X.v[t];
-        xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
-        xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
-      }
-    }
-    __syncthreads();  // every wave's R' stored and its entry buffer dead
-    {
-      const uint4* src = (const uint4*)g_ds_tab.e;
-      uint4* dst = (uint4*)lds;
-#pragma unroll
-      for (int k = 0; k < DS_TAB_ENTRIES / 2 / (64 * WPB); ++k)
-        dst[k * 64 * WPB + threadIdx.x] = src[k * 64 * WPB + threadIdx.x];
-      static_assert((DS_TAB_ENTRIES / 2) % (64 * WPB) == 0, "");
-    }
-    __syncthreads();
-    const uint64_t fw = (uint64_t)blockIdx.x * WPB + wave;
-    if (fw * 64 >= N) return;
-    finish_wave<1, PBFT_FIN_LV, false, false, true>(fw, lane, R, rs_stride, xyz, nullptr, N, bitmap,
-                                                   (const uint64_t*)lds);
-    return;
-  } else if constexpr (FG > 0) {
-    (void)flags;
-    if (live) {
-#pragma unroll
-      for (int t = 0; t < 10; ++t) {
-        const uint32_t x = t == 0 ? (P.X.v[0] | ((s_ok && kok) ? 0x80000000u : 0u)) : P.X.v[t];
-        __hip_atomic_store(&xyz[(size_t)t * N + i], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&xyz[(size_t)(10 + t) * N + i], P.Y.v[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&xyz[(size_t)(20 + t) * N + i], P.Z.v[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores before the count
-    __syncthreads();
-    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
-    const uint32_t g = blockIdx.x / FG;
-    if (threadIdx.x == 0) {
-      const uint32_t target = min((uint32_t)FG, gridDim.x - g * FG);
-      const uint32_t old = __hip_atomic_fetch_add(&group_ctr[g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t last = old + 1 == target ? 1u : 0u;
-      if (last) __hip_atomic_store(&group_ctr[g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      lds_write32(lds0, last);
-    }
-    __syncthreads();
-    const uint32_t last = lds_read32(lds0);
-    __syncthreads();  // (every wave has read the word before the table overwrites it)
-    if (!last) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the group's other blocks' R' (their stores drained)
-    {
-      const uint4* src = (const uint4*)g_ds_tab.e;
-      uint4* dst = (uint4*)lds;
-#pragma unroll
-      for (int k = 0; k < DS_TAB_ENTRIES / 2 / (64 * WPB); ++k)
-        dst[k * 64 * WPB + threadIdx.x] = src[k * 64 * WPB + threadIdx.x];
-      static_assert((DS_TAB_ENTRIES / 2) % (64 * WPB) == 0, "");
-    }
-    __syncthreads();
-    const uint64_t fw = (uint64_t)g * WPB + wave;  // finish wave: signatures (fw * FG + m) * 64 + lane
-    if (fw * FG * 64 >= N) return;
-    finish_wave<FG, PBFT_FIN_LV, false, false, true>(fw, lane, R, rs_stride, xyz, nullptr, N, bitmap,
-                                                    (const uint64_t*)lds);
-    return;
-  }
-  if (live) {
-#pragma unroll
-    for (int t = 0; t < 10; ++t) {
-      xyz[(size_t)t * N + i] = P.X.v[t];
-      xyz[(size_t)(10 + t) * N + i] = P.Y.v[t];
-      xyz[(size_t)(20 + t) * N + i] = P.Z.v[t];
-    }
-    flags[i] = (s_ok && kok) ? 1 : 0;
-  }
-}
-
-// ---- staggered hash: 8-wave blocks, one generation (PBFT_OPT_COMB_STAGGER) ---------------------------------
-// At 2 waves per SIMD (the 131k shard) both waves of a SIMD used to hash at the same time -- SHA-512 of R || A || M
-// is one serial dependency chain, ~55k shader cycles at ~55 % issue (profiles/r05/prio: hash 72k of a 267k-cycle
-// lifetime) -- and then ran their issue-bound steps together.  Here the base-point positions (which need only s)
-// come first and the two waves of a SIMD (w and w ^ 4 of an 8-wave block) take the hash at opposite ends of them:
-// wave w < 4 hashes, then sums its 10 base-point positions; wave w + 4 sums its base-point positions first and
-// hashes while its partner is stepping, so the latency-bound chain of one wave runs under the other's mads.  A
-// hashing wave runs at the highest priority (its chain is the latency); two stepping waves trade priorities by
-// their step counts as in comb_kernel<..., WPB = 8>.  Steps: base-point positions 0..PB-1, then key positions; one
-// copy of SHA-512 and of the step body (a runtime segment loop, so the instruction cache holds each once).
-template <int LEN, class PLA>
-__global__ void __launch_bounds__(8 * 64, 2) comb_stagger_kernel(  // (one block per CU: 256 VGPRs, no spill)
-    const uint8_t* __restrict__ R, const uint8_t* __restrict__ S, const uint8_t* __restrict__ key_idx,
-    uint32_t rs_stride, uint32_t k_stride,
-    const uint8_t* __restrict__ msg, uint32_t msg_len, uint32_t msg_stride, uint64_t N, uint64_t Npad,
-    const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
-    const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
-    uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
-    const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy) {
-  constexpr int PB = PLB::P, PA = PLA::P, NS = PB + PA;
-  using mask_t = typename std::conditional<(NS <= 32), uint32_t, uint64_t>::type;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t ebuf = (uint32_t)(uintptr_t)lds + wave * COMB_LDS_PER_WAVE;
-  const uint32_t prog = (uint32_t)(uintptr_t)lds + 8 * COMB_LDS_PER_WAVE;  // step count per wave
-  const uint64_t i = (uint64_t)blockIdx.x * (8 * 64) + threadIdx.x;  // < Npad
-  const bool live = i < N;
-  const uint64_t ii = live ? i : 0;
-  const bool late = (wave & 4u) != 0;  // hashes after its base-point positions
-  if (lane == 0) lds_write32(prog + 4u * wave, 0u);
-  __syncthreads();
-  mask_t sgn = 0;  // bit j: digit of step j is negative (steps 0..PB-1 base point, PB.. key)
-  bool s_ok, kok = false;
-  {
-    uint32_t s[8];
-    load32(s, S + (size_t)rs_stride * ii);
-    s_ok = sc_lt_L(s);
-    sc_clamp_rejected(s, s_ok);
-    digits ds;
-    ds.init(s);
-    static_for<PB>([&](auto pc) {
-      constexpr int pos = decltype(pc)::value;
-      const int d = ds.template take_pos<PLB, pos>();
-      sgn |= (mask_t)(d < 0 ? 1u : 0u) << pos;
-      eidx[(size_t)pos * Npad + i] = PLB::offset(pos) + (uint32_t)(d < 0 ? -d : d);
-    });
-  }
-  const uint8_t* tB = (const uint8_t*)tabB;
-  const uint8_t* tA = (const uint8_t*)tabA;
-  ge P;
-  auto prio_step = [&](int j) {  // publish my step count; lower my priority if I am ahead of my SIMD's partner
-    if (lane == 0) lds_write32(prog + 4u * wave, (uint32_t)j);
-    return lds_read32(prog + 4u * (wave ^ 4u));
-  };
-  auto prio_set = [&](int j, uint32_t partner) {
-    if ((uint32_t)j > (uint32_t)__builtin_amdgcn_readfirstlane((int)partner)) __builtin_amdgcn_s_setprio(0);
-    else __builtin_amdgcn_s_setprio(2);
-  };
-  // The hash is written out twice (before the base-point steps for waves w < 4, after them for w >= 4) rather than
-  // in a two-pass segment loop: inside one loop nest, values live across the hash (the gather's lane addresses,
-  // P) were spilled and reloaded at every step.  Two copies of SHA-512 + one step loop still fit the instruction
-  // cache.  A late wave parks P in LDS over its hash (its idle entry buffer + 2 KB of its own).
-  const uint32_t stash_hi = (uint32_t)(uintptr_t)lds + 8 * COMB_LDS_PER_WAVE + COMB_PRIO_LDS + wave * 2048u;
-  auto stash_addr = [&](int l) { return (l < 32 ? ebuf + 256u * l : stash_hi + 256u * (l - 32)) + 4u * lane; };
-  if (!late) {
-    // the challenge hash and the key positions' entry indices (steps PB..NS-1)
-    __builtin_amdgcn_s_setprio(3);
-    uint32_t r[8], a[8];
-    load32(r, R + (size_t)rs_stride * ii);
-    if (r_copy && live) {
-      uint4* rc = (uint4*)(r_copy + 8 * i);
-      rc[0] = uint4{r[0], r[1], r[2], r[3]};
-      rc[1] = uint4{r[4], r[5], r[6], r[7]};
-  }
-    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
-    kok = ki < n_keys;
-    if (!kok) ki = 0;
-    kok = kok && key_ok[ki];
-  {
-      const uint4* kp = (const uint4*)(keys + 8 * ki);
-      const uint4 k0 = kp[0], k1 = kp[1];
-      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
-  }
-    uint64_t mrow = ii;
-    if (msg_idx) {
-      mrow = msg_idx[(size_t)mi_stride * ii];
-      kok = kok && mrow < n_msg;
-      if (mrow >= n_msg) mrow = 0;
-  }
-    uint32_t h[16], k[8];
-    sha512_k<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len, wk, mrow);
-    sc_reduce512(k, h);
-    const uint32_t keybase = ki * PLA::ENTRIES;
-    digits dk;
-    dk.init(k);
-    static_for<PA>([&](auto pc) {
-      constexpr int pos = decltype(pc)::value;
-      const int d = dk.template take_pos<PLA, pos>();
-      sgn |= (mask_t)(d < 0 ? 1u : 0u) << (PB + pos);
-      eidx[(size_t)(PB + pos) * Npad + i] = keybase + PLA::offset(pos) + (uint32_t)(d < 0 ? -d : d);
-    });
-    __builtin_amdgcn_s_setprio(2);
-  }
-  {
-    // base-point positions: steps 0..PB-1, each entry gathered one step ahead.  (The lane-derived gather
-    // addresses are made here, not hoisted over the hash: live across it they were spilled and reloaded every
-    // step.)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint32_t rd0 = ebuf + 128u * ln + 16u * (ln & 7);
-    dma_entry_lines(tB, eidx[i], ln, ebuf);
-    uint32_t nidx = eidx[Npad + i];
-  {
-      fe qa, qb, k;
-      const bool neg = (uint32_t)sgn & 1u;
-      lds_entry_signed(rd0, neg, qa, qb, k);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      dma_entry_lines(tB, nidx, ln, ebuf);
-      nidx = eidx[2 * Npad + i];
-      ge_from_ab(P, qa, qb, k, neg);
-  }
-#pragma unroll 1
-    for (int j = 1; j < PB; ++j) {
-      fe qa, qb, k;
-      const bool neg = (uint32_t)(sgn >> j) & 1u;
-      const uint32_t partner = prio_step(j);
-      lds_entry_signed(rd0, neg, qa, qb, k);
-      __builtin_amdgcn_s_waitcnt(0xC07F);
-      prio_set(j, partner);
-      if (j + 1 < PB) dma_entry_lines(tB, nidx, ln, ebuf);
-      if (j + 2 < PB) nidx = eidx[(size_t)(j + 2) * Npad + i];
-      ge_madd_ab<true, true>(P, P, qa, qb, k, neg);
-#pragma unroll
-      for (int t = 0; t < 10; ++t) asm("" : "+v"(P.X.v[t]), "+v"(P.Y.v[t]), "+v"(P.Z.v[t]), "+v"(P.T.v[t]));
-  }
-  }
-  if (late) {
-#pragma unroll
-    for (int t = 0; t < 10; ++t) {
-      lds_write32(stash_addr(t), P.X.v[t]);
-      lds_write32(stash_addr(10 + t), P.Y.v[t]);
-      lds_write32(stash_addr(20 + t), P.Z.v[t]);
-      lds_write32(stash_addr(30 + t), P.T.v[t]);
-    }
-    // the challenge hash and the key positions' entry indices (steps PB..NS-1)
-    __builtin_amdgcn_s_setprio(3);
-    uint32_t r[8], a[8];
-    load32(r, R + (size_t)rs_stride * ii);
-    if (r_copy && live) {
-      uint4* rc = (uint4*)(r_copy + 8 * i);
-      rc[0] = uint4{r[0], r[1], r[2], r[3]};
-      rc[1] = uint4{r[4], r[5], r[6], r[7]};
-    }
-    uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
-    kok = ki < n_keys;
-    if (!kok) ki = 0;
-    kok = kok && key_ok[ki];
-    {
-      const uint4* kp = (const uint4*)(keys + 8 * ki);
-      const uint4 k0 = kp[0], k1 = kp[1];
-      a[0] = k0.x; a[1] = k0.y; a[2] = k0.z; a[3] = k0.w; a[4] = k1.x; a[5] = k1.y; a[6] = k1.z; a[7] = k1.w;
-    }
-    uint64_t mrow = ii;
-    if (msg_idx) {
-      mrow = msg_idx[(size_t)mi_stride * ii];
-      kok = kok && mrow < n_msg;
-      if (mrow >= n_msg) mrow = 0;
-    }
-    uint32_t h[16], k[8];
-    sha512_k<LEN>(h, r, a, msg + (size_t)msg_stride * mrow, (int)msg_len, wk, mrow);
-    sc_reduce512(k, h);
-    const uint32_t keybase = ki * PLA::ENTRIES;
-    digits dk;
-    dk.init(k);
-    static_for<PA>([&](auto pc) {
-      constexpr int pos = decltype(pc)::value;
-      const int d = dk.template take_pos<PLA, pos>();
-      sgn |= (mask_t)(d < 0 ? 1u : 0u) << (PB + pos);
-      eidx[(size_t)(PB + pos) * Npad + i] = keybase + PLA::offset(pos) + (uint32_t)(d < 0 ? -d : d);
-    });
-    __builtin_amdgcn_s_setprio(2);
-#pragma unroll
-    for (int t = 0; t < 10; ++t) {
-      P.X.v[t] = lds_read32(stash_addr(t));
-      P.Y.v[t] = lds_read32(stash_addr(10 + t));
-      P.Z.v[t] = lds_read32(stash_addr(20 + t));
-      P.T.v[t] = lds_read32(stash_addr(30 + t));
-    }
-  }
-  // key positions: steps PB..NS-1
-  int ln = lane;
-  asm volatile("" : "+v"(ln));
-  const uint32_t rd0 = ebuf + 128u * ln + 16u * (ln & 7);
-  dma_entry_lines(tA, eidx[(size_t)PB * Npad + i], ln, ebuf);
-  uint32_t nidx = eidx[(size_t)(PB + 1) * Npad + i];
-#pragma unroll 1
-  for (int j = PB; j < NS - 1; ++j) {
-    fe qa, qb, k;
-    const bool neg = (uint32_t)(sgn >> j) & 1u;
-    const uint32_t partner = prio_step(j);
-    lds_entry_signed(rd0, neg, qa, qb, k);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    prio_set(j, partner);
-    dma_entry_lines(tA, nidx, ln, ebuf);
-    if (j + 2 < NS) nidx = eidx[(size_t)(j + 2) * Npad + i];
-    ge_madd_ab<true, true>(P, P, qa, qb, k, neg);
-#pragma unroll
-    for (int t = 0; t < 10; ++t) asm("" : "+v"(P.X.v[t]), "+v"(P.Y.v[t]), "+v"(P.Z.v[t]), "+v"(P.T.v[t]));
-  }
-  {
-    fe qa, qb, k;
-    const bool neg = (uint32_t)(sgn >> (NS - 1)) & 1u;
-    lds_entry_signed(rd0, neg, qa, qb, k);
-    if (lane == 0) lds_write32(prog + 4u * wave, 0xFFFFu);
-    ge_madd_ab<false, true>(P, P, qa, qb, k, neg);
-  }
   if (live) {
 #pragma unroll
     for (int t = 0; t < 10; ++t) {
@@ -827,7 +512,7 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_pair_kerne
     const uint32_t* __restrict__ tabB, const uint32_t* __restrict__ tabA, const uint32_t* __restrict__ keys,
     const uint8_t* __restrict__ key_ok, uint32_t n_keys, uint32_t* __restrict__ xyz, uint8_t* __restrict__ flags,
     uint32_t* __restrict__ eidx, const uint32_t* __restrict__ msg_idx, uint32_t n_msg, uint32_t mi_stride,
-    const uint64_t* __restrict__ wk, uint32_t* __restrict__ r_copy) {
+    const uint64_t* __restrict__ wk) {
   using SP = pair_split<PLA>;
   constexpr int PB = SP::PB, PA = SP::PA, A0 = SP::A0, N1 = SP::N1;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -854,11 +539,6 @@ __global__ void __launch_bounds__(BLOCK, PBFT_COMB_WAVES_PER_EU) comb_pair_kerne
     {
       uint32_t r[8], a[8];
       load32(r, R + (size_t)rs_stride * ii);
-      if (r_copy && live) {
-        uint4* rc = (uint4*)(r_copy + 8 * i);
-        rc[0] = uint4{r[0], r[1], r[2], r[3]};
-        rc[1] = uint4{r[4], r[5], r[6], r[7]};
-      }
       uint32_t ki = *(const uint16_t*)(key_idx + (size_t)k_stride * ii);
       kok = ki < n_keys;
       if (!kok) ki = 0;
@@ -1334,15 +1014,10 @@ struct comb_launch_args {
   uint32_t mi_stride = 1;  // msg_idx[mi_stride * i] (the votes rows layout: PBFT_VOTES_ROW_BYTES / 4)
   uint32_t n_msg;
   const uint64_t* wk;      // votes form, 85-byte envelopes: per-envelope block-2 schedule (null: hash in full)
-  uint32_t* r_copy = nullptr;  // one-lane mode: [N][8] copy of R for the finish (R read from host memory)
   bool latency_mode;
   int lat_split;           // latency mode lanes per signature: 4, 8 or 0 (by batch size)
   int pair = -1;           // one-lane mode: comb_pair_kernel 1 / comb_kernel 0 / by batch size -1
   int cus = 0;             // compute units of the device (0: unknown)
-  int spread = 1;          // one-lane mode: cap blocks per CU at the launch's share (comb_spread_lds)
-  uint32_t* group_ctr = nullptr;  // fused form: per-group arrival counters (zero between launches)
-  int fuse = 0;            // one-lane chain-form comb with the finish in the same launch: 1, 0, -1 by size
-  int stagger = 0;         // the 8-wave launch staggers its waves' hashes (comb_stagger_kernel): 1 on, 0 off
   int prio = -1;           // one-lane chain-form comb: 8-wave blocks with paired wave priorities (WPB = 8): 1 on,
                            // 0 off, -1 by batch size
   hipStream_t st;
@@ -1362,8 +1037,7 @@ static inline size_t comb_spread_lds(uint64_t blocks, int cus, size_t lds_min) {
   return want > lds_min ? want : lds_min;
 }
 
-// Which one-lane comb a launch runs (launch_comb_plan) -- shared with launch_verify, which skips the separate
-// finish when the comb fuses it.
+// Which one-lane comb a launch runs (launch_comb_plan).
 static inline bool comb_pair_sel(const comb_launch_args& a) {
   return a.pair >= 0 ? a.pair > 0 : (a.N >= PBFT_PAIR_MIN_N && a.N <= PBFT_PAIR_MAX_N);
 }
@@ -1379,15 +1053,6 @@ static inline bool comb_chain_prio(const comb_launch_args& a) {
   return comb_chain(a) &&
          (a.prio >= 0 ? a.prio > 0 : (a.cus > 0 && (a.N + 2 * BLOCK - 1) / (2 * BLOCK) <= (uint64_t)a.cus));
 }
-// the finish runs inside the chain-form comb launch (comb_kernel<..., FG>): forced (fuse 1: groups of
-// PBFT_FUSE_G blocks, or each 8-wave block its own) or by size (fuse -1): the one-generation 8-wave launch, where
-// every block finishes its own signatures right after its comb (no launch gap, no R' round trip across blocks).
-// Groups across blocks at 2^20 measured +11.8 % (a finishing block holds a CU slot through its latency-bound
-// inversion: profiles/r05/fuse/), so they are not the default anywhere.
-static inline bool comb_fused(const comb_launch_args& a) {
-  return a.group_ctr && comb_chain(a) && (a.fuse > 0 || (a.fuse < 0 && comb_chain_prio(a)));
-}
-
 // Launch the comb (or, in latency mode, the 4-lanes-per-signature kernel) for
 // key plan PLA; LEN 85 (the signed envelope) is a specialised template.
 template <class PLA>
@@ -1413,52 +1078,37 @@ hipError_t launch_comb_plan(const comb_launch_args& a) {
   } else {
     const uint64_t blocks = (N + BLOCK - 1) / BLOCK, Npad = blocks * BLOCK;
     const bool pair = comb_pair_sel(a);
-    const size_t lds = a.spread ? comb_spread_lds(blocks, a.cus, (BLOCK / 64) * COMB_LDS_PER_WAVE)
-                                : (BLOCK / 64) * COMB_LDS_PER_WAVE;
+    const size_t lds = comb_spread_lds(blocks, a.cus, (BLOCK / 64) * COMB_LDS_PER_WAVE);
     if (pair) {
       const uint64_t pblocks = (N + PAIR_SIGS - 1) / PAIR_SIGS;
-      const size_t plds = a.spread ? comb_spread_lds(pblocks, a.cus, PAIR_LDS) : PAIR_LDS;
+      const size_t plds = comb_spread_lds(pblocks, a.cus, PAIR_LDS);
 #define PBFT_LAUNCH_PAIR(LEN_)                                                                                     \
   hipLaunchKernelGGL((comb_pair_kernel<LEN_, PLA>), dim3((unsigned)pblocks), dim3(BLOCK), plds, a.st, a.R, a.S,     \
                      a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,    \
-                     a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy)
+                     a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk)
       if (a.msg_len == PBFT_ENVELOPE_LEN) PBFT_LAUNCH_PAIR(PBFT_ENVELOPE_LEN);
       else PBFT_LAUNCH_PAIR(-1);
 #undef PBFT_LAUNCH_PAIR
     } else if (comb_chain_prio(a)) {
       const uint64_t b2 = (N + 2 * BLOCK - 1) / (2 * BLOCK), Npad2 = b2 * 2 * BLOCK;  // (eidx sized for this pad)
       const size_t lds2 = 8 * COMB_LDS_PER_WAVE + COMB_PRIO_LDS;
-#define PBFT_LAUNCH_CHAIN8(FG_)                                                                                     \
-  hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true, 8, FG_>), dim3((unsigned)b2), dim3(2 * BLOCK), lds2, \
-                     a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad2, a.tabB,   \
-                     a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride,    \
-                     a.wk, a.r_copy, a.bitmap, a.group_ctr)
-      if (comb_fused(a)) PBFT_LAUNCH_CHAIN8(1);  // one generation: each block finishes its own signatures
-      else if (a.stagger > 0)
-        hipLaunchKernelGGL((comb_stagger_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)b2), dim3(2 * BLOCK),
-                           lds2 + 8 * 2048,  // + the P stash (8 waves x 2 KB)
-                           a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad2,
-                           a.tabB, a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg,
-                           a.mi_stride, a.wk, a.r_copy);
-      else PBFT_LAUNCH_CHAIN8(0);
-#undef PBFT_LAUNCH_CHAIN8
+      hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true, 8>), dim3((unsigned)b2), dim3(2 * BLOCK), lds2,
+                         a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad2, a.tabB,
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride,
+                         a.wk);
     } else if (comb_chain(a)) {
-#define PBFT_LAUNCH_CHAIN4(FG_, LDS_)                                                                               \
-  hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true, 4, FG_>), dim3((unsigned)blocks), dim3(BLOCK), LDS_,  \
-                     a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,    \
-                     a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride,    \
-                     a.wk, a.r_copy, a.bitmap, a.group_ctr)
-      if (comb_fused(a)) PBFT_LAUNCH_CHAIN4(PBFT_FUSE_G, lds > FUSE_LDS ? lds : (size_t)FUSE_LDS);
-      else PBFT_LAUNCH_CHAIN4(0, lds);
-#undef PBFT_LAUNCH_CHAIN4
+      hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA, true, 4>), dim3((unsigned)blocks), dim3(BLOCK), lds,
+                         a.st, a.R, a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB,
+                         a.tabA, a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride,
+                         a.wk);
     } else if (a.msg_len == PBFT_ENVELOPE_LEN)
       hipLaunchKernelGGL((comb_kernel<PBFT_ENVELOPE_LEN, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R,
                          a.S, a.K, a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA,
-                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy, a.bitmap, a.group_ctr);
+                         a.keys, a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk);
     else
       hipLaunchKernelGGL((comb_kernel<-1, PLA>), dim3((unsigned)blocks), dim3(BLOCK), lds, a.st, a.R, a.S, a.K,
                          a.rs_stride, a.k_stride, a.M, a.msg_len, a.msg_stride, N, Npad, a.tabB, a.tabA, a.keys,
-                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk, a.r_copy, a.bitmap, a.group_ctr);
+                         a.key_ok, a.n_keys, a.xyz, a.flags, a.eidx, a.msg_idx, a.n_msg, a.mi_stride, a.wk);
   }
   return hipGetLastError();
 }

@@ -292,13 +292,9 @@ class GpuBatchVerifier:
     OPT_SPLIT_BELOW, OPT_FINISH_WIDTH, OPT_KEY_TABLE_BUDGET_MB, OPT_FINISH_TREE, OPT_LAT_SPLIT = 1, 2, 3, 4, 5
     OPT_KERNEL_TIMING = 7
     OPT_FINISH_WAVES = 8
-    OPT_VOTES_ZERO_COPY = 9
     OPT_COMB_PAIR = 10
     OPT_FAULT_INJECT = 11
-    OPT_COMB_SPREAD = 12
     OPT_COMB_PRIO = 13
-    OPT_COMB_FUSE = 14
-    OPT_COMB_STAGGER = 15
 
     def set_option(self, option: int, value: int) -> None:
         """pbft_verify_set_option: latency-mode threshold, finish width, key-table budget (include/pbft_verify.h)."""

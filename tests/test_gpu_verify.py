@@ -208,44 +208,34 @@ def test_comb_pair_matches_oracle(gv, coracle):
         gv.set_option(gv.OPT_COMB_PAIR, 2)
 
 
-def test_comb_fuse_and_prio_match_oracle(gv, coracle):
-    """r05 comb variants, forced on and off and by size, against the oracle's bits: PBFT_OPT_COMB_STAGGER (the two
-    waves of a SIMD hash at opposite ends of their base-point steps), PBFT_OPT_COMB_PRIO (8-wave blocks
-    whose SIMD-sharing waves trade priorities), PBFT_OPT_COMB_FUSE (the finish inside the comb launch: the last block
-    of each group verifies the group, after agent-scope hand-off of the others' R'), PBFT_OPT_COMB_SPREAD (LDS-capped
-    placement) -- at the 131k shard, ragged sizes whose last group / block is partial, and a size with several
-    generations of blocks; the pair comb forced off so that the chain form runs below its threshold too."""
+def test_comb_prio_match_oracle(gv, coracle):
+    """r05 comb form PBFT_OPT_COMB_PRIO (8-wave blocks whose SIMD-sharing waves trade priorities), forced on and off
+    and by size, against the oracle's bits -- at the 131k shard, ragged sizes whose last block is partial, and a size
+    with several generations of blocks; the pair comb forced off so that the chain form runs below its threshold
+    too.  r06: the rejected variants' options (zero-copy votes 9, spread 12, fused finish 14, staggered hash 15) are
+    gone and refused."""
+    from pbft_amd import PbftError
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 64, 2100, tag=7)         # 268,800 signatures
     assert gv.set_keys(pub).all()
     rng = np.random.default_rng(7)
     R2, S2, K2, M2, idx = adversarial(rng, pub, R, S, key_idx, msg)
     exp = oracle_bits(coracle, pub, R2, S2, K2, M2, 85)
     assert not exp[idx].any()
+    for removed in (9, 12, 14, 15):
+        with pytest.raises(PbftError):
+            gv.set_option(removed, 1)
     try:
         gv.set_option(gv.OPT_COMB_PAIR, 0)
         for n in (131072, 65536 + 63, 131072 - 256 - 5, 200_003, len(R2)):
-            for fuse, prio, spread, stagger in ((2, 2, 1, 0), (1, 2, 1, 0), (1, 1, 1, 0), (1, 0, 0, 0), (0, 1, 1, 0),
-                                                (0, 0, 0, 0), (0, 1, 1, 1), (0, 2, 1, 1)):
-                gv.set_option(gv.OPT_COMB_FUSE, fuse)
+            for prio in (2, 1, 0):
                 gv.set_option(gv.OPT_COMB_PRIO, prio)
-                gv.set_option(gv.OPT_COMB_SPREAD, spread)
-                gv.set_option(gv.OPT_COMB_STAGGER, stagger)
                 got, bm = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
-                assert (got == exp[:n]).all(), (n, fuse, prio, spread, stagger, np.nonzero(got != exp[:n])[0][:10])
+                assert (got == exp[:n]).all(), (n, prio, np.nonzero(got != exp[:n])[0][:10])
                 if n % 64:
                     assert int(bm[-1]) >> (n % 64) == 0
-            # twice in a row with the fused forms: the group counters were reset by the first launch
-            for prio in (0, 1):
-                gv.set_option(gv.OPT_COMB_FUSE, 1)
-                gv.set_option(gv.OPT_COMB_PRIO, prio)
-                got, _ = verify(gv, R2[:n], S2[:n], K2[:n], M2[:n], 85)
-                assert (got == exp[:n]).all(), (n, "repeat", prio)
     finally:
         gv.set_option(gv.OPT_COMB_PAIR, 2)
-        gv.set_option(gv.OPT_COMB_FUSE, 2)
         gv.set_option(gv.OPT_COMB_PRIO, 2)
-        gv.set_option(gv.OPT_COMB_SPREAD, 1)
-        gv.set_option(gv.OPT_COMB_STAGGER, 0)
 
 
 def test_config4_full_size_properties(gv, coracle):
@@ -871,13 +861,10 @@ def test_votes_submit_host_rows(gv, coracle, N):
     assert (bitmap_to_bool(gv.verify_votes(R[:4096], S[:4096], K[:4096], ei[:4096], env), 4096) == exp[:4096]).all()
 
 
-def test_votes_zero_copy_equals_copied(gv, coracle):
-    """PBFT_OPT_VOTES_ZERO_COPY (r04, off by default: slower): votes rows in the context's pinned staging are read
-    by the kernels in place over PCIe (the comb leaves an HBM copy of R for the finish) instead of being copied to
-    HBM chunk by chunk.  On
-    the staged path (pbft_verify_votes_stage / _submit) and the pageable path (copied into the staging first), at
-    a multi-chunk size, one chunk, and latency-mode sizes (that kernel reads R at the end too), both settings give
-    the oracle's bits."""
+def test_votes_staged_and_pageable_chunks(gv, coracle):
+    """The votes form's chunked H2D path (the only one since r06 removed the zero-copy option) on the staged path
+    (pbft_verify_votes_stage / _submit) and the pageable path (copied into the staging first), at a multi-chunk size,
+    one chunk, and latency-mode sizes: the oracle's bits."""
     from pbft_amd import bitmap_to_bool
     seeds, pub, R, S, key_idx, msg = round_batch(gv, 16, 2048, tag=53)   # 65,536 signatures
     assert gv.set_keys(pub).all()
@@ -889,19 +876,14 @@ def test_votes_zero_copy_equals_copied(gv, coracle):
     big = (1 << 18) + 3 * (1 << 16) + 77                                  # chunks 2^16, 2^17, 2^18, rest
     reps = big // len(R) + 1
     RR, SS, KK, II, EE = (np.concatenate([a] * reps)[:big] for a in (R, S, K, ei, exp))
-    try:
-        for zc in (1, 0):
-            gv.set_option(gv.OPT_VOTES_ZERO_COPY, zc)
-            for n in (big, 1 << 16, 4096, 777):
-                st = gv.stage_votes(n, len(env))
-                st["sig"][:, :32], st["sig"][:, 32:] = RR[:n], SS[:n]
-                st["key_idx"][:], st["env_idx"][:], st["envelopes"][:] = KK[:n], II[:n], env
-                got = bitmap_to_bool(gv.wait(gv.submit_staged(n, len(env))), n)
-                assert (got == EE[:n]).all(), ("staged", zc, n, np.nonzero(got != EE[:n])[0][:8])
-                got = bitmap_to_bool(gv.verify_votes(RR[:n], SS[:n], KK[:n], II[:n], env), n)
-                assert (got == EE[:n]).all(), ("pageable", zc, n)
-    finally:
-        gv.set_option(gv.OPT_VOTES_ZERO_COPY, 0)
+    for n in (big, 1 << 16, 4096, 777):
+        st = gv.stage_votes(n, len(env))
+        st["sig"][:, :32], st["sig"][:, 32:] = RR[:n], SS[:n]
+        st["key_idx"][:], st["env_idx"][:], st["envelopes"][:] = KK[:n], II[:n], env
+        got = bitmap_to_bool(gv.wait(gv.submit_staged(n, len(env))), n)
+        assert (got == EE[:n]).all(), ("staged", n, np.nonzero(got != EE[:n])[0][:8])
+        got = bitmap_to_bool(gv.verify_votes(RR[:n], SS[:n], KK[:n], II[:n], env), n)
+        assert (got == EE[:n]).all(), ("pageable", n)
 
 
 def test_multi_gpu_rccl_allgather_one_rank(gv, coracle):

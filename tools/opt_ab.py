@@ -3,7 +3,7 @@
 launches of the config-#4 round's first n signatures (comb + finish per launch), per size.
 
 usage: python tools/opt_ab.py OPTION VALUE_A VALUE_B [--sizes 131072,65536] [--rounds 8] [--iters 20]
-e.g. tools/opt_ab.py 12 0 1   (PBFT_OPT_COMB_SPREAD off / on)"""
+e.g. tools/opt_ab.py 13 0 1   (PBFT_OPT_COMB_PRIO off / on)"""
 import argparse
 import os
 import sys
