@@ -532,7 +532,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
         for mode, rounds, warm in modes:
             out = res.setdefault(mode, {"ingress_ms": [], "flush_ms": [], "timings": []}) if not warm else None
             for _ in range(rounds):
-                seq0 = 1 + (1 << 20) + rnd * n_seq  # (seqs past the replica_flush leg's)
+                seq0 = 1 + rnd * n_seq  # (a replica of its own: its log starts at seq 1)
                 rnd += 1
                 m, _ = envelopes(seq0, n_seq, n_rep)
                 Rr, Sr, _ = v.sign(seeds, key_idx, m, ENVELOPE)

@@ -54,6 +54,9 @@ struct fin_unroll<0> {
 #endif
 #define FIN_USE_TAB (PBFT_FIN_TAB && !PBFT_ABL_NOINV && !PBFT_FIN_EXP)
 static_assert(PBFT_FIN_LV == 4 || PBFT_FIN_LV == 6, "");
+#ifndef PBFT_FIN_PREFETCH_R
+#define PBFT_FIN_PREFETCH_R 1  // PRE: R's encoding and the comb's flag loaded up front too
+#endif
 #ifndef PBFT_FIN_DPP
 #define PBFT_FIN_DPP 0  // 1: product-tree partners by DPP / ds_swizzle instead of ds_bpermute (r04 A/B: no difference)
 #endif
@@ -96,6 +99,9 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
   // prefix products of Z (lanes past N contribute 1)
   fe pre[FM];
   fe zs[PRE ? FM : 1], xs[PRE ? FM : 1], ys[PRE ? FM : 1];
+  constexpr bool PRE_R = PRE && PBFT_FIN_PREFETCH_R;
+  uint32_t rs[PRE_R ? FM : 1][8];
+  bool fls[PRE_R ? FM : 1];
   fin_unroll<FM>::up([&](auto mc) {
     constexpr int m = decltype(mc)::value;
     const uint64_t i = base + (uint64_t)m * 64;
@@ -106,6 +112,10 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
       const uint64_t ii = i < N ? i : 0;
       load_fe(xs[m], Xb, N, ii);
       load_fe(ys[m], Yb, N, ii);
+      if constexpr (PRE_R) {  // (issued before the inversion: the compare no longer waits on memory at the end)
+        load32(rs[m], R + (size_t)rs_stride * ii);
+        fls[m] = flags[ii];
+      }
     }
     if constexpr (m == 0) pre[0] = z;
     else fe_mul(pre[m], pre[m - 1], z);
@@ -181,13 +191,21 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
       load_fe(X, Xb, N, ii);
       load_fe(Y, Yb, N, ii);
     }
-    const bool fl = flags[ii];
+    bool fl;
+    uint32_t r[8];
+    if constexpr (PRE_R) {
+      fl = fls[m];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) r[t] = rs[m][t];
+    } else {
+      fl = flags[ii];
+      load32(r, R + (size_t)rs_stride * ii);
+    }
     fe_mul(x, X, zi);
     fe_mul(y, Y, zi);
-    uint32_t xw[8], yw[8], r[8], ry[8];
+    uint32_t xw[8], yw[8], ry[8];
     fe_to_words(xw, x);
     fe_to_words(yw, y);
-    load32(r, R + (size_t)rs_stride * ii);
     canon_y(ry, r);
     bool eq = (xw[0] & 1u) == (r[7] >> 31);
 #pragma unroll

@@ -1629,6 +1629,29 @@ static inline int push_fast(pbft_replica* r, uint8_t kind, uint64_t seq, const u
   return 1;
 }
 
+// The same common case for a push_many thread writing into its sink's reserved rows: push_into's outcome, or -1
+// (then push_into decides).
+static inline int push_into_fast(Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer, const uint8_t* sig,
+                                 PushCounts& st, Sink& sk) {
+  if (w.committed_reported) return -1;
+  Phase& p = w.ph[kind];
+  if (p.cnt.empty() || p.digs.size() != 1 || p.cnt[signer] || p.acc[signer] || p.row.size() == p.row.capacity() ||
+      sk.grow || sk.row >= sk.row_end || p.dgen[0] != sk.a->gen || !eq64(p.digs[0].data(), digest))
+    return -1;
+  const uint64_t ri = sk.row++;
+  put_row(sk.a->rows + ROWB * ri, sig, signer, p.denv[0], sk.nt);
+  p.row.push_back(sk.aid << 31 | (uint32_t)ri);
+  p.who.push_back((uint16_t)signer);
+  p.dix.push_back(0);
+  ++p.n_pending;
+  if (ri + 1 > p.row_hi) p.row_hi = ri + 1;
+  ++p.distinct;
+  ++p.cnt[signer];
+  ++sk.added;
+  ++st.queued;
+  return 1;
+}
+
 int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]) {
   if (!r || !digest || !sig || (kind != PBFT_KIND_PREPARE && kind != PBFT_KIND_COMMIT)) return PBFT_EINVAL;
@@ -1837,7 +1860,8 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         for (const Run& u : runs) {
           if (u.owner != t) continue;
           for (uint64_t i = u.lo; i < u.hi; ++i)
-            if (!bad[i]) push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
+            if (!bad[i] && push_into_fast(*u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk) < 0)
+              push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
         }
         for (; sk.row < sk.row_end; ++sk.row) put_row(A.rows + ROWB * sk.row, zero_sig, 0, 0, g_stream_stores);
         for (; sk.env < sk.env_end; ++sk.env)
@@ -1868,8 +1892,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
             if (bad[i] || k >= P) continue;  // (k < P always: the quotas add up to the thread's good rows)
             sk.row = slot;
             sk.row_end = slot + 1;
-            if (push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk) != 1)
-              put_row(A.rows + ROWB * slot, zero_sig, 0, 0, g_stream_stores);
+            int got = push_into_fast(*u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
+            if (got < 0) got = push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
+            if (got != 1) put_row(A.rows + ROWB * slot, zero_sig, 0, 0, g_stream_stores);
             ++slot;
             if (++used == q_rows[t * P + k])
               do close_part(); while (k < P && q_rows[t * P + k] == 0);
@@ -2409,6 +2434,11 @@ int pbft_replica_push_records(pbft_replica* r, uint32_t peer_idx, const uint8_t*
   size_t i = 0;
   for (; i < n; ++i) {
     const uint8_t* rec = stream + (size_t)PBFT_RECORD_BYTES * i;
+    if (i + 4 < n) {  // (a read's records are consumed in order: fetch ahead of the push)
+      __builtin_prefetch(rec + 4 * PBFT_RECORD_BYTES);
+      __builtin_prefetch(rec + 4 * PBFT_RECORD_BYTES + 64);
+      __builtin_prefetch(rec + 4 * PBFT_RECORD_BYTES + 128);
+    }
     const uint8_t* env = rec + 64;
     uint16_t key;
     memcpy(&key, rec + 150, 2);

@@ -1,0 +1,24 @@
+#!/bin/bash
+# r06 GPU step: replica GPU tests, the changed verify tests, the ingress probe, the finish stamps at the 131k shard.
+# usage: tools/gpu_r06.sh TAG [steps...]   steps: replica verify ingress finstamps (default: all)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
+TAG=${1:-run}; shift; D=gpurun_out/r06_$TAG; mkdir -p $D
+STEPS=${@:-replica verify ingress finstamps}
+for s in $STEPS; do
+  case $s in
+    replica) timeout -k 10 480 python -u -m pytest tests/test_gpu_replica.py -x -v --timeout 300 --timeout-method thread > $D/replica_tests.log 2>&1 ;;
+    verify) timeout -k 10 400 python -u -m pytest tests/test_gpu_verify.py -x -v -k "prio_match or staged_and_pageable or update_keys" --timeout 300 --timeout-method thread > $D/verify_tests.log 2>&1 ;;
+    gputests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1 ;;
+    ingress) timeout -k 10 480 python -u tools/ingress_probe.py > $D/ingress.json 2> $D/ingress.err ;;
+    finstamps) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_finstamps.so build/ab/libpbft_finpre_stamps.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finstamps.txt 2>&1 ;;
+    bench) timeout -k 10 600 python -u bench.py > $D/bench.json 2> $D/bench.err ;;
+    step) timeout -k 10 120 tools/microbench/step_study > $D/step_study.txt 2>&1 ;;
+    pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
+    smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;
+  esac
+  rc=$?
+  echo "step $s rc=$rc"
+  [ $rc -ne 0 ] && { tail -5 $D/*.log $D/*.err 2>/dev/null | tail -20; exit $rc; }
+done
+exit 0
