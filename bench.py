@@ -142,7 +142,7 @@ def cpu_baselines(keys, R, S, key_idx, msg, expect, budget_s: float = 10.0):
 def pmc_traffic(pb: int, pa: int, n: int) -> dict:
     """HBM bytes per launch of the verify pair from the committed rocprofv3 --pmc passes (separate runs of this
     same command, tools/gpu_prof.sh): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE of comb + finish."""
-    for rel in ("r05/pmc_comb", "r04/pmc_comb", "r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
+    for rel in ("r06/pmc_comb", "r05/pmc_comb", "r04/pmc_comb", "r03/pmc_comb", "r02_pmc_comb", "r01_pmc_comb"):
         p = os.path.join(ROOT, "profiles", rel, "derived.json")
         try:
             d = json.load(open(p))
@@ -156,6 +156,24 @@ def pmc_traffic(pb: int, pa: int, n: int) -> dict:
                 "valu_insts_per_sig_comb": d["comb_kernel"].get("valu_insts_per_sig"),
                 "source": f"profiles/{rel}/derived.json (PMC passes, not this run)"}
     return {}
+
+
+def shard_pmc(n: int) -> dict:
+    """the shard's comb and finish duration and VALU busy from the committed rocprofv3 trace + PMC
+    passes of this library at the shard size (tools/gpu_prof.sh with --seqs 256; profiles/r06/shard/derived.json)."""
+    p = os.path.join(ROOT, "profiles", "r06", "shard", "derived.json")
+    try:
+        d = json.load(open(p))
+    except (OSError, ValueError):
+        return {}
+    if d.get("sigs_per_launch") != n:
+        return {}
+    out = {"source": "profiles/r06/shard/derived.json (rocprofv3 trace + PMC passes, not this run)"}
+    for k in ("comb_kernel", "finish_kernel"):
+        e = d.get(k, {})
+        out[k] = {"us": (e.get("avg_ns") or 0) / 1e3 or None, "valu_busy_pct": e.get("valu_busy_pct"),
+                  "valu_insts_per_sig": e.get("valu_insts_per_sig")}
+    return out
 
 
 def stream_latency(v, R, S, key_idx, msg, offered_sigs_per_s: float, batch: int = 4096, n_ctx: int = 4,
@@ -510,8 +528,10 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
     L = lib()
     D = ctypes.CDLL(INGRESS_LIB)
     vp = ctypes.c_void_p
-    D.ingress_push.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp]
-    D.ingress_streams.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp, vp, vp]
+    D.ingress_push.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    D.ingress_streams.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
+    pmu_names = ("cycles", "instructions", "llc_references", "llc_misses", "l1d_read_misses", "dtlb_read_misses")
+    pmu = (ctypes.c_uint64 * D.ingress_pmu_counters())()
     n_rep = len(pub)
     n = 2 * n_rep * n_seq
     modes = modes or [("push", 2, True), ("push", 3, False), ("records_1", 3, False), ("records_64", 2, False),
@@ -530,7 +550,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
     rnd = 0
     try:
         for mode, rounds, warm in modes:
-            out = res.setdefault(mode, {"ingress_ms": [], "flush_ms": [], "timings": []}) if not warm else None
+            out = res.setdefault(mode, {"ingress_ms": [], "flush_ms": [], "timings": [], "pmu": []}) if not warm else None
             for _ in range(rounds):
                 seq0 = 1 + rnd * n_seq  # (a replica of its own: its log starts at seq 1)
                 rnd += 1
@@ -553,7 +573,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
                     qd = ctypes.c_uint64()
                     assert D.ingress_push(rep, n, kind.ctypes.data, view.ctypes.data, seq.ctypes.data,
                                           digs.ctypes.data, signer.ctypes.data, sigs.ctypes.data, ctypes.byref(qd),
-                                          ctypes.byref(sec)) == 0 and qd.value == n
+                                          ctypes.byref(sec), pmu) == 0 and qd.value == n
                 else:
                     binary, per_visit = mode.startswith("records"), int(mode.split("_")[1])
                     streams = []
@@ -568,7 +588,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
                     lens = (ctypes.c_uint64 * n_rep)(*[len(s_) for s_ in streams])
                     pushed, dropped, calls = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
                     assert D.ingress_streams(rep, int(binary), n_rep, ptrs, lens, per_visit, ctypes.byref(pushed),
-                                             ctypes.byref(dropped), ctypes.byref(calls), ctypes.byref(sec)) == 0
+                                             ctypes.byref(dropped), ctypes.byref(calls), ctypes.byref(sec), pmu) == 0
                     assert pushed.value == n and dropped.value == 0, (pushed.value, dropped.value)
                 rows = ctypes.c_uint64()
                 ne = ctypes.c_uint32()
@@ -590,6 +610,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
                     out["ingress_ms"].append(sec.value * 1e3)
                     out["flush_ms"].append((t1 - t0) * 1e3)
                     out["timings"].append(replica_timings(L, rep))
+                    out["pmu"].append([int(x) for x in pmu])
     finally:
         L.pbft_replica_destroy(rep)
     legs = {}
@@ -597,7 +618,14 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
         ing, fl = np.array(o["ingress_ms"]), np.array(o["flush_ms"])
         tot = ing + fl
         worst = int(np.argmax(tot))
+        pm = np.median(np.array(o["pmu"], dtype=np.float64), axis=0) if o["pmu"] else None
+        host = None
+        if pm is not None and pm[0] > 0:  # per vote, medians over the rounds (perf_event_open, user space)
+            host = {k: float(v / n) for k, v in zip(pmu_names, pm)}
+            host["ipc"] = float(pm[1] / pm[0])
+            host["ghz"] = float(pm[0] / (np.median(ing) * 1e-3) / 1e9)
         legs[mode] = {"ingress_votes_per_s": n / (np.median(ing) * 1e-3), "ingress_ms": float(np.median(ing)),
+                      "host_pmu_per_vote": host,
                       "flush_ms": float(np.median(fl)), "flush_ms_max": float(fl.max()),
                       "end_to_end_votes_per_s": n / (np.median(tot) * 1e-3), "rounds": len(ing),
                       "max_round": {"ingress_ms": float(ing[worst]), "flush_ms": float(fl[worst]),
@@ -1099,6 +1127,7 @@ def main():
         p8 = (time.perf_counter() - tp) * 1e3 / 50
         extras["shard_of_8"] = {"sigs": n8, "kernel_ms": k8, "wall_ms_per_launch": w8,
                                 "verifies_per_s_per_gpu": n8 / (k8 * 1e-3), "pipelined_wall_ms_per_launch": p8,
+                                "kernel_ms_5_samples": [a for a, _ in s8], "pmc": shard_pmc(n8),
                                 "note": "device-resident launches over the shard one GPU of 8 verifies"}
         # p50 latency of a 4096-signature round (config #5 batch size), device-resident
         lat = []

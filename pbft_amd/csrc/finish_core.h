@@ -55,7 +55,10 @@ struct fin_unroll<0> {
 #define FIN_USE_TAB (PBFT_FIN_TAB && !PBFT_ABL_NOINV && !PBFT_FIN_EXP)
 static_assert(PBFT_FIN_LV == 4 || PBFT_FIN_LV == 6, "");
 #ifndef PBFT_FIN_PREFETCH_R
-#define PBFT_FIN_PREFETCH_R 1  // PRE: R's encoding and the comb's flag loaded up front too
+#define PBFT_FIN_PREFETCH_R 0  // 1: (PRE) R and the flag loaded up front too -- r06: no faster at the shard (the wait moves)
+#endif
+#ifndef PBFT_FIN_PAR
+#define PBFT_FIN_PAR 0  // 1: the tree and back-substitution products with the latency-oriented reduction (fe_reduce_par)
 #endif
 #ifndef PBFT_FIN_DPP
 #define PBFT_FIN_DPP 0  // 1: product-tree partners by DPP / ds_swizzle instead of ds_bpermute (r04 A/B: no difference)
@@ -118,7 +121,7 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
       }
     }
     if constexpr (m == 0) pre[0] = z;
-    else fe_mul(pre[m], pre[m - 1], z);
+    else fe_mulT<PBFT_FIN_PAR>(pre[m], pre[m - 1], z);
   });
   FIN_STAMP(1);
   fe inv;
@@ -128,7 +131,7 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
     constexpr int k = decltype(kc)::value;
 #pragma unroll
     for (int u = 0; u < 10; ++u) tq[k].v[u] = tree_partner<k>(t.v[u]);
-    fe_mul(t, t, tq[k]);
+    fe_mulT<PBFT_FIN_PAR>(t, t, tq[k]);
   });
   FIN_STAMP(2);
 #if PBFT_ABL_NOINV  // ablation: no inversion (timing only, results wrong)
@@ -165,7 +168,7 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
   FIN_STAMP(3);
   static_for<LV>([&](auto kc) {
     constexpr int k = LV - 1 - decltype(kc)::value;
-    fe_mul(inv, inv, tq[k]);  // 1 / (product of this lane's 2^k group)
+    fe_mulT<PBFT_FIN_PAR>(inv, inv, tq[k]);  // 1 / (product of this lane's 2^k group)
   });
   FIN_STAMP(4);
   fin_unroll<FM>::down([&](auto mc) {
@@ -175,11 +178,11 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
     const uint64_t ii = live ? i : 0;
     fe zi;
     if constexpr (m > 0) {
-      fe_mul(zi, inv, pre[m - 1]);   // 1 / Z_m
+      fe_mulT<PBFT_FIN_PAR>(zi, inv, pre[m - 1]);   // 1 / Z_m
       fe z;
       if constexpr (PRE) z = zs[m];
       else if (live) load_fe(z, Zb, N, ii); else fe_one(z);
-      fe_mul(inv, inv, z);           // 1 / (Z_0 ... Z_{m-1})
+      fe_mulT<PBFT_FIN_PAR>(inv, inv, z);           // 1 / (Z_0 ... Z_{m-1})
     } else {
       zi = inv;
     }
@@ -201,8 +204,8 @@ __device__ __forceinline__ void finish_wave(uint64_t wave, int lane, const uint8
       fl = flags[ii];
       load32(r, R + (size_t)rs_stride * ii);
     }
-    fe_mul(x, X, zi);
-    fe_mul(y, Y, zi);
+    fe_mulT<PBFT_FIN_PAR>(x, X, zi);
+    fe_mulT<PBFT_FIN_PAR>(y, Y, zi);
     uint32_t xw[8], yw[8], ry[8];
     fe_to_words(xw, x);
     fe_to_words(yw, y);

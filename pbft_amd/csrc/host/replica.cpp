@@ -586,15 +586,13 @@ static bool sink_row(pbft_replica* r, Sink& s, uint64_t* idx) {
 // (pbft_verify_votes_open) and every further piece is launched (pbft_verify_votes_piece) while the caller keeps
 // pushing, so at the flush only the last < piece + 64 rows are left to copy and verify: flush_submit launches them,
 // closes the batch and adopts it (one context; a replica over several contexts hands its arena over at the flush).
-// PBFT_EARLY_PIECE: rows per piece (default 2^16; read once -- this runs on every push).
-static uint64_t early_piece_rows() {
-  static const uint64_t rows = [] {
-    const char* e = getenv("PBFT_EARLY_PIECE");
-    const long long v = e ? strtoll(e, nullptr, 10) : (1 << 16);
-    return (uint64_t)(v < 4096 ? 4096 : v > (1 << 22) ? (1 << 22) : v) & ~(uint64_t)63;
-  }();
-  return rows;
-}
+// PBFT_EARLY_PIECE: rows per piece (default 2^16; read once, at load -- this runs on every push).
+static const uint64_t g_early_piece = [] {
+  const char* e = getenv("PBFT_EARLY_PIECE");
+  const long long v = e ? strtoll(e, nullptr, 10) : (1 << 16);
+  return (uint64_t)(v < 4096 ? 4096 : v > (1 << 22) ? (1 << 22) : v) & ~(uint64_t)63;
+}();
+static inline uint64_t early_piece_rows() { return g_early_piece; }
 static void early_single(pbft_replica* r) {
   if (r->eu.active && !r->eu.open) return;  // push_many's batch (closed): nothing to add
   Arena& A = r->arena[r->cur];
@@ -1585,6 +1583,7 @@ static void add_counts(pbft_replica* r, const PushCounts& c) {
 // inject_node_event Prepare / Commit arms (src/behavior.rs:340-412): enqueue into the round window
 static inline bool eq64(const uint8_t* a, const uint8_t* b) {  // 64 bytes, branch-free
   uint64_t x = 0;
+#pragma GCC unroll 8
   for (int q = 0; q < 8; ++q) {
     uint64_t u, v;
     memcpy(&u, a + 8 * q, 8);
@@ -1599,8 +1598,10 @@ static inline bool eq64(const uint8_t* a, const uint8_t* b) {  // 64 bytes, bran
 // looked up or in the ring, its phase already holds exactly this digest with an envelope in the current arena, the
 // signer has neither a candidate nor an accepted vote there, and the arena and the phase's columns have room.  The
 // outcome is the general path's (push_into) for the same vote; anything else takes the general path.
-static inline int push_fast(pbft_replica* r, uint8_t kind, uint64_t seq, const uint8_t* digest, uint32_t signer,
-                            const uint8_t* sig) {
+// (flatten: the columns' push_back and the row's stores inline -- host PMU on the GPU box, r06: ~250 instructions per
+// vote through this call with them as calls)
+__attribute__((flatten)) static int push_fast(pbft_replica* r, uint8_t kind, uint64_t seq, const uint8_t* digest,
+                                              uint32_t signer, const uint8_t* sig) {
   Window* w = r->last_w && r->last_seq == seq ? r->last_w : nullptr;
   if (!w) {
     Window* x = r->ring[seq & r->ring_mask];
@@ -1631,8 +1632,8 @@ static inline int push_fast(pbft_replica* r, uint8_t kind, uint64_t seq, const u
 
 // The same common case for a push_many thread writing into its sink's reserved rows: push_into's outcome, or -1
 // (then push_into decides).
-static inline int push_into_fast(Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer, const uint8_t* sig,
-                                 PushCounts& st, Sink& sk) {
+__attribute__((flatten)) static int push_into_fast(Window& w, uint8_t kind, const uint8_t* digest, uint32_t signer,
+                                                   const uint8_t* sig, PushCounts& st, Sink& sk) {
   if (w.committed_reported) return -1;
   Phase& p = w.ph[kind];
   if (p.cnt.empty() || p.digs.size() != 1 || p.cnt[signer] || p.acc[signer] || p.row.size() == p.row.capacity() ||
@@ -1706,37 +1707,43 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; bool first; };
     RTRACE(r, "push", n_ok);
     const uint64_t tp0 = now_ns();
-    std::vector<std::vector<Run>> slice_runs(T);
+    // (in 8 chunks per thread, taken dynamically: a worker the host deschedules holds up one chunk, not a
+    // sixteenth of the call -- the r06 replica leg's slowest round had this pass at 4.1 ms against 0.3)
+    const size_t C = T * 8;
+    std::vector<std::vector<Run>> slice_runs(C);
     std::vector<uint8_t> bad(n_ok);
     std::vector<PushCounts> cnt(T);
+    std::atomic<size_t> next_chunk{0};
     WorkerPool::get().run(T, [&](size_t t) {
-      const uint64_t lo = n_ok * t / T, hi = n_ok * (t + 1) / T;
-      std::vector<Run>& runs = slice_runs[t];
-      // (locals: the byte stores below may alias anything, which would reload every field per row)
-      const uint32_t n = r->n;
-      const uint64_t cur = r->current_view, h = r->h, win = r->log_window;
-      uint64_t rv = 0, rw = 0, run_seq = ~0ull, run_lo = 0, run_good = 0;
-      uint8_t* bd = bad.data();
-      for (uint64_t i = lo; i < hi; ++i) {
-        const uint64_t q = seq[i];
-        const bool v_bad = signer[i] >= n || view[i] != cur;
-        const bool w_bad = !v_bad && !(q > h && q - h <= win);
-        rv += v_bad;
-        rw += w_bad;
-        bd[i] = v_bad | w_bad;
-        if (v_bad | w_bad) continue;
-        if (q != run_seq) {
-          if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0, run_good, false});
-          run_seq = q;
-          run_lo = i;
-          run_good = 0;
+      for (size_t ch; (ch = next_chunk.fetch_add(1, std::memory_order_relaxed)) < C;) {
+        const uint64_t lo = n_ok * ch / C, hi = n_ok * (ch + 1) / C;
+        std::vector<Run>& runs = slice_runs[ch];
+        // (locals: the byte stores below may alias anything, which would reload every field per row)
+        const uint32_t n = r->n;
+        const uint64_t cur = r->current_view, h = r->h, win = r->log_window;
+        uint64_t rv = 0, rw = 0, run_seq = ~0ull, run_lo = 0, run_good = 0;
+        uint8_t* bd = bad.data();
+        for (uint64_t i = lo; i < hi; ++i) {
+          const uint64_t q = seq[i];
+          const bool v_bad = signer[i] >= n || view[i] != cur;
+          const bool w_bad = !v_bad && !(q > h && q - h <= win);
+          rv += v_bad;
+          rw += w_bad;
+          bd[i] = v_bad | w_bad;
+          if (v_bad | w_bad) continue;
+          if (q != run_seq) {
+            if (run_seq != ~0ull) runs.push_back({run_lo, i, run_seq, nullptr, 0, run_good, false});
+            run_seq = q;
+            run_lo = i;
+            run_good = 0;
+          }
+          ++run_good;
         }
-        ++run_good;
+        if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good, false});
+        cnt[t].pushed += hi - lo;
+        cnt[t].rejected_view += rv;
+        cnt[t].rejected_watermark += rw;
       }
-      if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good, false});
-      cnt[t].pushed += hi - lo;
-      cnt[t].rejected_view += rv;
-      cnt[t].rejected_watermark += rw;
     });
     //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
     //     owner: the thread whose share of the rows its first run starts in; each thread's range of the arena:

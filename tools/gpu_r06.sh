@@ -13,6 +13,7 @@ for s in $STEPS; do
     ingress) timeout -k 10 480 python -u tools/ingress_probe.py > $D/ingress.json 2> $D/ingress.err ;;
     finstamps) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_finstamps.so build/ab/libpbft_finpre_stamps.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finstamps.txt 2>&1 ;;
     bench) timeout -k 10 600 python -u bench.py > $D/bench.json 2> $D/bench.err ;;
+    finvar) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_findpp.so build/ab/libpbft_finpar.so build/ab/libpbft_finboth.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finvar.txt 2>&1 ;;
     step) timeout -k 10 120 tools/microbench/step_study > $D/step_study.txt 2>&1 ;;
     pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;

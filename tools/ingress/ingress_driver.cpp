@@ -8,7 +8,11 @@
 //                    (UviBytes/JSON frames -> pbft_replica_push_frames, or 160-byte binary records ->
 //                    pbft_replica_push_records) to the replica, the connection being the authenticated peer.
 // Built by __graft_entry__.build() next to the library it links (tools/ingress/libingress.so).
+#include <linux/perf_event.h>
+#include <sys/ioctl.h>
+#include <sys/syscall.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <cstdint>
 #include <cstring>
@@ -35,13 +39,62 @@ static size_t frames_bytes(const uint8_t* buf, size_t len, uint32_t k) {
   return off;
 }
 
+// Host PMU counters around the timed loop (perf_event_open, user space only; every counter 0 where the kernel
+// refuses them): cycles, instructions, LLC references, LLC misses, L1D read misses, dTLB read misses.
+static constexpr int N_PMU = 6;
+struct Pmu {
+  int fd[N_PMU];
+  Pmu() {
+    static const uint32_t type[N_PMU] = {PERF_TYPE_HARDWARE, PERF_TYPE_HARDWARE, PERF_TYPE_HARDWARE,
+                                         PERF_TYPE_HARDWARE, PERF_TYPE_HW_CACHE, PERF_TYPE_HW_CACHE};
+    static const uint64_t cfg[N_PMU] = {
+        PERF_COUNT_HW_CPU_CYCLES, PERF_COUNT_HW_INSTRUCTIONS, PERF_COUNT_HW_CACHE_REFERENCES,
+        PERF_COUNT_HW_CACHE_MISSES,
+        PERF_COUNT_HW_CACHE_L1D | (PERF_COUNT_HW_CACHE_OP_READ << 8) | (PERF_COUNT_HW_CACHE_RESULT_MISS << 16),
+        PERF_COUNT_HW_CACHE_DTLB | (PERF_COUNT_HW_CACHE_OP_READ << 8) | (PERF_COUNT_HW_CACHE_RESULT_MISS << 16)};
+    for (int k = 0; k < N_PMU; ++k) {
+      perf_event_attr a;
+      memset(&a, 0, sizeof a);
+      a.type = type[k];
+      a.size = sizeof a;
+      a.config = cfg[k];
+      a.disabled = 1;
+      a.exclude_kernel = 1;
+      a.exclude_hv = 1;
+      fd[k] = (int)syscall(SYS_perf_event_open, &a, 0, -1, -1, 0);
+    }
+  }
+  void start() {
+    for (int k = 0; k < N_PMU; ++k)
+      if (fd[k] >= 0) { ioctl(fd[k], PERF_EVENT_IOC_RESET, 0); ioctl(fd[k], PERF_EVENT_IOC_ENABLE, 0); }
+  }
+  void stop(uint64_t* out) {
+    for (int k = 0; k < N_PMU; ++k) {
+      uint64_t v = 0;
+      if (fd[k] >= 0) {
+        ioctl(fd[k], PERF_EVENT_IOC_DISABLE, 0);
+        if (read(fd[k], &v, sizeof v) != (ssize_t)sizeof v) v = 0;
+      }
+      if (out) out[k] = v;
+    }
+  }
+  ~Pmu() {
+    for (int k = 0; k < N_PMU; ++k)
+      if (fd[k] >= 0) close(fd[k]);
+  }
+};
+
 extern "C" {
+
+int ingress_pmu_counters() { return N_PMU; }
 
 int ingress_push(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
                  const uint8_t* digests, const uint32_t* signer, const uint8_t* sigs, uint64_t* queued,
-                 double* seconds) {
+                 double* seconds, uint64_t* pmu) {
   uint64_t q = 0;
   int rc = 0;
+  Pmu P;
+  P.start();
   const double t0 = now_s();
   for (uint64_t i = 0; i < N; ++i) {
     const int p = pbft_replica_push(r, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i);
@@ -49,16 +102,19 @@ int ingress_push(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_
     q += (uint64_t)p;
   }
   *seconds = now_s() - t0;
+  P.stop(pmu);
   *queued = q;
   return rc;
 }
 
 int ingress_streams(pbft_replica* r, int binary, uint32_t n_conn, const uint8_t* const* streams,
                     const uint64_t* lens, uint32_t per_visit, uint64_t* pushed, uint64_t* dropped, uint64_t* calls,
-                    double* seconds) {
+                    double* seconds, uint64_t* pmu) {
   std::vector<uint64_t> off(n_conn, 0);
   uint64_t np = 0, nd = 0, nc = 0;
   int rc = 0;
+  Pmu P;
+  P.start();
   const double t0 = now_s();
   for (bool more = true; more && rc == 0;) {
     more = false;
@@ -81,6 +137,7 @@ int ingress_streams(pbft_replica* r, int binary, uint32_t n_conn, const uint8_t*
     }
   }
   *seconds = now_s() - t0;
+  P.stop(pmu);
   *pushed = np;
   *dropped = nd;
   *calls = nc;
