@@ -470,6 +470,10 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
     if modes:
         by_mode = {m: {k: float(np.median([x for x, mm in zip(v_, mode_of) if mm == m])) for k, v_ in res.items()}
                    for m in sorted(set(modes))}
+        for m in by_mode:
+            tot = [x for x, mm in zip(res["total_ms"], mode_of) if mm == m]
+            by_mode[m]["total_ms_mean"] = float(np.mean(tot))
+            by_mode[m]["total_ms_max"] = float(np.max(tot))
     return {"value": n / (med["total_ms"] * 1e-3), "unit": "verifies/s", "ms_per_round": med["total_ms"],
             **({"by_mode": by_mode} if by_mode else {}),
             "ms_per_round_min_max": [float(np.min(res["total_ms"])), float(np.max(res["total_ms"]))],
@@ -491,7 +495,7 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
 
 TIMING_FIELDS = ("push_checks_ns", "push_windows_ns", "push_rows_ns", "submit_segs_ns", "submit_launch_ns", "wait_ns",
                  "apply_partial_ns", "apply_final_ns", "gc_ns", "polls", "early_pieces", "early_piece_ns",
-                 "early_last_rows")
+                 "early_last_rows", "push_checks_end_min_ns", "push_rows_start_max_ns", "push_rows_end_min_ns")
 
 
 def replica_timings(L, rep):

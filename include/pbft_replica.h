@@ -132,6 +132,12 @@ typedef struct {
   uint64_t early_pieces;     /* single pushes before that flush_submit: early-batch pieces launched...            */
   uint64_t early_piece_ns;   /*   ...and the pushing thread's time inside those launches                          */
   uint64_t early_last_rows;  /* rows flush_submit launched as the early batch's last piece                        */
+  /* the last push_many's worker spread (from the start of its pass): the first worker done with the checks, the
+   * last worker to start pushing rows and the first one done -- a late start is a descheduled or slow-waking worker,
+   * an early end far from push_rows_ns an imbalance or a worker interrupted mid-pass */
+  uint64_t push_checks_end_min_ns;
+  uint64_t push_rows_start_max_ns;
+  uint64_t push_rows_end_min_ns;
 } pbft_replica_timings;
 
 /* Optional verifier override (tests without a GPU): same SoA contract as

@@ -112,6 +112,9 @@ pub struct pbft_replica_timings {
     pub early_pieces: u64,
     pub early_piece_ns: u64,
     pub early_last_rows: u64,
+    pub push_checks_end_min_ns: u64,
+    pub push_rows_start_max_ns: u64,
+    pub push_rows_end_min_ns: u64,
 }
 
 /// Phases of the last pbft_verify_set_keys / pbft_verify_update_keys (host wall time, ms).

@@ -1005,13 +1005,11 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
 
 // Threads for the batch fill and the bitmap application of large batches: PBFT_REPLICA_THREADS (default 16,
 // capped by the host; 16 vs 8: 2^20 round 5.3-5.7 vs 5.8-6.2 ms, profiles/r03/ab_threads.txt).
+// (read per call -- once per batch, not per vote: an A/B can vary it round by round in one process)
 static size_t host_threads() {
-  static const size_t t = [] {
-    const char* e = getenv("PBFT_REPLICA_THREADS");
-    const long v = e ? strtol(e, nullptr, 10) : 16;
-    return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
-  }();
-  return t;
+  const char* e = getenv("PBFT_REPLICA_THREADS");
+  const long v = e ? strtol(e, nullptr, 10) : 16;
+  return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
 }
 
 // Apply segments [s0, s1) of the batch (rows all verified); large ranges on several threads, cut at window
@@ -1714,6 +1712,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     std::vector<uint8_t> bad(n_ok);
     std::vector<PushCounts> cnt(T);
     std::atomic<size_t> next_chunk{0};
+    std::vector<uint64_t> t_done(T, 0);
     WorkerPool::get().run(T, [&](size_t t) {
       for (size_t ch; (ch = next_chunk.fetch_add(1, std::memory_order_relaxed)) < C;) {
         const uint64_t lo = n_ok * ch / C, hi = n_ok * (ch + 1) / C;
@@ -1744,6 +1743,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         cnt[t].rejected_view += rv;
         cnt[t].rejected_watermark += rw;
       }
+      t_done[t] = now_ns();
     });
     //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
     //     owner: the thread whose share of the rows its first run starts in; each thread's range of the arena:
@@ -1859,7 +1859,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //     unused rows (rejected pushes) become rows no candidate references (key 0, envelope 0), its unused
     //     envelopes copies of envelope 0
     static const uint8_t zero_sig[64] = {0};
+    std::vector<uint64_t> t_beg(T, 0), t_end(T, 0);
     WorkerPool::get().start(T, [&](size_t t) {
+      t_beg[t] = now_ns();
       // (thread-local copies: the threads' entries of cnt / sinks share cache lines, and every row updates them)
       PushCounts c = cnt[t];
       Sink sk = sinks[t];
@@ -1912,6 +1914,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       if (g_stream_stores) stream_fence();  // (streaming stores are weakly ordered: drained before the join)
       cnt[t] = c;
       sinks[t] = sk;
+      t_end[t] = now_ns();
     });
     if (early) {  // launch part k as soon as every thread has finished it (its 64-row padding written here first)
       for (size_t k = 0; k < P; ++k) {
@@ -1964,6 +1967,9 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     r->tm.push_checks_ns = tp1 - tp0;
     r->tm.push_windows_ns = tp2 - tp1;
     r->tm.push_rows_ns = now_ns() - tp2;
+    r->tm.push_checks_end_min_ns = *std::min_element(t_done.begin(), t_done.end()) - tp0;
+    r->tm.push_rows_start_max_ns = *std::max_element(t_beg.begin(), t_beg.end()) - tp2;
+    r->tm.push_rows_end_min_ns = *std::min_element(t_end.begin(), t_end.end()) - tp2;
     if (g_push_trace && r->trace.size() >= 4) {  // PBFT_PUSH_TRACE (with PBFT_REPLICA_TRACE): pass times of this call
       auto at = [&](const char* what) {
         for (size_t x = r->trace.size(); x-- > 0;)

@@ -30,7 +30,9 @@ class Stats(ctypes.Structure):
 class Timings(ctypes.Structure):  # include/pbft_replica.h pbft_replica_timings
     _fields_ = [(n, ctypes.c_uint64) for n in ("push_checks_ns", "push_windows_ns", "push_rows_ns", "submit_segs_ns",
                                                 "submit_launch_ns", "wait_ns", "apply_partial_ns", "apply_final_ns",
-                                                "gc_ns", "polls", "early_pieces", "early_piece_ns", "early_last_rows")]
+                                                "gc_ns", "polls", "early_pieces", "early_piece_ns", "early_last_rows",
+                                                "push_checks_end_min_ns", "push_rows_start_max_ns",
+                                                "push_rows_end_min_ns")]
 
 
 VERIFY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,

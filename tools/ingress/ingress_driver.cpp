@@ -61,6 +61,8 @@ struct Pmu {
       a.disabled = 1;
       a.exclude_kernel = 1;
       a.exclude_hv = 1;
+      // (more events than the core has counters: the kernel time-multiplexes them -- scaled by enabled / running)
+      a.read_format = PERF_FORMAT_TOTAL_TIME_ENABLED | PERF_FORMAT_TOTAL_TIME_RUNNING;
       fd[k] = (int)syscall(SYS_perf_event_open, &a, 0, -1, -1, 0);
     }
   }
@@ -70,10 +72,11 @@ struct Pmu {
   }
   void stop(uint64_t* out) {
     for (int k = 0; k < N_PMU; ++k) {
-      uint64_t v = 0;
+      uint64_t v = 0, rd[3];
       if (fd[k] >= 0) {
         ioctl(fd[k], PERF_EVENT_IOC_DISABLE, 0);
-        if (read(fd[k], &v, sizeof v) != (ssize_t)sizeof v) v = 0;
+        if (read(fd[k], rd, sizeof rd) == (ssize_t)sizeof rd && rd[2] > 0)
+          v = (uint64_t)((double)rd[0] * (double)rd[1] / (double)rd[2]);
       }
       if (out) out[k] = v;
     }

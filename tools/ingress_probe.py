@@ -19,6 +19,9 @@ def main():
     ap.add_argument("--seqs", type=int, default=bench.SEQS)
     ap.add_argument("--skip-flush-leg", action="store_true")
     ap.add_argument("--modes", default="")
+    ap.add_argument("--skip-ingress-leg", action="store_true")
+    ap.add_argument("--flush-ab", default="", help="ENV=v1,v2,...: the flush leg cycled over these values")
+    ap.add_argument("--rounds", type=int, default=9)
     a = ap.parse_args()
     import torch  # noqa: F401
     from pbft_amd import GpuBatchVerifier
@@ -34,7 +37,16 @@ def main():
     assert v.set_keys(pub).all()
     out = {}
     if not a.skip_flush_leg:
-        out["replica_flush_2^20"] = bench.replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect)
+        fa = {}
+        if a.flush_ab:
+            env, vals = a.flush_ab.split("=")
+            fa = {"modes": vals.split(","), "mode_env": env}
+        out["replica_flush_2^20"] = bench.replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect,
+                                                            rounds=a.rounds, **fa)
+        if a.skip_ingress_leg:
+            print(json.dumps(out), flush=True)
+            v.close()
+            return
     modes = None
     if a.modes:
         modes = [("push", 2, True)] + [(m, 2, False) for m in a.modes.split(",")]
