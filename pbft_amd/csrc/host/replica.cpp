@@ -182,11 +182,16 @@ static inline void stream_fence() {
   _mm_sfence();
 #endif
 }
+static inline void cpu_relax() {
+#if defined(__x86_64__)
+  _mm_pause();
+#endif
+}
 
 struct Window {
   Phase ph[3];  // [0] PrePrepare candidates, [1] Prepare, [2] Commit
   uint64_t seq = 0;        // its (current-view) sequence number: the ring slot seq & ring_mask holds it
-  uint64_t push_call = 0;  // the last push_many that routed rows here, and the thread it gave the window to
+  uint64_t push_call = 0;  // the last push_many that routed rows here, and the task it gave the window to
   uint32_t push_owner = 0;
   bool have_pre_prepare = false;
   bool dirty = false;      // in pbft_replica::dirty (events to be re-evaluated)
@@ -344,8 +349,9 @@ struct pbft_replica {
   uint32_t peak_envs = 0;  // sizes the arena for a whole round before it opens: pieces read it in place)
   uint32_t busy_arena = 0;
   uint64_t applied_upto = 0;  // rows_done at the last progressive application
-  bool adopted = false;       // the batch in flight is push_many's early batch: applied once, when done (its rows
-                              // lie part by part, so a landed prefix of rows is no prefix of the windows)
+  bool adopted = false;       // the batch in flight is an early batch (push_many's or the single pushes')
+  bool adopt_partial = true;  // ... applied as its pieces land (r06: push_many's rows lie task by task, so a landed
+                              // prefix of rows is a prefix of the windows; PBFT_ADOPT_PARTIAL=0: once, when done)
   pbft_ctx* ctx = nullptr;         // ctxs[0]: digests, small batches
   std::vector<pbft_ctx*> ctxs;     // pbft_replica_create_multi: large batches split over these (one per GPU)
   uint32_t n = 0, f = 0, self = 0;
@@ -1678,6 +1684,12 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
 
 // push_many of at least this many rows runs on the worker pool (PBFT_REPLICA_THREADS threads)
 static constexpr uint64_t PUSH_PAR_MIN = 1u << 14;
+// push_many's tasks per worker thread (PBFT_PUSH_TASKS, 1..64, default 8; read per call)
+static size_t push_tasks_per_thread() {
+  const char* e = getenv("PBFT_PUSH_TASKS");
+  const long v = e ? strtol(e, nullptr, 10) : 8;
+  return (size_t)(v < 1 ? 1 : v > 64 ? 64 : v);
+}
 
 int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_t* view, const uint64_t* seq,
                            const uint8_t* digests, const uint32_t* signer, const uint8_t* sigs, uint64_t* queued) {
@@ -1745,38 +1757,47 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       }
       t_done[t] = now_ns();
     });
-    //  2. (this thread) the windows of the runs -- created here, the only map insertions -- and each window's
-    //     owner: the thread whose share of the rows its first run starts in; each thread's range of the arena:
-    //     a row per row it may push, two envelopes per window it owns (one per kind: honest rounds) + 64
+    //  2. (this thread) the windows of the runs -- created here, the only window insertions -- grouped into G tasks
+    //     (r06: PBFT_PUSH_TASKS per thread, default 8) by the input position of each window's first run; a task
+    //     holds every run of its windows, in input order (per-window order is all the state machine depends on), and
+    //     its own range of the arena: a row per row it may push, two envelopes per window whose first run it holds
+    //     + 8.  The threads take the tasks in order as they free up, so a worker the host slows (a remote socket, a
+    //     busy SMT sibling, an interrupt) takes fewer of them instead of holding the pass up: with one fixed range per
+    //     thread, the first worker of a slow round finished in a third of the pass (push_rows_end_min_ns).
     RTRACE(r, "push_checked", T);
     const uint64_t tp1 = now_ns();
     std::vector<Run> runs;
     for (auto& v : slice_runs) runs.insert(runs.end(), v.begin(), v.end());
     const uint64_t call = ++r->push_calls;
-    std::vector<uint64_t> t_rows(T, 0), t_envs(T, 64);
+    const size_t G = std::max<size_t>(1, std::min<size_t>(T * push_tasks_per_thread(), runs.size()));
+    std::vector<uint64_t> g_rows(G, 0), g_envs(G, 8);
     for (Run& u : runs) {
       Window& w = window_at(r, u.seq);
       u.w = &w;
       u.first = w.push_call != call;
-      if (u.first) {  // the window's first run in this call: its owner
+      if (u.first) {  // the window's first run in this call: its task
         w.push_call = call;
-        w.push_owner = (uint32_t)(u.lo * T / n_ok);
-        t_envs[w.push_owner] += 2;
+        w.push_owner = (uint32_t)(u.lo * G / n_ok);
+        g_envs[w.push_owner] += 2;
       }
       u.owner = w.push_owner;
-      t_rows[u.owner] += u.good;
+      g_rows[u.owner] += u.good;
+    }
+    std::vector<uint32_t> g_first(G + 1, 0), order(runs.size());  // runs by task, input order within a task
+    for (const Run& u : runs) ++g_first[u.owner + 1];
+    for (size_t g = 0; g < G; ++g) g_first[g + 1] += g_first[g];
+    {
+      std::vector<uint32_t> at(g_first.begin(), g_first.end() - 1);
+      for (size_t x = 0; x < runs.size(); ++x) order[at[runs[x].owner]++] = (uint32_t)x;
     }
     Arena& A = push_arena(r);
     uint64_t rows_all = 0;
-    for (size_t t = 0; t < T; ++t) rows_all += t_rows[t];
-    // Early batch (r05): with one GPU context, no batch in flight and a large call, the arena range of this call is
-    // cut into P parts, each thread's rows split evenly over them (part k of every thread side by side), so that
-    // part k is complete once every thread has pushed the first (k + 1) / P of its rows: this thread launches each
-    // part (pbft_verify_votes_piece) as soon as it is, while the threads push the next -- the copies and kernels of
-    // the round run under push_many instead of after flush_submit.  Each part's envelopes are its own range (two per
-    // window whose first run falls in it, + 8 per thread); rows of rejected pushes and the 64-row padding of a part
-    // are rows no candidate references.
-    // (PBFT_EARLY_PARTS: the part count, 2..32, default 8 -- read per call: A/B in one process)
+    for (size_t g = 0; g < G; ++g) rows_all += g_rows[g];
+    // Early batch (r05): with GPU contexts, no batch in flight and a large call, the arena range of this call is
+    // launched in pieces while the threads push -- each piece a prefix of finished tasks (every task's range starts
+    // 64-aligned: bitmap words), about 1/P of the rows (PBFT_EARLY_PARTS, 2..32, default 8, read per call: A/B in one
+    // process) -- so the copies and kernels of the round run under push_many instead of after flush_submit.  Rows
+    // of rejected pushes and each task's padding are rows no candidate references.
     const size_t P = [] {
       const char* e = getenv("PBFT_EARLY_PARTS");
       const long v = e ? strtol(e, nullptr, 10) : 8;
@@ -1785,159 +1806,118 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     const bool early = early_enabled() && direct_enabled() && r->ctx && !r->verify_fn && !r->vsub &&
                        !r->in_flight && !r->eu.active && A.rows_pinned && A.envs_pinned &&
                        A.clean.load(std::memory_order_relaxed) && rows_all >= (1u << 17);
-    std::vector<uint64_t> q_rows(early ? T * P : 0), q_envs(early ? T * P : 0);  // [t * P + k]
-    std::vector<uint64_t> r_off(early ? T * P : 0), e_off(early ? T * P : 0), piece_end(P), env_end(P), part_end(P);
-    uint64_t rows_total = rows_all, envs_total = 0;
-    for (size_t t = 0; t < T; ++t) envs_total += t_envs[t];
-    if (early) {
-      for (size_t t = 0; t < T; ++t)
-        for (size_t k = 0; k < P; ++k) {
-          q_rows[t * P + k] = t_rows[t] * (k + 1) / P - t_rows[t] * k / P;
-          q_envs[t * P + k] = 8;
-        }
-      std::vector<uint64_t> cum(T, 0);
-      for (const Run& u : runs) {  // (a window's envelopes are written with its first row: the part of that row)
-        const uint64_t g = t_rows[u.owner];
-        if (u.first && g) q_envs[u.owner * P + std::min<uint64_t>(P - 1, cum[u.owner] * P / g)] += 2;
-        cum[u.owner] += u.good;
-      }
+    std::vector<uint64_t> g_row0(G + 1), g_env0(G + 1);
+    {
       uint64_t row = A.n, env = A.ne;
-      for (size_t k = 0; k < P; ++k) {
-        for (size_t t = 0; t < T; ++t) {
-          r_off[t * P + k] = row;
-          e_off[t * P + k] = env;
-          row += q_rows[t * P + k];
-          env += q_envs[t * P + k];
-        }
-        part_end[k] = row;
-        if (k + 1 < P) row = (row + 63) & ~(uint64_t)63;  // (pieces start 64-aligned: bitmap words)
-        piece_end[k] = row;
-        env_end[k] = env;
+      for (size_t g = 0; g < G; ++g) {
+        g_row0[g] = row;
+        g_env0[g] = env;
+        row += g_rows[g];
+        if (early) row = (row + 63) & ~(uint64_t)63;
+        env += g_envs[g];
       }
-      rows_total = piece_end[P - 1] - A.n;
-      envs_total = env_end[P - 1] - A.ne;
+      g_row0[G] = row;
+      g_env0[G] = env;
     }
-    if (!arena_reserve(r, A, rows_total, envs_total)) return PBFT_ENOMEM;  // (nothing pushed)
-    std::vector<Sink> sinks;
-    if (!early) {
-      uint64_t row = A.n, env = A.ne;
-      for (size_t t = 0; t < T; ++t) {
-        sinks.push_back(Sink{&A, r->cur, row, row + t_rows[t], (uint32_t)env, (uint32_t)(env + t_envs[t]), false,
-                             g_stream_stores});
-        row += t_rows[t];
-        env += t_envs[t];
+    if (!arena_reserve(r, A, g_row0[G] - A.n, g_env0[G] - A.ne)) return PBFT_ENOMEM;  // (nothing pushed)
+    // several contexts (one per GPU): context j takes tasks [tb[j], tb[j + 1]) -- balanced by rows, the first tasks
+    // to the first context, whose GPU starts first -- as one batch of its own, its first piece carrying every
+    // envelope written so far (its rows may name any of them)
+    const size_t K = early ? std::min<size_t>(r->ctxs.size(), G) : 0;
+    std::vector<size_t> tb(K + 1, G);
+    std::vector<uint64_t> ctx_lo(K + 1);
+    if (early) {
+      tb[0] = 0;
+      const uint64_t span = g_row0[G] - A.n;
+      for (size_t j = 1; j < K; ++j) {
+        size_t g = tb[j - 1] + 1;
+        while (g < G - (K - j) && g_row0[g] - A.n < span * j / K) ++g;
+        tb[j] = g;
       }
-    } else {
-      for (size_t t = 0; t < T; ++t) sinks.push_back(Sink{&A, r->cur, 0, 0, 0, 0, false, g_stream_stores});
+      for (size_t j = 0; j <= K; ++j) ctx_lo[j] = j == 0 ? 0 : g_row0[tb[j]];
     }
     bool launched = false;
-    // several contexts (one per GPU): context j takes parts [j P / K, (j + 1) P / K) as one batch of its own -- the
-    // earlier parts to the first context, whose GPU starts first -- each batch's first piece carrying every envelope
-    // written so far (its rows may name any of them)
-    const size_t K = early ? std::min<size_t>(r->ctxs.size(), P) : 0;
-    std::vector<size_t> part0(K + 1);
-    std::vector<uint64_t> ctx_lo(K + 1);
-    for (size_t j = 0; j <= K; ++j) {
-      part0[j] = j * P / (K ? K : 1);
-      ctx_lo[j] = part0[j] == 0 ? 0 : piece_end[part0[j] - 1];
-    }
     size_t opened = 0;
     if (early) {  // the batches are opened before the threads start: envelope 0 and the rows pushed before this call
-      r->bitmap.assign((piece_end[P - 1] + 63) / 64, 0);
+      r->bitmap.assign((g_row0[G] + 63) / 64, 0);
       launched = true;
       for (size_t j = 0; j < K && launched; ++j) {
-        launched = pbft_verify_votes_open(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j], (uint32_t)env_end[part0[j + 1] - 1],
+        launched = pbft_verify_votes_open(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j], (uint32_t)g_env0[tb[j + 1]],
                                           r->bitmap.data() + ctx_lo[j] / 64) == PBFT_OK;
         if (launched) opened = j + 1;
       }
     }
-    std::unique_ptr<std::atomic<uint32_t>[]> parts_done(new std::atomic<uint32_t>[P]);
-    for (size_t k = 0; k < P; ++k) parts_done[k].store(0, std::memory_order_relaxed);
+    std::unique_ptr<std::atomic<uint32_t>[]> g_done(new std::atomic<uint32_t>[G]);
+    for (size_t g = 0; g < G; ++g) g_done[g].store(0, std::memory_order_relaxed);
+    std::atomic<size_t> next_task{0};
+    std::vector<int64_t> added(T, 0);
     RTRACE(r, "push_windows", runs.size());
     const uint64_t tp2 = now_ns();
-    //  3. (threads) every thread pushes the rows of the windows it owns, in input order, into its range; the range's
-    //     unused rows (rejected pushes) become rows no candidate references (key 0, envelope 0), its unused
+    //  3. (threads) every task pushes the rows of its windows in input order into its range; the range's unused
+    //     rows (rejected pushes, the padding) become rows no candidate references (key 0, envelope 0), its unused
     //     envelopes copies of envelope 0
     static const uint8_t zero_sig[64] = {0};
     std::vector<uint64_t> t_beg(T, 0), t_end(T, 0);
     WorkerPool::get().start(T, [&](size_t t) {
       t_beg[t] = now_ns();
-      // (thread-local copies: the threads' entries of cnt / sinks share cache lines, and every row updates them)
+      // (thread-local copies: the threads' entries of cnt share cache lines, and every row updates them)
       PushCounts c = cnt[t];
-      Sink sk = sinks[t];
-      if (!early) {
-        for (const Run& u : runs) {
-          if (u.owner != t) continue;
+      int64_t add = 0;
+      for (size_t g; (g = next_task.fetch_add(1, std::memory_order_relaxed)) < G;) {
+        Sink sk{&A, r->cur, g_row0[g], g_row0[g] + g_rows[g], (uint32_t)g_env0[g], (uint32_t)(g_env0[g] + g_envs[g]),
+                false, g_stream_stores};
+        for (uint32_t x = g_first[g]; x < g_first[g + 1]; ++x) {
+          const Run& u = runs[order[x]];
           for (uint64_t i = u.lo; i < u.hi; ++i)
             if (!bad[i] && push_into_fast(*u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk) < 0)
               push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
         }
-        for (; sk.row < sk.row_end; ++sk.row) put_row(A.rows + ROWB * sk.row, zero_sig, 0, 0, g_stream_stores);
+        for (uint64_t x = sk.row; x < g_row0[g + 1]; ++x) put_row(A.rows + ROWB * x, zero_sig, 0, 0, g_stream_stores);
         for (; sk.env < sk.env_end; ++sk.env)
           memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
-      } else {
-        // every good row takes the next slot of the current part (its row, or a row no candidate references)
-        size_t k = 0;
-        uint64_t used = 0, slot = r_off[t * P];
-        sk.env = (uint32_t)e_off[t * P];
-        sk.env_end = (uint32_t)(e_off[t * P] + q_envs[t * P]);
-        auto close_part = [&]() {  // part k of this thread is written: its unused envelopes, then the signal
-          for (; sk.env < sk.env_end; ++sk.env)
-            memcpy(A.envs + (size_t)PBFT_ENVELOPE_BYTES * sk.env, A.envs, PBFT_ENVELOPE_BYTES);
-          stream_fence();
-          parts_done[k].fetch_add(1, std::memory_order_release);
-          ++k;
-          used = 0;
-          if (k < P) {
-            slot = r_off[t * P + k];
-            sk.env = (uint32_t)e_off[t * P + k];
-            sk.env_end = (uint32_t)(e_off[t * P + k] + q_envs[t * P + k]);
-          }
-        };
-        while (k < P && q_rows[t * P + k] == 0) close_part();
-        for (const Run& u : runs) {
-          if (u.owner != t) continue;
-          for (uint64_t i = u.lo; i < u.hi; ++i) {
-            if (bad[i] || k >= P) continue;  // (k < P always: the quotas add up to the thread's good rows)
-            sk.row = slot;
-            sk.row_end = slot + 1;
-            int got = push_into_fast(*u.w, kind[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
-            if (got < 0) got = push_into(r, *u.w, kind[i], view[i], seq[i], digests + 64 * i, signer[i], sigs + 64 * i, c, sk);
-            if (got != 1) put_row(A.rows + ROWB * slot, zero_sig, 0, 0, g_stream_stores);
-            ++slot;
-            if (++used == q_rows[t * P + k])
-              do close_part(); while (k < P && q_rows[t * P + k] == 0);
-          }
+        add += sk.added;
+        if (early) {
+          stream_fence();  // (streaming stores are weakly ordered: visible before the task is marked done)
+          g_done[g].store(1, std::memory_order_release);
         }
-        while (k < P) close_part();  // (never: the quotas add up to the thread's good rows)
       }
-      if (g_stream_stores) stream_fence();  // (streaming stores are weakly ordered: drained before the join)
+      if (g_stream_stores) stream_fence();  // (drained before the join)
       cnt[t] = c;
-      sinks[t] = sk;
+      added[t] = add;
       t_end[t] = now_ns();
     });
-    if (early) {  // launch part k as soon as every thread has finished it (its 64-row padding written here first)
-      for (size_t k = 0; k < P; ++k) {
-        // (sleeping, not spinning: the T workers have the host's cores; a 17th runnable thread slows one of them,
-        // and the pass waits for its slowest worker)
-        while (parts_done[k].load(std::memory_order_acquire) < T) std::this_thread::sleep_for(std::chrono::microseconds(20));
-        for (uint64_t x = part_end[k]; x < piece_end[k]; ++x) put_row(A.rows + ROWB * x, zero_sig, 0, 0, false);
-        if (launched) {
-          size_t j = 0;
-          while (part0[j + 1] <= k) ++j;  // the context of part k
-          const uint64_t lo = (k ? piece_end[k - 1] : 0) - ctx_lo[j];
-          const uint32_t elo = k == part0[j] ? 0 : (uint32_t)env_end[k - 1];
-          launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], lo, piece_end[k] - ctx_lo[j], A.envs,
-                                             elo, (uint32_t)env_end[k]) == PBFT_OK;
-          if (launched && k + 1 == part0[j + 1])
-            launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
+    if (early) {
+      // launch each context's finished prefix of tasks once it holds ~1/P of the rows (or the context is complete)
+      const uint64_t step = std::max<uint64_t>(64, (g_row0[G] - A.n) / P);
+      size_t done = 0, j = 0;
+      uint64_t plo = 0;   // the context's next piece starts here (absolute row)
+      uint32_t elo = 0;   // ... and its new envelopes here
+      while (j < K) {
+        while (done < G && g_done[done].load(std::memory_order_acquire)) ++done;
+        const size_t end = std::min(done, tb[j + 1]);
+        if (end == tb[j + 1] || (end > tb[j] && g_row0[end] - plo >= step)) {
+          if (launched && g_row0[end] > plo)
+            launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], plo - ctx_lo[j],
+                                               g_row0[end] - ctx_lo[j], A.envs, elo, (uint32_t)g_env0[end]) == PBFT_OK;
+          plo = g_row0[end];
+          elo = (uint32_t)g_env0[end];
+          if (end == tb[j + 1]) {
+            if (launched) launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
+            ++j;
+            elo = 0;
+          }
+          continue;
         }
+        // (sleeping, not spinning, while most tasks are left: the T workers have the host's cores; the last ones
+        // are waited for with pauses, so that the last piece goes out as soon as they are done)
+        if (G - done > T) std::this_thread::sleep_for(std::chrono::microseconds(20));
+        else for (int s = 0; s < 64; ++s) cpu_relax();
       }
     }
     WorkerPool::get().wait();
+    A.n = g_row0[G];
+    A.ne = (uint32_t)g_env0[G];
     if (early) {
-      A.n = piece_end[P - 1];
-      A.ne = (uint32_t)env_end[P - 1];
       if (launched) {
         r->eu.active = true;
         r->eu.done = false;
@@ -1948,17 +1928,14 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       } else {
         // (a failed open, piece or close dropped that context's batch; the other opened ones are dropped -- a close
         // that does not match drops a batch still open -- or finished, and forgotten)
-        for (size_t j = 0; j < opened; ++j) {
-          (void)pbft_verify_votes_close(r->ctxs[j], 0);
-          (void)pbft_verify_wait(r->ctxs[j]);
+        for (size_t jj = 0; jj < opened; ++jj) {
+          (void)pbft_verify_votes_close(r->ctxs[jj], 0);
+          (void)pbft_verify_wait(r->ctxs[jj]);
         }
       }
       RTRACE(r, "early", launched);
-    } else {
-      A.n += rows_all;
-      A.ne += (uint32_t)envs_total;
     }
-    for (Sink& sk : sinks) A.live.fetch_add(sk.added, std::memory_order_relaxed);
+    for (int64_t a : added) A.live.fetch_add(a, std::memory_order_relaxed);
     for (const PushCounts& c : cnt) {
       add_counts(r, c);
       q += c.queued;
@@ -2082,6 +2059,10 @@ static int adopt_early(pbft_replica* r, uint64_t N) {
   r->in_flight_via = 0;
   r->eu.active = false;
   r->adopted = true;
+  r->adopt_partial = [] {
+    const char* e = getenv("PBFT_ADOPT_PARTIAL");
+    return !e || atoi(e) != 0;
+  }();
   RTRACE(r, "adopted", A.n);
   return PBFT_OK;
 }
@@ -2315,7 +2296,7 @@ int pbft_replica_flush_poll(pbft_replica* r, pbft_round_event* events, uint32_t 
       // (a window's segments stay in order: a prefix of the batch)
       const size_t G = r->segs.size();
       // (at least 2^16 more rows in since the last application: the pool wakes for a chunk, not per poll)
-      if (!r->adopted && r->seg_next < G && rows_done >= r->applied_upto + (1u << 16)) {
+      if ((!r->adopted || r->adopt_partial) && r->seg_next < G && rows_done >= r->applied_upto + (1u << 16)) {
         RTRACE(r, "landed", rows_done);
         size_t s1 = r->seg_next;
         while (s1 < G && r->segs[s1].row_end <= rows_done) ++s1;

@@ -19,6 +19,8 @@ for s in $STEPS; do
     threads) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 36 --flush-ab PBFT_REPLICA_THREADS=16,15,12,8 > $D/threads.json 2> $D/threads.err ;;
     hostbw) timeout -k 10 120 tools/microbench/host_bw > $D/host_bw.txt 2>&1 ;;
     tail) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 > $D/tail.json 2> $D/tail.err ;;
+    tasksab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_PUSH_TASKS=1,8,4,16 > $D/tasksab.json 2> $D/tasksab.err ;;
+    partialab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_ADOPT_PARTIAL=0,1 > $D/partialab.json 2> $D/partialab.err ;;
     pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;
   esac
