@@ -236,7 +236,8 @@ class WorkerPool {
       new (&cv_) std::condition_variable();
       new (&done_) std::condition_variable();
       gen_ = 0;
-      active_ = pending_ = 0;
+      active_ = pending_ = running_ = 0;
+      closed_ = false;
       pid_ = getpid();
     }
     job_mu_.lock();
@@ -249,6 +250,8 @@ class WorkerPool {
       job_ = std::move(f);
       active_ = T;
       pending_ = T;
+      running_ = 0;
+      closed_ = false;
       ++gen_;
     }
     cv_.notify_all();
@@ -264,6 +267,26 @@ class WorkerPool {
     start(T, std::move(f));
     wait();
   }
+  // Retire the job once the caller's own counters say all of its work is done: workers that have not started it by
+  // then skip it, and only those still inside it are waited for -- a worker the host deschedules for milliseconds
+  // (r06: up to 10 ms on the GPU boxes, push_rows_start_max_ns) no longer holds up the join (instead of wait()).
+  void close() {
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      closed_ = true;
+      done_.wait(lk, [&] { return running_ == 0; });
+    }
+    job_mu_.unlock();
+  }
+  // f(0) .. f(T - 1) on the workers and f(T) on the calling thread; done() (the job's own counter of finished items,
+  // which the f's take dynamically) ends it, then close()
+  template <class Done>
+  void run_with_caller(size_t T, const std::function<void(size_t)>& f, Done done) {
+    start(T, f);
+    f(T);
+    while (!done()) cpu_relax();
+    close();
+  }
 
  private:
   void loop(size_t id) {
@@ -273,10 +296,16 @@ class WorkerPool {
         std::unique_lock<std::mutex> lk(mu_);
         cv_.wait(lk, [&] { return gen_ != seen && id < active_; });
         seen = gen_;
+        if (closed_) {  // retired before this worker got to it
+          if (--pending_ == 0) done_.notify_all();
+          continue;
+        }
+        ++running_;
       }
       job_(id);
       std::lock_guard<std::mutex> lk(mu_);
-      if (--pending_ == 0) done_.notify_all();
+      --running_;
+      if (--pending_ == 0 || (closed_ && running_ == 0)) done_.notify_all();
     }
   }
   std::vector<std::thread> th_;
@@ -284,7 +313,8 @@ class WorkerPool {
   std::condition_variable cv_, done_;
   std::function<void(size_t)> job_;
   uint64_t gen_ = 0;
-  size_t active_ = 0, pending_ = 0;
+  size_t active_ = 0, pending_ = 0, running_ = 0;
+  bool closed_ = false;
   pid_t pid_ = getpid();  // the process whose threads th_ holds
 };
 
@@ -1019,28 +1049,34 @@ static size_t host_threads() {
 }
 
 // Apply segments [s0, s1) of the batch (rows all verified); large ranges on several threads, cut at window
-// boundaries (balanced by rows).
+// boundaries (balanced by rows) into 4 pieces per thread that the threads -- the calling one too -- take as they
+// free up (events kept in piece order).
 static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
   if (s1 <= s0) return;
   const uint64_t lo = r->segs[s0].row0, nrows = r->segs[s1 - 1].row0 + r->segs[s1 - 1].count - lo;
   const unsigned hw = std::thread::hardware_concurrency();
   const size_t T = nrows >= (1u << 16) ? std::min<size_t>(std::min<size_t>(hw ? hw : 1, host_threads()), s1 - s0) : 1;
-  std::vector<std::array<uint64_t, 3>> st(T, {0, 0, 0});
-  std::vector<std::vector<pbft_round_event>> ev(T);
+  const size_t C = T <= 1 ? 1 : std::min<size_t>(4 * T, s1 - s0);
+  std::vector<std::array<uint64_t, 3>> st(C, {0, 0, 0});
+  std::vector<std::vector<pbft_round_event>> ev(C);
   if (T <= 1) {
     apply_range(r, s0, s1, st[0].data(), r->touched.data(), ev[0]);
   } else {
-    std::vector<size_t> cut(T + 1, s1);
+    std::vector<size_t> cut(C + 1, s1);
     cut[0] = s0;
-    for (size_t t = 0; t < T && cut[t] < s1; ++t) {
-      const uint64_t hi_row = lo + nrows * (t + 1) / T;
+    for (size_t t = 0; t < C && cut[t] < s1; ++t) {
+      const uint64_t hi_row = lo + nrows * (t + 1) / C;
       size_t b = cut[t] + 1;
-      while (b < s1 && (t + 1 == T || r->segs[b].row0 < hi_row || r->segs[b].key == r->segs[b - 1].key)) ++b;
+      while (b < s1 && (t + 1 == C || r->segs[b].row0 < hi_row || r->segs[b].key == r->segs[b - 1].key)) ++b;
       cut[t + 1] = b;
     }
-    WorkerPool::get().run(T, [&](size_t t) {
-      if (cut[t + 1] > cut[t]) apply_range(r, cut[t], cut[t + 1], st[t].data(), r->touched.data(), ev[t]);
-    });
+    std::atomic<size_t> next{0}, done{0};
+    WorkerPool::get().run_with_caller(T - 1, [&](size_t) {
+      for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < C;) {
+        if (cut[c + 1] > cut[c]) apply_range(r, cut[c], cut[c + 1], st[c].data(), r->touched.data(), ev[c]);
+        done.fetch_add(1, std::memory_order_release);
+      }
+    }, [&] { return done.load(std::memory_order_acquire) == C; });
   }
   for (const auto& e : ev) r->evq.insert(r->evq.end(), e.begin(), e.end());
   for (const auto& c : st) {
@@ -1723,9 +1759,10 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     std::vector<std::vector<Run>> slice_runs(C);
     std::vector<uint8_t> bad(n_ok);
     std::vector<PushCounts> cnt(T);
-    std::atomic<size_t> next_chunk{0};
+    std::atomic<size_t> next_chunk{0}, chunks_done{0};
     std::vector<uint64_t> t_done(T, 0);
-    WorkerPool::get().run(T, [&](size_t t) {
+    // (T - 1 workers and this thread; a worker that has not started when the last chunk is done is not waited for)
+    WorkerPool::get().run_with_caller(T - 1, [&](size_t t) {
       for (size_t ch; (ch = next_chunk.fetch_add(1, std::memory_order_relaxed)) < C;) {
         const uint64_t lo = n_ok * ch / C, hi = n_ok * (ch + 1) / C;
         std::vector<Run>& runs = slice_runs[ch];
@@ -1754,9 +1791,10 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         cnt[t].pushed += hi - lo;
         cnt[t].rejected_view += rv;
         cnt[t].rejected_watermark += rw;
+        chunks_done.fetch_add(1, std::memory_order_release);
       }
       t_done[t] = now_ns();
-    });
+    }, [&] { return chunks_done.load(std::memory_order_acquire) == C; });
     //  2. (this thread) the windows of the runs -- created here, the only window insertions -- grouped into G tasks
     //     (r06: PBFT_PUSH_TASKS per thread, default 8) by the input position of each window's first run; a task
     //     holds every run of its windows, in input order (per-window order is all the state machine depends on), and
@@ -1849,7 +1887,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     }
     std::unique_ptr<std::atomic<uint32_t>[]> g_done(new std::atomic<uint32_t>[G]);
     for (size_t g = 0; g < G; ++g) g_done[g].store(0, std::memory_order_relaxed);
-    std::atomic<size_t> next_task{0};
+    std::atomic<size_t> next_task{0}, tasks_done{0};
     std::vector<int64_t> added(T, 0);
     RTRACE(r, "push_windows", runs.size());
     const uint64_t tp2 = now_ns();
@@ -1858,7 +1896,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //     envelopes copies of envelope 0
     static const uint8_t zero_sig[64] = {0};
     std::vector<uint64_t> t_beg(T, 0), t_end(T, 0);
-    WorkerPool::get().start(T, [&](size_t t) {
+    const std::function<void(size_t)> work = [&](size_t t) {
       t_beg[t] = now_ns();
       // (thread-local copies: the threads' entries of cnt share cache lines, and every row updates them)
       PushCounts c = cnt[t];
@@ -1880,13 +1918,17 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
           stream_fence();  // (streaming stores are weakly ordered: visible before the task is marked done)
           g_done[g].store(1, std::memory_order_release);
         }
+        tasks_done.fetch_add(1, std::memory_order_acq_rel);
       }
       if (g_stream_stores) stream_fence();  // (drained before the join)
       cnt[t] = c;
       added[t] = add;
       t_end[t] = now_ns();
-    });
-    if (early) {
+    };
+    if (!early) {  // (T - 1 workers and this thread)
+      WorkerPool::get().run_with_caller(T - 1, work, [&] { return tasks_done.load(std::memory_order_acquire) == G; });
+    } else {  // (T workers; this thread launches the pieces)
+      WorkerPool::get().start(T, work);
       // launch each context's finished prefix of tasks once it holds ~1/P of the rows (or the context is complete)
       const uint64_t step = std::max<uint64_t>(64, (g_row0[G] - A.n) / P);
       size_t done = 0, j = 0;
@@ -1913,8 +1955,8 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         if (G - done > T) std::this_thread::sleep_for(std::chrono::microseconds(20));
         else for (int s = 0; s < 64; ++s) cpu_relax();
       }
+      WorkerPool::get().close();  // (j == K: every task is done)
     }
-    WorkerPool::get().wait();
     A.n = g_row0[G];
     A.ne = (uint32_t)g_env0[G];
     if (early) {
@@ -1944,9 +1986,15 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     r->tm.push_checks_ns = tp1 - tp0;
     r->tm.push_windows_ns = tp2 - tp1;
     r->tm.push_rows_ns = now_ns() - tp2;
-    r->tm.push_checks_end_min_ns = *std::min_element(t_done.begin(), t_done.end()) - tp0;
+    // (workers retired before they started left 0: not counted)
+    auto min_set = [](const std::vector<uint64_t>& v, uint64_t t0) {
+      uint64_t m = ~0ull;
+      for (uint64_t x : v) if (x && x < m) m = x;
+      return m == ~0ull ? 0 : m - t0;
+    };
+    r->tm.push_checks_end_min_ns = min_set(t_done, tp0);
     r->tm.push_rows_start_max_ns = *std::max_element(t_beg.begin(), t_beg.end()) - tp2;
-    r->tm.push_rows_end_min_ns = *std::min_element(t_end.begin(), t_end.end()) - tp2;
+    r->tm.push_rows_end_min_ns = min_set(t_end, tp2);
     if (g_push_trace && r->trace.size() >= 4) {  // PBFT_PUSH_TRACE (with PBFT_REPLICA_TRACE): pass times of this call
       auto at = [&](const char* what) {
         for (size_t x = r->trace.size(); x-- > 0;)
