@@ -223,15 +223,18 @@ int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq
 /* N pushes in one call (kind[i], view[i], seq[i], digests[i][64], signer[i], sigs[i][64]); *queued = how many
  * were queued.  Returns 0 or the first negative code.
  * Every queued vote's 72-byte staged row (PBFT_VOTES_ROW_BYTES) goes into the replica's pinned row arena as it is
- * pushed (r05).  With GPU contexts, no override verifier, no batch in flight and >= 2^17 rows, push_many also starts
- * verifying the arena while it pushes ("early batch": 8 parts launched through pbft_verify_votes_open / _piece /
- * _close, the parts spread over the contexts); the next flush_submit adopts that batch when the arena is unchanged
- * since, and otherwise finishes it and verifies the arena again -- so the contexts are busy between push_many and the
- * flush, and a digest on the context (on_pre_prepare without a digest override), a key update or a verifier change
- * in between waits for the early batch first.  Environment (read per call, for A/B runs): PBFT_REPLICA_EARLY=0 (no
- * early batch), PBFT_EARLY_PARTS (parts, default 8), PBFT_REPLICA_DIRECT=0 (flush_submit fills the context's
- * staging instead of handing the arena over), PBFT_APPLY_PREFETCH=0; read once: PBFT_REPLICA_THREADS (worker
- * threads, default 16), PBFT_STREAM_STORES=0 (plain stores for the rows). */
+ * pushed (r05), by tasks of consecutive windows that the worker threads take as they free up (r06).  With GPU
+ * contexts, no override verifier, no batch in flight and >= 2^17 rows, push_many also starts verifying the arena
+ * while it pushes ("early batch": pieces of 2^17 rows launched through pbft_verify_votes_open / _piece / _close as
+ * soon as the tasks below their ends are done, each context taking a contiguous run of tasks); the next flush_submit
+ * adopts that batch when the arena is unchanged since (and flush_poll applies its windows as its pieces land), and
+ * otherwise finishes it and verifies the arena again -- so the contexts are busy between push_many and the flush,
+ * and a key update or a verifier change in between waits for the early batch first.  Environment (read per call,
+ * for A/B runs): PBFT_REPLICA_EARLY=0 (no early batch), PBFT_MANY_PIECE (rows per piece, default 2^17),
+ * PBFT_PUSH_TASKS (tasks per thread, default 8), PBFT_ADOPT_PARTIAL=0 (an adopted batch applied once, when done),
+ * PBFT_REPLICA_DIRECT=0 (flush_submit fills the context's staging instead of handing the arena over),
+ * PBFT_APPLY_PREFETCH=0, PBFT_REPLICA_THREADS (worker threads, default 16); read once: PBFT_STREAM_STORES=0 (plain
+ * stores for the rows). */
 int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, const uint64_t *view, const uint64_t *seq,
                            const uint8_t *digests, const uint32_t *signer, const uint8_t *sigs, uint64_t *queued);
 

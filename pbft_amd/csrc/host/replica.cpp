@@ -1720,6 +1720,12 @@ int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq
 
 // push_many of at least this many rows runs on the worker pool (PBFT_REPLICA_THREADS threads)
 static constexpr uint64_t PUSH_PAR_MIN = 1u << 14;
+// push_many's early-batch pieces: rows per piece (PBFT_MANY_PIECE, 2^12..2^22, default 2^17; read per call)
+static uint64_t many_piece_rows() {
+  const char* e = getenv("PBFT_MANY_PIECE");
+  const long long v = e ? strtoll(e, nullptr, 10) : (1 << 17);
+  return (uint64_t)(v < 4096 ? 4096 : v > (1 << 22) ? (1 << 22) : v) & ~(uint64_t)63;
+}
 // push_many's tasks per worker thread (PBFT_PUSH_TASKS, 1..64, default 8; read per call)
 static size_t push_tasks_per_thread() {
   const char* e = getenv("PBFT_PUSH_TASKS");
@@ -1832,15 +1838,10 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     uint64_t rows_all = 0;
     for (size_t g = 0; g < G; ++g) rows_all += g_rows[g];
     // Early batch (r05): with GPU contexts, no batch in flight and a large call, the arena range of this call is
-    // launched in pieces while the threads push -- each piece a prefix of finished tasks (every task's range starts
-    // 64-aligned: bitmap words), about 1/P of the rows (PBFT_EARLY_PARTS, 2..32, default 8, read per call: A/B in one
-    // process) -- so the copies and kernels of the round run under push_many instead of after flush_submit.  Rows
-    // of rejected pushes and each task's padding are rows no candidate references.
-    const size_t P = [] {
-      const char* e = getenv("PBFT_EARLY_PARTS");
-      const long v = e ? strtol(e, nullptr, 10) : 8;
-      return (size_t)(v < 2 ? 2 : v > 32 ? 32 : v);
-    }();
+    // launched in pieces while the threads push (each piece's rows all written: every task below its end done;
+    // every task's range starts 64-aligned, so the pieces' bitmap words are their own), so that the copies and
+    // kernels of the round run under push_many instead of after flush_submit.  Rows of rejected pushes and each
+    // task's padding are rows no candidate references.
     const bool early = early_enabled() && direct_enabled() && r->ctx && !r->verify_fn && !r->vsub &&
                        !r->in_flight && !r->eu.active && A.rows_pinned && A.envs_pinned &&
                        A.clean.load(std::memory_order_relaxed) && rows_all >= (1u << 17);
@@ -1929,25 +1930,34 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       WorkerPool::get().run_with_caller(T - 1, work, [&] { return tasks_done.load(std::memory_order_acquire) == G; });
     } else {  // (T workers; this thread launches the pieces)
       WorkerPool::get().start(T, work);
-      // launch each context's finished prefix of tasks once it holds ~1/P of the rows (or the context is complete)
-      const uint64_t step = std::max<uint64_t>(64, (g_row0[G] - A.n) / P);
+      // launch context j's rows in pieces of exactly `piece` rows (2^17 by default: a whole wave generation of the
+      // comb at 2 waves per SIMD, as efficient per row as a 2^20 launch -- r06 trace: pieces of ~1/8 of the rows at
+      // arbitrary sizes ran comb + finish 20-40 % slower) as soon as every task below the piece's end is done, the
+      // rest once the context's last task is; each piece carries the envelopes of every task done so far
+      const uint64_t piece = many_piece_rows();
       size_t done = 0, j = 0;
       uint64_t plo = 0;   // the context's next piece starts here (absolute row)
       uint32_t elo = 0;   // ... and its new envelopes here
+      auto launch = [&](uint64_t hi, uint32_t ehi) {
+        if (launched && hi > plo)
+          launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], plo - ctx_lo[j], hi - ctx_lo[j],
+                                             A.envs, elo, ehi) == PBFT_OK;
+        plo = hi;
+        elo = ehi;
+      };
       while (j < K) {
         while (done < G && g_done[done].load(std::memory_order_acquire)) ++done;
         const size_t end = std::min(done, tb[j + 1]);
-        if (end == tb[j + 1] || (end > tb[j] && g_row0[end] - plo >= step)) {
-          if (launched && g_row0[end] > plo)
-            launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], plo - ctx_lo[j],
-                                               g_row0[end] - ctx_lo[j], A.envs, elo, (uint32_t)g_env0[end]) == PBFT_OK;
-          plo = g_row0[end];
-          elo = (uint32_t)g_env0[end];
-          if (end == tb[j + 1]) {
-            if (launched) launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
-            ++j;
-            elo = 0;
-          }
+        if (end == tb[j + 1]) {  // the context's rows are all written
+          while (plo + piece < ctx_lo[j + 1]) launch(plo + piece, (uint32_t)g_env0[end]);
+          launch(ctx_lo[j + 1], (uint32_t)g_env0[end]);
+          if (launched) launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
+          ++j;
+          elo = 0;
+          continue;
+        }
+        if (g_row0[end] >= plo + piece) {
+          launch(plo + piece, (uint32_t)g_env0[end]);
           continue;
         }
         // (sleeping, not spinning, while most tasks are left: the T workers have the host's cores; the last ones
