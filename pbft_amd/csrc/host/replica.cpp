@@ -1932,12 +1932,18 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
       WorkerPool::get().start(T, work);
       // launch context j's rows in pieces of exactly `piece` rows (2^17 by default: a whole wave generation of the
       // comb at 2 waves per SIMD, as efficient per row as a 2^20 launch -- r06 trace: pieces of ~1/8 of the rows at
-      // arbitrary sizes ran comb + finish 20-40 % slower) as soon as every task below the piece's end is done, the
-      // rest once the context's last task is; each piece carries the envelopes of every task done so far
+      // arbitrary sizes ran comb + finish 20-40 % slower), each as soon as every task below its end is done and
+      // carrying the envelopes of every task done so far; the context's odd rows go FIRST, as a short piece (at the
+      // end, a short piece's latency-form kernels ran beside the last full one and finished after it)
       const uint64_t piece = many_piece_rows();
+      auto first_end = [&](size_t jj) {
+        const uint64_t span = ctx_lo[jj + 1] - ctx_lo[jj];
+        return ctx_lo[jj] + (span % piece ? span % piece : std::min(piece, span));
+      };
       size_t done = 0, j = 0;
       uint64_t plo = 0;   // the context's next piece starts here (absolute row)
-      uint32_t elo = 0;   // ... and its new envelopes here
+      uint64_t pend = K ? first_end(0) : 0;  // ... and ends here
+      uint32_t elo = 0;   // ... and its new envelopes start here
       auto launch = [&](uint64_t hi, uint32_t ehi) {
         if (launched && hi > plo)
           launched = pbft_verify_votes_piece(r->ctxs[j], A.rows + ROWB * ctx_lo[j], plo - ctx_lo[j], hi - ctx_lo[j],
@@ -1949,15 +1955,20 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
         while (done < G && g_done[done].load(std::memory_order_acquire)) ++done;
         const size_t end = std::min(done, tb[j + 1]);
         if (end == tb[j + 1]) {  // the context's rows are all written
-          while (plo + piece < ctx_lo[j + 1]) launch(plo + piece, (uint32_t)g_env0[end]);
-          launch(ctx_lo[j + 1], (uint32_t)g_env0[end]);
+          while (plo < ctx_lo[j + 1]) {
+            const uint64_t hi = std::min(ctx_lo[j + 1], pend);
+            launch(hi, (uint32_t)g_env0[end]);
+            pend = hi + piece;
+          }
           if (launched) launched = pbft_verify_votes_close(r->ctxs[j], ctx_lo[j + 1] - ctx_lo[j]) == PBFT_OK;
           ++j;
           elo = 0;
+          if (j < K) pend = first_end(j);
           continue;
         }
-        if (g_row0[end] >= plo + piece) {
-          launch(plo + piece, (uint32_t)g_env0[end]);
+        if (pend < ctx_lo[j + 1] && g_row0[end] >= pend) {
+          launch(pend, (uint32_t)g_env0[end]);
+          pend += piece;
           continue;
         }
         // (sleeping, not spinning, while most tasks are left: the T workers have the host's cores; the last ones
