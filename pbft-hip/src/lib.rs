@@ -575,6 +575,22 @@ impl<'a> Replica<'a> {
         })?;
         Ok(used as usize)
     }
+    /// 160-byte binary records (pbft_wire.h PBFT_RECORD_BYTES) read from peer `peer_idx`'s connection;
+    /// returns (bytes consumed, votes pushed, records dropped) -- keep the unconsumed tail for the next read.
+    pub fn push_records(&mut self, peer_idx: u32, stream: &[u8]) -> Result<(usize, u64, u64)> {
+        let (mut used, mut pushed, mut dropped) = (0u64, 0u64, 0u64);
+        check(unsafe {
+            ffi::pbft_replica_push_records(self.raw, peer_idx, stream.as_ptr(), stream.len(), &mut used,
+                                           &mut pushed, &mut dropped)
+        })?;
+        Ok((used as usize, pushed, dropped))
+    }
+    /// Where the last push_many and the last flush spent their time (host clock, ns).
+    pub fn timings(&self) -> Result<ffi::pbft_replica_timings> {
+        let mut t = ffi::pbft_replica_timings::default();
+        check(unsafe { ffi::pbft_replica_get_timings(self.raw, &mut t) })?;
+        Ok(t)
+    }
     /// Launch one batch of every ready sub-window (force = the deadline: everything pending) without
     /// waiting for it; returns its signatures (0: nothing launched).  Err(PBFT_EBUSY) while one is in flight.
     pub fn flush_submit(&mut self, force: bool) -> Result<u64> {

@@ -32,7 +32,6 @@
 #include <mutex>
 #include <thread>
 #include <unistd.h>
-#include <sched.h>
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -245,7 +244,6 @@ class WorkerPool {
     while (th_.size() < T) {
       const size_t id = th_.size();
       th_.emplace_back([this, id] { loop(id); });
-      pin(th_.back(), id);
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -308,28 +306,6 @@ class WorkerPool {
       std::lock_guard<std::mutex> lk(mu_);
       --running_;
       if (--pending_ == 0 || (closed_ && running_ == 0)) done_.notify_all();
-    }
-  }
-  // PBFT_PIN_WORKERS=1 (read when a worker starts; an A/B of the r06 tail rounds): worker id on its own CPU, the
-  // (id + 1)-th allowed CPU after the one the creating thread runs on, within its block of 64 (one socket's cores)
-  static void pin(std::thread& t, size_t id) {
-    const char* e = getenv("PBFT_PIN_WORKERS");
-    if (!e || atoi(e) == 0) return;
-    cpu_set_t allowed;
-    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
-    const int here = sched_getcpu();
-    if (here < 0) return;
-    const int block = here & ~63;
-    for (int k = 1, seen = 0; k < 64; ++k) {
-      const int cpu = block + ((here - block + k) & 63);
-      if (!CPU_ISSET(cpu, &allowed)) continue;
-      if ((size_t)seen++ == id) {
-        cpu_set_t one;
-        CPU_ZERO(&one);
-        CPU_SET(cpu, &one);
-        (void)pthread_setaffinity_np(t.native_handle(), sizeof one, &one);
-        return;
-      }
     }
   }
   std::vector<std::thread> th_;
