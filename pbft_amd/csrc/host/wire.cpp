@@ -76,9 +76,17 @@ void write_client_request(Out& o, const pbft_wire_msg* m) {
 }
 
 // ------------------------------------------------------------------ parser
+// (r06: the frames are ASCII but for an operation's text -- 8 bytes per step while no byte has its top bit set)
+static inline uint64_t load8(const void* p) {
+  uint64_t w;
+  memcpy(&w, p, 8);
+  return w;
+}
 bool utf8_valid(const unsigned char* s, size_t n) {
   size_t i = 0;
   while (i < n) {
+    while (n - i >= 8 && !(load8(s + i) & 0x8080808080808080ull)) i += 8;
+    if (i >= n) break;
     const unsigned char c = s[i];
     if (c < 0x80) { ++i; continue; }
     int k;
@@ -143,12 +151,53 @@ struct Parser {
     *v = x;
     return true;
   }
+  // The bytes of a string up to its closing quote when it has no escape or control character: 8 per step (SWAR:
+  // a byte equal to '"' or '\\', or below 0x20, stops the word loop), then byte by byte; q = where it stopped.
+  static inline bool special8(uint64_t w) {
+    constexpr uint64_t ones = 0x0101010101010101ull, high = 0x8080808080808080ull;
+    const uint64_t quote = w ^ (ones * '"'), bslash = w ^ (ones * '\\');
+    return (((quote - ones) & ~quote) | ((bslash - ones) & ~bslash) | ((w - ones * 0x20) & ~w)) & high;
+  }
+  const char* plain_end(const char* q) const {
+    while (e - q >= 8 && !special8(load8(q))) q += 8;
+    while (q < e && *q != '"' && *q != '\\' && (unsigned char)*q >= 0x20) ++q;
+    return q;
+  }
+  // A string in place (no copy) when it has no escape -- the keys, the hex digest and signature; else unescaped into
+  // the arena (the caller restores `used` after reading it).
+  bool view(const char** s, size_t* n) {
+    ws();
+    if (p >= e || *p != '"') return false;
+    const char* q = plain_end(p + 1);
+    if (q < e && *q == '"') {
+      *s = p + 1;
+      *n = (size_t)(q - p - 1);
+      p = q + 1;
+      return true;
+    }
+    return str(s, n, true);
+  }
   // string -> arena (store=true) or validated and skipped; *s/*n describe the unescaped bytes
   bool str(const char** s, size_t* n, bool store) {
     ws();
     if (p >= e || *p != '"') return false;
     ++p;
     const size_t start = used;
+    {  // the common case: no escape -- one copy
+      const char* q = plain_end(p);
+      if (q < e && *q == '"') {
+        const size_t k = (size_t)(q - p);
+        if (store) {
+          if (!arena || cap - used < k) return false;
+          memcpy(arena + used, p, k);
+          used += k;
+        }
+        p = q + 1;
+        if (s) *s = store ? arena + start : nullptr;
+        if (n) *n = k;
+        return true;
+      }
+    }
     while (true) {
       if (p >= e) return false;
       const unsigned char c = (unsigned char)*p++;
@@ -194,11 +243,11 @@ struct Parser {
   }
   char kbuf[64];
   bool key(const char** s, size_t* n) {
-    // keys are short: unescape into a private buffer (the caller compares immediately)
+    // keys are short: in place, or (escaped) unescaped into a private buffer (the caller compares immediately)
     char* a = arena;
     const size_t c = cap, u = used;
     arena = kbuf; cap = sizeof kbuf; used = 0;
-    const bool ok = str(s, n, true);
+    const bool ok = view(s, n);
     arena = a; cap = c; used = u;
     return ok && lit(':');
   }
@@ -253,20 +302,44 @@ struct Parser {
 
 bool eq(const char* s, size_t n, const char* lit_) { return strlen(lit_) == n && memcmp(s, lit_, n) == 0; }
 
+// lowercase hex digit values (format!("{:x}") is lowercase), 0xFF for anything else
+struct HexTable {
+  uint8_t v[256];
+  constexpr HexTable() : v() {
+    for (int c = 0; c < 256; ++c) v[c] = 0xFF;
+    for (int c = '0'; c <= '9'; ++c) v[c] = (uint8_t)(c - '0');
+    for (int c = 'a'; c <= 'f'; ++c) v[c] = (uint8_t)(c - 'a' + 10);
+  }
+};
+constexpr HexTable HEX_VAL{};
+// 8 lowercase hex characters -> 4 bytes, SWAR; false if any is not one of 0-9a-f.  Per character: value = low
+// nibble + 9 if bit 6 is set (letters); valid iff the value is < 16 and maps back to exactly that character.
+static inline bool hex8(const char* s, uint8_t out[4]) {
+  constexpr uint64_t ones = 0x0101010101010101ull, high = 0x8080808080808080ull;
+  const uint64_t w = load8(s);
+  const uint64_t val = (w & (ones * 0x0F)) + ((w >> 6) & ones) * 9;
+  const uint64_t gt9 = ((val + ones * 0x76) & high) >> 7;
+  const uint64_t recon = val + ones * 0x30 + gt9 * 0x27;
+  if (recon != w || ((val + ones * 0x70) & high)) return false;
+  uint64_t x = ((val & 0x00FF00FF00FF00FFull) << 4) | ((val >> 8) & 0x00FF00FF00FF00FFull);
+  x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
+  x = (x | (x >> 16)) & 0xFFFFFFFFull;
+  const uint32_t v = (uint32_t)x;
+  memcpy(out, &v, 4);
+  return true;
+}
 bool parse_hex(const char* s, size_t n, uint8_t* out, size_t nbytes) {
   if (n != 2 * nbytes) return false;
-  for (size_t i = 0; i < nbytes; ++i) {
-    int v = 0;
-    for (int j = 0; j < 2; ++j) {
-      const char c = s[2 * i + j];
-      v <<= 4;
-      if (c >= '0' && c <= '9') v |= c - '0';
-      else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
-      else return false;  // format!("{:x}") is lowercase
-    }
-    out[i] = (uint8_t)v;
+  size_t i = 0;
+  for (; i + 4 <= nbytes; i += 4)
+    if (!hex8(s + 2 * i, out + i)) return false;
+  uint8_t bad = 0;
+  for (; i < nbytes; ++i) {
+    const uint8_t hi = HEX_VAL.v[(uint8_t)s[2 * i]], lo = HEX_VAL.v[(uint8_t)s[2 * i + 1]];
+    bad |= (uint8_t)(hi | lo);
+    out[i] = (uint8_t)(hi << 4 | (lo & 15));
   }
-  return true;
+  return !(bad & 0x80);  // (every valid digit is < 16: an invalid one sets the top bit)
 }
 
 bool parse_client_request(Parser& P, pbft_wire_msg* m) {
@@ -327,7 +400,7 @@ bool parse_body(Parser& P, uint32_t kind, pbft_wire_msg* m) {
         const size_t mark = P.used;
         const char* s;
         size_t n;
-        if (!P.str(&s, &n, true)) return false;
+        if (!P.view(&s, &n)) return false;
         m->digest_ok = parse_hex(s, n, m->digest, 64) ? 1u : 0u;
         P.used = mark;
         has_d = true;
@@ -344,7 +417,7 @@ bool parse_body(Parser& P, uint32_t kind, pbft_wire_msg* m) {
         const size_t mark = P.used;
         const char* s;
         size_t n;
-        if (!P.str(&s, &n, true) || !parse_hex(s, n, m->sig, 64)) return false;
+        if (!P.view(&s, &n) || !parse_hex(s, n, m->sig, 64)) return false;
         P.used = mark;
         has_s = true;
       } else if (!P.skip_value()) {

@@ -99,6 +99,24 @@ def test_decoder_accepts_what_serde_accepts():
     assert wire.decode_json(up).digest_ok is False
 
 
+def test_decoder_fast_paths_match_the_escaped_forms():
+    """r06: strings without escapes are read in place (keys, hex digest / signature: 8 characters per step); an
+    escaped spelling of the same text must decode the same, and one wrong character anywhere must be caught."""
+    d = bytes(range(64)).hex()
+    plain = b'{"Commit":{"view":3,"sequence_number":7,"digest":"%s"}}' % d.encode()
+    # the same JSON text with the key and some digest characters written as \\u escapes
+    esc_d = "".join("\\u%04x" % ord(c) if i % 5 == 0 else c for i, c in enumerate(d))
+    escaped = b'{"Commit":{"vi\\u0065w":3,"sequence_number":7,"digest":"%s"}}' % esc_d.encode()
+    for js in (plain, escaped):
+        m = wire.decode_json(js)
+        assert (m.kind, m.view, m.seq, m.digest_ok, m.digest.hex()) == (COMMIT, 3, 7, True, d)
+    for pos in (0, 1, 7, 8, 63, 64, 120, 127):
+        for c in "gG/:`{AF\x7f":
+            bad_d = d[:pos] + c + d[pos + 1:]
+            js = b'{"Commit":{"view":3,"sequence_number":7,"digest":"%s"}}' % bad_d.encode()
+            assert wire.decode_json(js).digest_ok is False, (pos, c)
+
+
 @pytest.mark.parametrize("bad", [
     b'{"Prepare":{"view":1,"sequence_number":2}}',                                   # missing digest
     b'{"Prepare":{"view":1,"view":1,"sequence_number":2,"digest":""}}',              # duplicate field
