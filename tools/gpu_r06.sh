@@ -24,6 +24,7 @@ for s in $STEPS; do
     dppab) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_findpp.so --replicas 16 --seqs 32768 --sizes 131072 --rounds 24 --iters 20 > $D/dppab.txt 2>&1 ;;
     timeline) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $D/tl -o tl -- python3 tools/ingress_probe.py --skip-ingress-leg --rounds 4 > $D/timeline.out 2>&1 ;;
     pieceab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_MANY_PIECE=131072,262144 > $D/pieceab.json 2> $D/pieceab.err ;;
+    benchprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D/benchprof -o bench -- python3 bench.py > $D/benchprof.json 2> $D/benchprof.err && rm -f $D/benchprof/bench_kernel_trace.csv ;;
     pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;
   esac
