@@ -763,8 +763,8 @@ static void test_replica_progressive(uint32_t n_ctx, bool many) {
     early += x.early_batches;
   }
   // + the padding that 64-aligns each slice (staging fill), or push_many's unused rows (the arena as it is)
-  // (+ 64-row padding of each part of an early batch: 8 parts by default, at most 32)
-  CHECK(staged >= rows && staged < rows + 64 * n_ctx + dups + (early ? 32 * 64 : 0));
+  // (+ the padding that 64-aligns every push_many task of an early batch: at most 64 tasks per thread, 64 threads)
+  CHECK(staged >= rows && staged < rows + 64 * n_ctx + dups + (early ? 64 * 64 * 63 : 0));
   std::vector<pbft_round_event> ev(4 * seqs);
   uint32_t ne = 0;
   int polls = 0, st;
@@ -1034,6 +1034,21 @@ int main() {
   for (bool many : {false, true}) {
     test_replica_progressive(1, many);
     test_replica_progressive(3, many);
+  }
+  // r06: push_many's tasks and early pieces at their extremes -- one task per thread (pieces wait for whole thread
+  // ranges), 64 per thread; pieces of 4,096 rows (hundreds of pieces, the short one first) and the default
+  {
+    const char* tp = getenv("PBFT_PUSH_TASKS");
+    const char* pp = getenv("PBFT_MANY_PIECE");
+    const std::string keep_t = tp ? tp : "", keep_p = pp ? pp : "";
+    const char* combos[3][3] = {{"1", "4096", "3"}, {"64", "4096", "1"}, {"64", "131072", "3"}};
+    for (auto& c : combos) {
+      setenv("PBFT_PUSH_TASKS", c[0], 1);
+      setenv("PBFT_MANY_PIECE", c[1], 1);
+      test_replica_progressive((uint32_t)atoi(c[2]), true);
+    }
+    if (tp) setenv("PBFT_PUSH_TASKS", keep_t.c_str(), 1); else unsetenv("PBFT_PUSH_TASKS");
+    if (pp) setenv("PBFT_MANY_PIECE", keep_p.c_str(), 1); else unsetenv("PBFT_MANY_PIECE");
   }
   if (!(getenv("PBFT_REPLICA_DIRECT") && atoi(getenv("PBFT_REPLICA_DIRECT")) == 0)) {
     test_replica_early_dropped(0);

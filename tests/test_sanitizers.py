@@ -50,7 +50,7 @@ def test_host_code_clean_under_asan_ubsan(direct):
     assert "sanitized host run ok" in p.stdout
     assert "arithmetic: 120 accepted, 120 rejected" in p.stdout
     lines = [l for l in p.stdout.splitlines() if l.startswith("replica progressive")]
-    assert len(lines) == 4
+    assert len(lines) == 7  # 1 and 3 contexts x push / push_many, + push_many at 3 task / piece extremes (r06)
     for l in lines:  # every context's batch the arena itself (direct), or none of them; push_many on one context:
         # the early batch launched piecewise while pushing, then adopted by the flush
         n_ctx = int(l.split("(")[1].split()[0])
