@@ -474,6 +474,8 @@ def replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds: int = 9
             tot = [x for x, mm in zip(res["total_ms"], mode_of) if mm == m]
             by_mode[m]["total_ms_mean"] = float(np.mean(tot))
             by_mode[m]["total_ms_max"] = float(np.max(tot))
+            ph = [x for x, mm in zip(phases, mode_of) if mm == m]
+            by_mode[m]["phases_median"] = {k: float(np.median([x[k] for x in ph])) for k in ph[0]} if ph else {}
     return {"value": n / (med["total_ms"] * 1e-3), "unit": "verifies/s", "ms_per_round": med["total_ms"],
             **({"by_mode": by_mode} if by_mode else {}),
             "ms_per_round_min_max": [float(np.min(res["total_ms"])), float(np.max(res["total_ms"]))],

@@ -812,7 +812,11 @@ static size_t host_threads();
 // Chunks of a serial walk over the windows run on the pool (T - 1 workers and the calling thread) once there are
 // this many live windows (r06: the flush's segment walk and the GC each took 0.12-0.2 ms for a 2048-seq round,
 // every window's lines last written by the push_many and apply workers)
-static constexpr size_t PAR_WINDOWS = 1024;
+// (PBFT_PAR_WINDOWS overrides it, read per call: an A/B in one process)
+static size_t par_windows() {
+  const char* e = getenv("PBFT_PAR_WINDOWS");
+  return e ? (size_t)strtoull(e, nullptr, 10) : 1024;
+}
 template <class F>
 static void par_chunks(size_t C, F&& f) {
   std::atomic<size_t> next{0}, done{0};
@@ -829,7 +833,7 @@ static void gc(pbft_replica* r) {
   r->last_w = nullptr;  // windows may go away
   // committed prefix: h advances over consecutive committed windows (ring slot h + 1, h + 2, ...)
   const uint64_t h0 = r->h;
-  if (r->n_windows >= PAR_WINDOWS && r->win_hi > r->h) {
+  if (r->n_windows >= par_windows() && r->win_hi > r->h) {
     // many windows: the first seq that is not a committed window, chunk by chunk on the pool; then the committed
     // prefix is dropped chunk by chunk (each chunk's ring slots are its own; the free list and counts merged after)
     const uint64_t lo = r->h + 1, span = std::min<uint64_t>(r->win_hi - r->h, r->ring.size());
@@ -856,13 +860,15 @@ static void gc(pbft_replica* r) {
       std::vector<std::vector<Window*>> freed(D);
       if (r->in_flight) r->erased_in_flight = true;
       par_chunks(D, [&](size_t c) {
+        std::vector<Window*> f;  // (local: the chunks' vectors share cache lines)
         for (uint64_t q = lo + cnt * c / D, e = lo + cnt * (c + 1) / D; q < e; ++q) {
           Window* w = r->ring[q & r->ring_mask];
           release_window(r, *w);
           r->ring[q & r->ring_mask] = nullptr;
           w->seq = 0;
-          freed[c].push_back(w);
+          f.push_back(w);
         }
+        freed[c] = std::move(f);
       });
       for (auto& v : freed) r->win_free.insert(r->win_free.end(), v.begin(), v.end());
       r->n_windows -= cnt;
@@ -1131,7 +1137,11 @@ static void apply_segs(pbft_replica* r, size_t s0, size_t s1) {
     std::atomic<size_t> next{0}, done{0};
     WorkerPool::get().run_with_caller(T - 1, [&](size_t) {
       for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < C;) {
-        if (cut[c + 1] > cut[c]) apply_range(r, cut[c], cut[c + 1], st[c].data(), r->touched.data(), ev[c]);
+        if (cut[c + 1] > cut[c]) {
+          std::vector<pbft_round_event> e;  // (local: the pieces' vectors share cache lines)
+          apply_range(r, cut[c], cut[c + 1], st[c].data(), r->touched.data(), e);
+          ev[c] = std::move(e);
+        }
         done.fetch_add(1, std::memory_order_release);
       }
     }, [&] { return done.load(std::memory_order_acquire) == C; });
@@ -1829,7 +1839,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     WorkerPool::get().run_with_caller(T - 1, [&](size_t t) {
       for (size_t ch; (ch = next_chunk.fetch_add(1, std::memory_order_relaxed)) < C;) {
         const uint64_t lo = n_ok * ch / C, hi = n_ok * (ch + 1) / C;
-        std::vector<Run>& runs = slice_runs[ch];
+        std::vector<Run> runs;  // (local, stored once: the chunks' vectors share cache lines)
         // (locals: the byte stores below may alias anything, which would reload every field per row)
         const uint32_t n = r->n;
         const uint64_t cur = r->current_view, h = r->h, win = r->log_window;
@@ -1852,6 +1862,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
           ++run_good;
         }
         if (run_seq != ~0ull) runs.push_back({run_lo, hi, run_seq, nullptr, 0, run_good, false});
+        slice_runs[ch] = std::move(runs);
         cnt[t].pushed += hi - lo;
         cnt[t].rejected_view += rv;
         cnt[t].rejected_watermark += rw;
@@ -2107,7 +2118,7 @@ static void mark_arena_segs(pbft_replica* r) {
     }
   };
   const size_t S = r->segs.size();
-  if (S < 3 * PAR_WINDOWS) {
+  if (S < 3 * par_windows()) {
     mark(0, S);
   } else {
     const size_t C = std::min<size_t>(4 * host_threads(), (S + 511) / 512);
@@ -2260,14 +2271,23 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   };
   if (r->n_windows && r->win_hi > r->h) {
     const uint64_t lo = r->h + 1, span = r->win_hi - r->h;
-    if (r->n_windows < PAR_WINDOWS) {
+    if (r->n_windows < par_windows()) {
       walk(lo, lo + span, r->segs, N, E);
     } else {  // (chunks on the pool, then renumbered in order)
       const size_t C = std::min<size_t>(4 * host_threads(), (size_t)((span + 255) / 256));
       std::vector<std::vector<Seg>> part(C);
       std::vector<uint64_t> pn(C, 0);
       std::vector<uint32_t> pe(C, 0);
-      par_chunks(C, [&](size_t c) { walk(lo + span * c / C, lo + span * (c + 1) / C, part[c], pn[c], pe[c]); });
+      // (each chunk in locals, stored once: the chunks' entries of part / pn / pe share cache lines)
+      par_chunks(C, [&](size_t c) {
+        std::vector<Seg> out;
+        uint64_t n = 0;
+        uint32_t e = 0;
+        walk(lo + span * c / C, lo + span * (c + 1) / C, out, n, e);
+        part[c] = std::move(out);
+        pn[c] = n;
+        pe[c] = e;
+      });
       size_t total = 0;
       for (auto& v : part) total += v.size();
       r->segs.reserve(total);
