@@ -1761,16 +1761,27 @@ __attribute__((flatten)) static int push_into_fast(Window& w, uint8_t kind, cons
   return 1;
 }
 
+// The single push's every case but the common one (push_fast), out of line: the common case then needs no stack
+// frame for the counts and the sink (r06: ~280 instructions per vote through pbft_replica_push, host PMU).
+__attribute__((noinline)) static int push_slow(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq,
+                                               const uint8_t* digest, uint32_t signer, const uint8_t* sig);
+
 int pbft_replica_push(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t digest[64],
                       uint32_t signer, const uint8_t sig[64]) {
   if (!r || !digest || !sig || (kind != PBFT_KIND_PREPARE && kind != PBFT_KIND_COMMIT)) return PBFT_EINVAL;
   if (signer < r->n && view == r->current_view && in_log(r, seq) && push_fast(r, kind, seq, digest, signer, sig) == 1) {
     ++r->stats.pushed;
     const uint64_t n = r->arena[r->cur].n;  // (the early batch's next step is due: every piece's worth of rows)
-    if (r->eu.open ? n - r->eu.rows >= early_piece_rows() : (!r->eu.active && n >= early_piece_rows() && r->peak_rows))
+    if (__builtin_expect(r->eu.open ? n - r->eu.rows >= early_piece_rows()
+                                    : (!r->eu.active && n >= early_piece_rows() && r->peak_rows), 0))
       early_single(r);
     return 1;
   }
+  return push_slow(r, kind, view, seq, digest, signer, sig);
+}
+
+static int push_slow(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq, const uint8_t* digest,
+                     uint32_t signer, const uint8_t* sig) {
   PushCounts c;
   ++c.pushed;
   int rc = 0;

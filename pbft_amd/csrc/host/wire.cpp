@@ -431,6 +431,54 @@ bool parse_body(Parser& P, uint32_t kind, pbft_wire_msg* m) {
   return has_v && has_n && has_d && (kind != PBFT_MSG_PREPREPARE || has_m);
 }
 
+// The canonical compact form of a signed vote, exactly as serde_json (and pbft_wire_encode_json) writes it:
+//   {"Prepare":{"view":V,"sequence_number":N,"digest":"<128 hex>","replica":R,"signature":"<128 hex>"}}
+// (or "Commit") matched byte for byte, numbers and hex decoded in place (r06: the single-message JSON ingress).
+// Every byte it accepts is ASCII it checked, so no UTF-8 pass is needed; anything else -- whitespace, another field
+// order, an escape, unknown fields, a PrePrepare or an unsigned vote, an invalid number or hex digit -- returns
+// false and the general parser decides, with serde's rules, exactly as it did before.
+bool fast_vote(const char* s, size_t n, pbft_wire_msg* m) {
+  const char* p = s;
+  const char* const e = s + n;
+  auto lit = [&](const char* L, size_t k) {
+    if ((size_t)(e - p) < k || memcmp(p, L, k) != 0) return false;
+    p += k;
+    return true;
+  };
+  auto num = [&](uint64_t* v) {  // (the general parser's u64 rules: digits, no leading zero, no overflow)
+    if (p >= e || *p < '0' || *p > '9' || (*p == '0' && p + 1 < e && p[1] >= '0' && p[1] <= '9')) return false;
+    uint64_t x = 0;
+    for (; p < e && *p >= '0' && *p <= '9'; ++p) {
+      const uint64_t d = (uint64_t)(*p - '0');
+      if (x > (UINT64_MAX - d) / 10) return false;
+      x = x * 10 + d;
+    }
+    *v = x;
+    return true;
+  };
+  auto hex64 = [&](uint8_t* out) {
+    if (e - p < 129 || p[128] != '"' || !parse_hex(p, 128, out, 64)) return false;
+    p += 129;
+    return true;
+  };
+  uint32_t kind;
+  if (lit("{\"Prepare\":{\"view\":", 19)) kind = PBFT_MSG_PREPARE;
+  else if (lit("{\"Commit\":{\"view\":", 18)) kind = PBFT_MSG_COMMIT;
+  else return false;
+  uint64_t view, seq, rep;
+  if (!num(&view) || !lit(",\"sequence_number\":", 19) || !num(&seq) || !lit(",\"digest\":\"", 11) ||
+      !hex64(m->digest) || !lit(",\"replica\":", 11) || !num(&rep) || rep > 0xFFFFu ||
+      !lit(",\"signature\":\"", 14) || !hex64(m->sig) || !lit("}}", 2) || p != e)
+    return false;
+  m->kind = kind;
+  m->view = view;
+  m->seq = seq;
+  m->digest_ok = 1;
+  m->has_sig = 1;
+  m->replica = (uint32_t)rep;
+  return true;
+}
+
 }  // namespace
 
 extern "C" {
@@ -521,6 +569,8 @@ int pbft_wire_encode_frame(const pbft_wire_msg* m, uint8_t* out, size_t cap, siz
 int pbft_wire_decode_json(const char* json, size_t len, pbft_wire_msg* out, char* arena, size_t arena_cap) {
   if (!json || !out) return PBFT_EINVAL;
   memset(out, 0, sizeof *out);
+  if (fast_vote(json, len, out)) return 0;
+  memset(out, 0, sizeof *out);  // (a partial fast match may have written the digest)
   if (!utf8_valid((const unsigned char*)json, len)) return PBFT_EINVAL;
   Parser P{json, json + len, arena, arena_cap};
   if (!P.lit('{')) return PBFT_EINVAL;

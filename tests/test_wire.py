@@ -117,6 +117,51 @@ def test_decoder_fast_paths_match_the_escaped_forms():
             assert wire.decode_json(js).digest_ok is False, (pos, c)
 
 
+def _decode_or_err(js):
+    try:
+        m = wire.decode_json(js)
+    except Exception as e:  # noqa: BLE001 -- the error itself is what is compared
+        return ("err", getattr(e, "code", None))
+    return (m.kind, m.view, m.seq, m.digest, m.digest_ok, m.replica, m.sig, m.operation, m.timestamp, m.client)
+
+
+def test_canonical_vote_fast_path_equals_general_parser():
+    """r06: a signed vote in serde's exact compact form is matched byte for byte (fast_vote); with one space added
+    after every ':' the general parser decodes the same message.  Both must agree on every field, and on the
+    near-canonical inputs that the fast path hands back (bad numbers, hex, trailing bytes, other fields)."""
+    rnd = random.Random(6)
+    for i in range(300):
+        kind = rnd.choice([PREPARE, COMMIT])
+        m = WireMsg(kind=kind, view=rnd.choice([0, 1, 9, 10, 2**63, 2**64 - 1, rnd.randrange(2**64)]),
+                    seq=rnd.randrange(2**64), digest=bytes(rnd.randrange(256) for _ in range(64)),
+                    replica=rnd.choice([0, 1, 255, 65535, rnd.randrange(65536)]),
+                    sig=bytes(rnd.randrange(256) for _ in range(64)))
+        compact = wire.encode_json(m)
+        spaced = compact.replace(b'":', b'": ')
+        assert compact != spaced
+        a, b = _decode_or_err(compact), _decode_or_err(spaced)
+        assert a == b and a[0] == kind, (compact, a, b)
+    d, sg = bytes(range(64)).hex(), bytes(range(64, 128)).hex()
+    base = '{"Prepare":{"view":%s,"sequence_number":%s,"digest":"%s","replica":%s,"signature":"%s"}}'
+    cases = [("1", "2", d, "3", sg), ("01", "2", d, "3", sg), ("0", "00", d, "3", sg),
+             ("18446744073709551615", "2", d, "3", sg), ("18446744073709551616", "2", d, "3", sg),
+             ("1", "2", d.upper(), "3", sg), ("1", "2", d[:-1] + "g", "3", sg), ("1", "2", d, "65535", sg),
+             ("1", "2", d, "65536", sg), ("1", "2", d, "3", sg[:-2]), ("1", "2", d, "3", sg + "00"),
+             ("1.0", "2", d, "3", sg), ("1", "2e3", d, "3", sg), ("-1", "2", d, "3", sg), ("1", "2", d, "3", "zz" * 64)]
+    for c in cases:
+        compact = (base % c).encode()
+        spaced = compact.replace(b'":', b'": ')
+        assert _decode_or_err(compact) == _decode_or_err(spaced), (c, _decode_or_err(compact))
+    # trailing bytes, an extra field, a different field order: only the general parser can say (same answers)
+    tail = (base % ("1", "2", d, "3", sg)).encode()
+    for js in (tail + b" ", tail + b"x", tail[:-2] + b',"extra":null}}',
+               b'{"Prepare":{"sequence_number":2,"view":1,"digest":"%s","replica":3,"signature":"%s"}}' % (
+                   d.encode(), sg.encode())):
+        got = _decode_or_err(js)
+        assert got == _decode_or_err(js.replace(b'":', b'": ')), js
+    assert _decode_or_err(tail + b" ")[0] == PREPARE and _decode_or_err(tail + b"x")[0] == "err"
+
+
 @pytest.mark.parametrize("bad", [
     b'{"Prepare":{"view":1,"sequence_number":2}}',                                   # missing digest
     b'{"Prepare":{"view":1,"view":1,"sequence_number":2,"digest":""}}',              # duplicate field
