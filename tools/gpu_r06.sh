@@ -11,7 +11,7 @@ for s in $STEPS; do
     verify) timeout -k 10 400 python -u -m pytest tests/test_gpu_verify.py -x -v -k "prio_match or staged_and_pageable or update_keys" --timeout 300 --timeout-method thread > $D/verify_tests.log 2>&1 ;;
     gputests) timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $D/gpu_tests.log 2>&1 ;;
     ingress) timeout -k 10 480 python -u tools/ingress_probe.py > $D/ingress.json 2> $D/ingress.err ;;
-    finstamps) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_finstamps.so build/ab/libpbft_finpre_stamps.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finstamps.txt 2>&1 ;;
+    finstamps) echo "finstamps: build/ab variants are gpurun-ignored since r06 (rebuild with tools/build_variant.sh and drop ./build/ab from .gpurunignore)"; false ;;
     bench) timeout -k 10 600 python -u bench.py > $D/bench.json 2> $D/bench.err ;;
     finvar) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_findpp.so build/ab/libpbft_finpar.so build/ab/libpbft_finboth.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finvar.txt 2>&1 ;;
     step) timeout -k 10 120 tools/microbench/step_study > $D/step_study.txt 2>&1 ;;
