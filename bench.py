@@ -521,7 +521,8 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
                    per visit to pbft_replica_push_records;
       records_64   the same, 64 records (10 KiB, one socket read's worth) per visit;
       json_1       each connection's UviBytes/JSON frames (pbft_amd.wire.encode_votes), one frame per visit to
-                   pbft_replica_push_frames.
+                   pbft_replica_push_frames;
+      json_64      the same, 64 frames (~22 KiB) per visit: the parse rate once a read's frames are consecutive.
     Round-robin visits deliver the round in time order: for seq, for kind, every peer's vote.  The signed PrePrepares
     (on_pre_prepare, GPU digest) are delivered first, untimed.  With a flush behind it (the first rounds) the
     single-message path opens the arena as a batch in pieces on the GPU while the votes arrive (r06), so the flush is
@@ -541,7 +542,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
     n_rep = len(pub)
     n = 2 * n_rep * n_seq
     modes = modes or [("push", 2, True), ("push", 3, False), ("records_1", 3, False), ("records_64", 2, False),
-                      ("json_1", 1, False)]
+                      ("json_1", 1, False), ("json_64", 1, False)]
     primary = 1 % n_rep
     ev = (Event * 16384)()
     rep = ctypes.c_void_p()
