@@ -314,32 +314,38 @@ struct HexTable {
 constexpr HexTable HEX_VAL{};
 // 8 lowercase hex characters -> 4 bytes, SWAR; false if any is not one of 0-9a-f.  Per character: value = low
 // nibble + 9 if bit 6 is set (letters); valid iff the value is < 16 and maps back to exactly that character.
-static inline bool hex8(const char* s, uint8_t out[4]) {
+static inline bool hex8(const char* s, uint32_t* out) {
   constexpr uint64_t ones = 0x0101010101010101ull, high = 0x8080808080808080ull;
   const uint64_t w = load8(s);
   const uint64_t val = (w & (ones * 0x0F)) + ((w >> 6) & ones) * 9;
   const uint64_t gt9 = ((val + ones * 0x76) & high) >> 7;
   const uint64_t recon = val + ones * 0x30 + gt9 * 0x27;
-  if (recon != w || ((val + ones * 0x70) & high)) return false;
   uint64_t x = ((val & 0x00FF00FF00FF00FFull) << 4) | ((val >> 8) & 0x00FF00FF00FF00FFull);
   x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
   x = (x | (x >> 16)) & 0xFFFFFFFFull;
-  const uint32_t v = (uint32_t)x;
-  memcpy(out, &v, 4);
-  return true;
+  *out = (uint32_t)x;
+  return recon == w && !((val + ones * 0x70) & high);
 }
 bool parse_hex(const char* s, size_t n, uint8_t* out, size_t nbytes) {
   if (n != 2 * nbytes) return false;
   size_t i = 0;
-  for (; i + 4 <= nbytes; i += 4)
-    if (!hex8(s + 2 * i, out + i)) return false;
+  bool ok = true;
+  // (8 output bytes per store: the digest and signature are read back 8 bytes at a time -- push's compare and row
+  // copy -- and 4-byte stores under 8-byte loads would defeat store-to-load forwarding)
+  for (; i + 8 <= nbytes; i += 8) {
+    uint32_t lo, hi;
+    ok &= hex8(s + 2 * i, &lo);
+    ok &= hex8(s + 2 * i + 8, &hi);
+    const uint64_t v = (uint64_t)lo | (uint64_t)hi << 32;
+    memcpy(out + i, &v, 8);
+  }
   uint8_t bad = 0;
   for (; i < nbytes; ++i) {
     const uint8_t hi = HEX_VAL.v[(uint8_t)s[2 * i]], lo = HEX_VAL.v[(uint8_t)s[2 * i + 1]];
     bad |= (uint8_t)(hi | lo);
     out[i] = (uint8_t)(hi << 4 | (lo & 15));
   }
-  return !(bad & 0x80);  // (every valid digit is < 16: an invalid one sets the top bit)
+  return ok && !(bad & 0x80);  // (every valid digit is < 16: an invalid one sets the top bit)
 }
 
 bool parse_client_request(Parser& P, pbft_wire_msg* m) {
