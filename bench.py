@@ -522,7 +522,8 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
       records_64   the same, 64 records (10 KiB, one socket read's worth) per visit;
       json_1       each connection's UviBytes/JSON frames (pbft_amd.wire.encode_votes), one frame per visit to
                    pbft_replica_push_frames;
-      json_64      the same, 64 frames (~22 KiB) per visit: the parse rate once a read's frames are consecutive.
+      json_64      the same, 64 frames (~22 KiB) per visit: the parse rate once a read's frames are consecutive;
+    and json_decode_64: those visits' frames decoded only (pbft_wire_decode_json, no replica) -- the parse's share.
     Round-robin visits deliver the round in time order: for seq, for kind, every peer's vote.  The signed PrePrepares
     (on_pre_prepare, GPU digest) are delivered first, untimed.  With a flush behind it (the first rounds) the
     single-message path opens the arena as a batch in pieces on the GPU while the votes arrive (r06), so the flush is
@@ -537,6 +538,7 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
     vp = ctypes.c_void_p
     D.ingress_push.argtypes = [vp, ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     D.ingress_streams.argtypes = [vp, ctypes.c_int, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp, vp, vp, vp]
+    D.ingress_decode_only.argtypes = [ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp, vp]
     pmu_names = ("cycles", "instructions", "llc_references", "llc_misses", "l1d_read_misses", "dtlb_read_misses")
     pmu = (ctypes.c_uint64 * D.ingress_pmu_counters())()
     n_rep = len(pub)
@@ -597,6 +599,13 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
                     assert D.ingress_streams(rep, int(binary), n_rep, ptrs, lens, per_visit, ctypes.byref(pushed),
                                              ctypes.byref(dropped), ctypes.byref(calls), ctypes.byref(sec), pmu) == 0
                     assert pushed.value == n and dropped.value == 0, (pushed.value, dropped.value)
+                    if not binary and per_visit > 1 and out is not None:  # the same visits, decoded only
+                        frames, sec_d = ctypes.c_uint64(), ctypes.c_double()
+                        pmu_d = (ctypes.c_uint64 * D.ingress_pmu_counters())()
+                        assert D.ingress_decode_only(n_rep, ptrs, lens, per_visit, ctypes.byref(frames),
+                                                     ctypes.byref(sec_d), pmu_d) == 0 and frames.value == n
+                        out.setdefault("decode_ms", []).append(sec_d.value * 1e3)
+                        out.setdefault("decode_pmu", []).append([int(x) for x in pmu_d])
                 rows = ctypes.c_uint64()
                 ne = ctypes.c_uint32()
                 t0 = time.perf_counter()
@@ -631,6 +640,13 @@ def replica_ingress_leg(v, seeds, pub, S_bad, bad, n_seq: int, modes=None):
             host = {k: float(v / n) for k, v in zip(pmu_names, pm)}
             host["ipc"] = float(pm[1] / pm[0])
             host["ghz"] = float(pm[0] / (np.median(ing) * 1e-3) / 1e9)
+        if o.get("decode_ms"):
+            dm = float(np.median(o["decode_ms"]))
+            dp = np.median(np.array(o["decode_pmu"], dtype=np.float64), axis=0)
+            dh = {k: float(v / n) for k, v in zip(pmu_names, dp)} if dp[0] > 0 else None
+            if dh:
+                dh["ipc"] = float(dp[1] / dp[0])
+            legs[mode + "_decode_only"] = {"frames_per_s": n / (dm * 1e-3), "decode_ms": dm, "host_pmu_per_frame": dh}
         legs[mode] = {"ingress_votes_per_s": n / (np.median(ing) * 1e-3), "ingress_ms": float(np.median(ing)),
                       "host_pmu_per_vote": host,
                       "flush_ms": float(np.median(fl)), "flush_ms_max": float(fl.max()),

@@ -147,4 +147,40 @@ int ingress_streams(pbft_replica* r, int binary, uint32_t n_conn, const uint8_t*
   return rc;
 }
 
+// The JSON frames decoded only (pbft_wire_decode_json per frame, no replica), visited as ingress_streams visits
+// them: the parse's share of the json modes' instructions per vote.
+int ingress_decode_only(uint32_t n_conn, const uint8_t* const* streams, const uint64_t* lens, uint32_t per_visit,
+                        uint64_t* frames, double* seconds, uint64_t* pmu) {
+  std::vector<uint64_t> off(n_conn, 0);
+  static thread_local char arena[1 << 16];
+  uint64_t nf = 0;
+  int rc = 0;
+  Pmu P;
+  P.start();
+  const double t0 = now_s();
+  for (bool more = true; more && rc == 0;) {
+    more = false;
+    for (uint32_t c = 0; c < n_conn && rc == 0; ++c) {
+      for (uint32_t k = 0; k < per_visit && off[c] < lens[c]; ++k) {
+        uint64_t fl;
+        size_t hn;
+        const uint8_t* p = streams[c] + off[c];
+        if (pbft_uvi_decode(p, lens[c] - off[c], &fl, &hn) != 0) { rc = PBFT_EINVAL; break; }
+        pbft_wire_msg m;
+        if (pbft_wire_decode_json((const char*)p + hn, (size_t)fl, &m, arena, sizeof arena) != 0 || !m.has_sig) {
+          rc = PBFT_EINVAL;
+          break;
+        }
+        off[c] += hn + (size_t)fl;
+        ++nf;
+      }
+      more = more || off[c] < lens[c];
+    }
+  }
+  *seconds = now_s() - t0;
+  P.stop(pmu);
+  *frames = nf;
+  return rc;
+}
+
 }  // extern "C"
