@@ -14,6 +14,9 @@
 
 #include <stdio.h>
 #include <string.h>
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 
 #include "../../../include/pbft_replica.h"
 
@@ -326,10 +329,30 @@ static inline bool hex8(const char* s, uint32_t* out) {
   *out = (uint32_t)x;
   return recon == w && !((val + ones * 0x70) & high);
 }
+#if defined(__SSE2__)
+// 16 lowercase hex characters -> 8 bytes (one 8-byte store), SSE2 (the x86-64 baseline); the same rule as hex8
+static inline bool hex16_sse2(const char* s, uint8_t* out) {
+  const __m128i c = _mm_loadu_si128((const __m128i*)s);
+  const __m128i letter = _mm_cmpeq_epi8(_mm_and_si128(c, _mm_set1_epi8(0x40)), _mm_set1_epi8(0x40));
+  const __m128i val = _mm_add_epi8(_mm_and_si128(c, _mm_set1_epi8(0x0F)), _mm_and_si128(letter, _mm_set1_epi8(9)));
+  const __m128i gt9 = _mm_cmpgt_epi8(val, _mm_set1_epi8(9));
+  const __m128i recon = _mm_add_epi8(_mm_add_epi8(val, _mm_set1_epi8(0x30)), _mm_and_si128(gt9, _mm_set1_epi8(0x27)));
+  const __m128i bad = _mm_or_si128(_mm_xor_si128(_mm_cmpeq_epi8(recon, c), _mm_set1_epi8(-1)),
+                                   _mm_cmpgt_epi8(val, _mm_set1_epi8(15)));
+  // (byte 2k holds the high nibble of output byte k: 16-bit lanes (lo << 4) | hi, packed to bytes)
+  const __m128i pairs = _mm_or_si128(_mm_slli_epi16(_mm_and_si128(val, _mm_set1_epi16(0x00FF)), 4),
+                                     _mm_srli_epi16(val, 8));
+  _mm_storel_epi64((__m128i*)out, _mm_packus_epi16(pairs, pairs));
+  return _mm_movemask_epi8(bad) == 0;
+}
+#endif
 bool parse_hex(const char* s, size_t n, uint8_t* out, size_t nbytes) {
   if (n != 2 * nbytes) return false;
   size_t i = 0;
   bool ok = true;
+#if defined(__SSE2__)
+  for (; i + 8 <= nbytes; i += 8) ok &= hex16_sse2(s + 2 * i, out + i);
+#endif
   // (8 output bytes per store: the digest and signature are read back 8 bytes at a time -- push's compare and row
   // copy -- and 4-byte stores under 8-byte loads would defeat store-to-load forwarding)
   for (; i + 8 <= nbytes; i += 8) {
