@@ -940,6 +940,8 @@ def main():
     ap.add_argument("--replicas", type=int, default=N_REPLICAS)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="only the headline line (no side legs)")
+    ap.add_argument("--replica-only", action="store_true",
+                    help="diagnosis: the headline, then only the replica legs (r06: where the in-bench leg's time goes)")
     ap.add_argument("--latency-iters", type=int, default=200)
     ap.add_argument("--stream-s", type=float, default=20.0, help="config #5 offered-load leg duration (s)")
     ap.add_argument("--settle-s", type=float, default=1.0, help="untimed GPU settle time before the warmup steps")
@@ -1148,6 +1150,10 @@ def main():
                                       fin_stream.cuda_stream)
         torch.cuda.synchronize()
         p8 = (time.perf_counter() - tp) * 1e3 / 50
+        if args.replica_only:  # (no shard / latency legs before the replica legs)
+            extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=20)
+            print(json.dumps({"replica_only": extras["replica_flush_2^20"]}), flush=True)
+            return
         extras["shard_of_8"] = {"sigs": n8, "kernel_ms": k8, "wall_ms_per_launch": w8,
                                 "verifies_per_s_per_gpu": n8 / (k8 * 1e-3), "pipelined_wall_ms_per_launch": p8,
                                 "kernel_ms_5_samples": [a for a, _ in s8], "pmc": shard_pmc(n8),

@@ -27,6 +27,7 @@ for s in $STEPS; do
     benchprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D/benchprof -o bench -- python3 bench.py > $D/benchprof.json 2> $D/benchprof.err && rm -f $D/benchprof/bench_kernel_trace.csv ;;
     parab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_PAR_WINDOWS=1024,1000000000 > $D/parab.json 2> $D/parab.err ;;
     heat) timeout -k 10 300 python -u tools/replica_heat_probe.py > $D/heat.json 2> $D/heat.err ;;
+    replonly) timeout -k 10 300 python -u bench.py --replica-only --no-cpu > $D/replonly.json 2> $D/replonly.err ;;
     pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;
   esac
