@@ -1171,21 +1171,6 @@ def main():
                 lat.append((time.perf_counter() - t) * 1e3)
         extras["p50_ms_4k_round"] = float(np.median(lat))
         extras["p99_ms_4k_round"] = float(np.percentile(lat, 99))
-        # the replica legs (host-heavy) run early: after the e2e / config-#5 / CPU legs the same leg ran 3.6-3.9 ms
-        # against 3.1 ms in a fresh process on the same box (profiles/r06/final_a/, final_d/)
-        extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=20)
-        # the same round through pbft_replica_create_multi over this context + 1 clone (one slice each; on a node the
-        # contexts would be two GPUs with a PCIe link each -- here both share this GPU and its link)
-        extras["replica_flush_2^20_2ctx"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=20,
-                                                                n_ctx=2)
-        # the reference-shaped ingress: one message at a time on one thread (VERDICT r05 item 1)
-        extras["replica_ingress_2^20"] = replica_ingress_leg(v, seeds, pub, S, ~expect, n_seq)
-        # (an untimed settle and a short untimed stream before the config-#5 legs: right after the replica legs'
-        # teardown -- pinned arenas unregistered, a clone context freed -- the offered leg once saw a 40-ms GPU-side
-        # stall, profiles/r06/final_c/)
-        torch.cuda.synchronize()
-        time.sleep(args.settle_s)
-        stream_latency(v, R, S, key_idx, msg, float(1 << 21), duration_s=0.5)
         # config #5: 2^24 sigs/s offered to an 8-GPU node = 2^21 per GPU; and back-to-back 4k batches
         # (>= 10k batches for the p50 / p99, as SURVEY §8d asks: 20 s at 512 batches/s)
         extras["stream_4k"] = {"offered_2^21_per_gpu": stream_latency(v, R, S, key_idx, msg, float(1 << 21),
@@ -1194,6 +1179,17 @@ def main():
                                                                                duration_s=args.stream_s / 2,
                                                                                pinned=False),
                                "back_to_back": stream_latency(v, R, S, key_idx, msg, float("inf"))}
+        # the replica legs (host-heavy) right after the config-#5 legs: after the e2e / votes / CPU legs the same leg
+        # ran 3.6-3.9 ms against 3.1 ms in a fresh process on the same box (profiles/r06/final_a/, final_d/), and
+        # with the replica legs BEFORE them the offered config-#5 leg saw one 17-40-ms GPU-side wait in each of
+        # three lines (profiles/r06/final_b/ c/ e/: the host polling every ~20 us meanwhile), in none of three without
+        extras["replica_flush_2^20"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=20)
+        # the same round through pbft_replica_create_multi over this context + 1 clone (one slice each; on a node the
+        # contexts would be two GPUs with a PCIe link each -- here both share this GPU and its link)
+        extras["replica_flush_2^20_2ctx"] = replica_round_leg(v, seeds, pub, R, S, key_idx, msg, expect, rounds=20,
+                                                                n_ctx=2)
+        # the reference-shaped ingress: one message at a time on one thread (VERDICT r05 item 1)
+        extras["replica_ingress_2^20"] = replica_ingress_leg(v, seeds, pub, S, ~expect, n_seq)
         extras["e2e_2^20"] = e2e_host_round(v, R, S, key_idx, msg, expect, torch)
         extras["e2e_votes_2^20"] = e2e_votes_round(v, R, S, key_idx, msg, expect, torch)
         extras["votes_device_2^20"] = votes_device_round(v, d, msg, expect, stream, torch, dev)
