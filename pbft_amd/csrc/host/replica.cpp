@@ -987,9 +987,12 @@ static void revert_segs(pbft_replica* r) {
 // wins), the first accepted PrePrepare fixes the window's digest (conflicting ones rejected, :144-151); verified
 // candidates leave the windows.  Segments [s0, s1) (whole windows: a window's segments stay on one thread, in
 // order); counts into st[3] = accepted, rejected_sig, rejected_digest; touched[g] = some candidate accepted.
-static bool apply_prefetch() {  // PBFT_APPLY_PREFETCH=0: off (read per call: A/B in one process)
+// PBFT_APPLY_PREFETCH: how many segments ahead the application prefetches (0: off; default 1; read per call: A/B in
+// one process)
+static size_t apply_prefetch() {
   const char* e = getenv("PBFT_APPLY_PREFETCH");
-  return !(e && atoi(e) == 0);
+  const long v = e ? strtol(e, nullptr, 10) : 1;
+  return (size_t)(v < 0 ? 0 : v > 8 ? 8 : v);
 }
 static inline void prefetch_bytes(const void* p, size_t n) {
   for (size_t o = 0; o < n; o += 64) __builtin_prefetch((const uint8_t*)p + o);
@@ -1008,12 +1011,14 @@ static void apply_range(pbft_replica* r, size_t s0, size_t s1, uint64_t st_out[3
   std::vector<uint8_t> mism;
   uint64_t st[3] = {0, 0, 0};  // local: the threads' st_out entries share cache lines
   int64_t rel[2] = {0, 0};     // candidates leaving each arena (one atomic update per call)
-  const bool pf = apply_prefetch();
+  const size_t pf = apply_prefetch();
+  if (pf > 1 && !r->erased_in_flight)  // (the first pf - 1 segments of the range: the loop fetches pf ahead)
+    for (size_t j = s0 + 1; j < std::min(s1, s0 + pf); ++j) prefetch_phase(r->segs[j].w->ph[r->segs[j].kind]);
   for (size_t gi = s0; gi < s1; ++gi) {
     const Seg& g = r->segs[gi];
     // the next segment's columns and per-signer arrays, fetched while this one is applied (a batch handed over as
     // the arena reaches the application with them cold: nothing since the push has touched them)
-    if (pf && gi + 1 < s1 && !r->erased_in_flight) prefetch_phase(r->segs[gi + 1].w->ph[r->segs[gi + 1].kind]);
+    if (pf && gi + pf < s1 && !r->erased_in_flight) prefetch_phase(r->segs[gi + pf].w->ph[r->segs[gi + pf].kind]);
     Window* wp = g.w;
     if (r->erased_in_flight) {
       wp = find_window(r, g.key.first, g.key.second);
