@@ -8,14 +8,20 @@
 //                    (UviBytes/JSON frames -> pbft_replica_push_frames, or 160-byte binary records ->
 //                    pbft_replica_push_records) to the replica, the connection being the authenticated peer.
 // Built by __graft_entry__.build() next to the library it links (tools/ingress/libingress.so).
+#include <dlfcn.h>
 #include <linux/perf_event.h>
 #include <sys/ioctl.h>
+#include <sys/mman.h>
 #include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <map>
+#include <string>
 #include <vector>
 
 #include "../../include/pbft_replica.h"
@@ -87,6 +93,73 @@ struct Pmu {
   }
 };
 
+// PBFT_INGRESS_PROFILE=file: a sampling profile of the calling thread around each timed loop (perf_event_open,
+// PERF_SAMPLE_IP every 20,000 user-space cycles, a 4-MiB ring read once at the end), appended to `file` as lines
+// "count module offset" (tools/ingress_profile.py symbolizes them with llvm-symbolizer).
+struct Sampler {
+  int fd = -1;
+  uint8_t* ring = nullptr;
+  size_t pages = 1024, page = 4096;
+  const char* out = getenv("PBFT_INGRESS_PROFILE");
+  const char* tag;
+  explicit Sampler(const char* t) : tag(t) {
+    if (!out) return;
+    perf_event_attr a;
+    memset(&a, 0, sizeof a);
+    a.size = sizeof a;
+    a.type = PERF_TYPE_HARDWARE;
+    a.config = PERF_COUNT_HW_CPU_CYCLES;
+    a.sample_period = 20000;
+    a.sample_type = PERF_SAMPLE_IP;
+    a.exclude_kernel = 1;
+    a.exclude_hv = 1;
+    a.disabled = 1;
+    fd = (int)syscall(SYS_perf_event_open, &a, 0, -1, -1, 0);
+    if (fd < 0) return;
+    page = (size_t)sysconf(_SC_PAGESIZE);
+    void* m = mmap(nullptr, (pages + 1) * page, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) { close(fd); fd = -1; return; }
+    ring = (uint8_t*)m;
+    ioctl(fd, PERF_EVENT_IOC_RESET, 0);
+    ioctl(fd, PERF_EVENT_IOC_ENABLE, 0);
+  }
+  ~Sampler() {
+    if (fd < 0) return;
+    ioctl(fd, PERF_EVENT_IOC_DISABLE, 0);
+    const perf_event_mmap_page* hdr = (const perf_event_mmap_page*)ring;
+    const uint64_t head = __atomic_load_n(&hdr->data_head, __ATOMIC_ACQUIRE), size = pages * page;
+    const uint8_t* data = ring + page;
+    std::map<std::pair<std::string, uint64_t>, uint64_t> hist;
+    uint64_t lost = 0, n = 0;
+    for (uint64_t pos = head > size ? head - size : 0; pos + sizeof(perf_event_header) <= head;) {
+      perf_event_header h;
+      for (size_t b = 0; b < sizeof h; ++b) ((uint8_t*)&h)[b] = data[(pos + b) % size];
+      if (h.size == 0) break;
+      if (h.type == PERF_RECORD_SAMPLE) {
+        uint64_t ip = 0;
+        for (size_t b = 0; b < 8; ++b) ((uint8_t*)&ip)[b] = data[(pos + sizeof h + b) % size];
+        Dl_info di;
+        if (dladdr((void*)ip, &di) && di.dli_fname) ++hist[{di.dli_fname, ip - (uint64_t)di.dli_fbase}];
+        else ++hist[{"?", ip}];
+        ++n;
+      } else if (h.type == PERF_RECORD_LOST) {
+        ++lost;
+      }
+      pos += h.size;
+    }
+    FILE* f = fopen(out, "a");
+    if (f) {
+      fprintf(f, "# %s: %llu samples, %llu lost records\n", tag, (unsigned long long)n, (unsigned long long)lost);
+      for (const auto& kv : hist)
+        fprintf(f, "%llu %s 0x%llx\n", (unsigned long long)kv.second, kv.first.first.c_str(),
+                (unsigned long long)kv.first.second);
+      fclose(f);
+    }
+    munmap(ring, (pages + 1) * page);
+    close(fd);
+  }
+};
+
 extern "C" {
 
 int ingress_pmu_counters() { return N_PMU; }
@@ -96,6 +169,7 @@ int ingress_push(pbft_replica* r, uint64_t N, const uint8_t* kind, const uint64_
                  double* seconds, uint64_t* pmu) {
   uint64_t q = 0;
   int rc = 0;
+  Sampler prof("push");
   Pmu P;
   P.start();
   const double t0 = now_s();
@@ -116,6 +190,9 @@ int ingress_streams(pbft_replica* r, int binary, uint32_t n_conn, const uint8_t*
   std::vector<uint64_t> off(n_conn, 0);
   uint64_t np = 0, nd = 0, nc = 0;
   int rc = 0;
+  char tag[32];
+  snprintf(tag, sizeof tag, "%s_%u", binary ? "records" : "json", per_visit);
+  Sampler prof(tag);
   Pmu P;
   P.start();
   const double t0 = now_s();
