@@ -814,74 +814,10 @@ static bool is_done(const pbft_replica* r, uint64_t view, uint64_t seq) {
   return seq <= std::prev(it)->second;
 }
 
-static size_t host_threads();
-// Chunks of a serial walk over the windows run on the pool (T - 1 workers and the calling thread) once there are
-// this many live windows (r06: the flush's segment walk and the GC each took 0.12-0.2 ms for a 2048-seq round,
-// every window's lines last written by the push_many and apply workers)
-// (PBFT_PAR_WINDOWS overrides it, read per call: an A/B in one process)
-static size_t par_windows() {
-  const char* e = getenv("PBFT_PAR_WINDOWS");
-  return e ? (size_t)strtoull(e, nullptr, 10) : 1024;
-}
-template <class F>
-static void par_chunks(size_t C, F&& f) {
-  std::atomic<size_t> next{0}, done{0};
-  const size_t T = std::max<size_t>(1, std::min<size_t>(host_threads(), C));
-  WorkerPool::get().run_with_caller(T - 1, [&](size_t) {
-    for (size_t c; (c = next.fetch_add(1, std::memory_order_relaxed)) < C;) {
-      f(c);
-      done.fetch_add(1, std::memory_order_release);
-    }
-  }, [&] { return done.load(std::memory_order_acquire) == C; });
-}
-
 static void gc(pbft_replica* r) {
   r->last_w = nullptr;  // windows may go away
   // committed prefix: h advances over consecutive committed windows (ring slot h + 1, h + 2, ...)
   const uint64_t h0 = r->h;
-  if (r->n_windows >= par_windows() && r->win_hi > r->h) {
-    // many windows: the first seq that is not a committed window, chunk by chunk on the pool; then the committed
-    // prefix is dropped chunk by chunk (each chunk's ring slots are its own; the free list and counts merged after)
-    const uint64_t lo = r->h + 1, span = std::min<uint64_t>(r->win_hi - r->h, r->ring.size());
-    const size_t C = std::min<size_t>(4 * host_threads(), (size_t)((span + 255) / 256));
-    std::vector<uint64_t> stop(C);
-    const uint64_t view = r->current_view;
-    par_chunks(C, [&](size_t c) {
-      const uint64_t a = lo + span * c / C, b = lo + span * (c + 1) / C;
-      uint64_t q = a;
-      for (; q < b; ++q) {
-        const Window* w = find_window(r, view, q);
-        if (!w || !w->committed_reported) break;
-      }
-      stop[c] = q;
-    });
-    uint64_t hn = lo;
-    for (size_t c = 0; c < C; ++c) {
-      hn = stop[c];
-      if (stop[c] < lo + span * (c + 1) / C) break;
-    }
-    if (hn > lo) {  // drop seqs [lo, hn)
-      const uint64_t cnt = hn - lo;
-      const size_t D = std::min<size_t>(4 * host_threads(), (size_t)((cnt + 255) / 256));
-      std::vector<std::vector<Window*>> freed(D);
-      if (r->in_flight) r->erased_in_flight = true;
-      par_chunks(D, [&](size_t c) {
-        std::vector<Window*> f;  // (local: the chunks' vectors share cache lines)
-        for (uint64_t q = lo + cnt * c / D, e = lo + cnt * (c + 1) / D; q < e; ++q) {
-          Window* w = r->ring[q & r->ring_mask];
-          release_window(r, *w);
-          r->ring[q & r->ring_mask] = nullptr;
-          w->seq = 0;
-          f.push_back(w);
-        }
-        freed[c] = std::move(f);
-      });
-      for (auto& v : freed) r->win_free.insert(r->win_free.end(), v.begin(), v.end());
-      r->n_windows -= cnt;
-      r->stats.windows_gc += cnt;
-      r->h = hn - 1;
-    }
-  }
   for (;;) {
     Window* w = find_window(r, r->current_view, r->h + 1);
     if (!w || !w->committed_reported) break;
@@ -2128,23 +2064,15 @@ static uint64_t ns_since(std::chrono::steady_clock::time_point t0) {
 }
 
 // An arena batch's segments: every candidate of each in flight, each segment complete once the rows below its
-// phase's last row reference are (chunks on the pool for a large round: every segment its own phase)
+// phase's last row reference are.  (r06: these walks over every window -- segments, marking, GC -- ran in chunks on
+// the pool for a 0.1-ms median gain, until a worker descheduled while holding a chunk held one flush_submit for
+// 3.9 ms: profiles/r06/final/; serial again.)
 static void mark_arena_segs(pbft_replica* r) {
-  auto mark = [r](size_t a, size_t b) {
-    for (size_t i = a; i < b; ++i) {
-      Seg& g = r->segs[i];
-      Phase& p = g.w->ph[g.kind];
-      g.row_end = p.row_hi;
-      p.n_flight = g.count;
-      p.n_pending = 0;
-    }
-  };
-  const size_t S = r->segs.size();
-  if (S < 3 * par_windows()) {
-    mark(0, S);
-  } else {
-    const size_t C = std::min<size_t>(4 * host_threads(), (S + 511) / 512);
-    par_chunks(C, [&](size_t c) { mark(S * c / C, S * (c + 1) / C); });
+  for (Seg& g : r->segs) {
+    Phase& p = g.w->ph[g.kind];
+    g.row_end = p.row_hi;
+    p.n_flight = g.count;
+    p.n_pending = 0;
   }
 }
 
@@ -2274,55 +2202,18 @@ static int flush_submit_impl(pbft_replica* r, int force, uint64_t* n_rows) {
   uint64_t N = 0;
   uint32_t E = 0;
   const uint64_t view = r->current_view;
-  // (the ring in seq order; segments numbered from row 0 / envelope 0 of their chunk)
-  auto walk = [r, view, force](uint64_t a, uint64_t b, std::vector<Seg>& out, uint64_t& n, uint32_t& e) {
-    for (uint64_t q = a; q < b; ++q) {
-      Window* wp = r->ring[q & r->ring_mask];
-      if (!wp || wp->seq != q) continue;
-      Window& w = *wp;
-      const bool rd[3] = {w.ph[0].n_pending > 0, force ? w.ph[1].n_pending > 0 : prepare_ready(r, view, w),
-                          force ? w.ph[2].n_pending > 0 : commit_ready(r, w)};
-      for (int kind = 0; kind < 3; ++kind) {
-        if (!rd[kind]) continue;
-        Phase& p = w.ph[kind];
-        out.push_back({&w, Key{view, q}, n, n + p.size(), (uint32_t)p.size(), e, (uint8_t)kind});
-        n += p.size();
-        e += (uint32_t)p.digs.size();
-      }
-    }
-  };
-  if (r->n_windows && r->win_hi > r->h) {
-    const uint64_t lo = r->h + 1, span = r->win_hi - r->h;
-    if (r->n_windows < par_windows()) {
-      walk(lo, lo + span, r->segs, N, E);
-    } else {  // (chunks on the pool, then renumbered in order)
-      const size_t C = std::min<size_t>(4 * host_threads(), (size_t)((span + 255) / 256));
-      std::vector<std::vector<Seg>> part(C);
-      std::vector<uint64_t> pn(C, 0);
-      std::vector<uint32_t> pe(C, 0);
-      // (each chunk in locals, stored once: the chunks' entries of part / pn / pe share cache lines)
-      par_chunks(C, [&](size_t c) {
-        std::vector<Seg> out;
-        uint64_t n = 0;
-        uint32_t e = 0;
-        walk(lo + span * c / C, lo + span * (c + 1) / C, out, n, e);
-        part[c] = std::move(out);
-        pn[c] = n;
-        pe[c] = e;
-      });
-      size_t total = 0;
-      for (auto& v : part) total += v.size();
-      r->segs.reserve(total);
-      for (size_t c = 0; c < C; ++c) {
-        for (Seg g : part[c]) {
-          g.row0 += N;
-          g.row_end += N;
-          g.env0 += E;
-          r->segs.push_back(g);
-        }
-        N += pn[c];
-        E += pe[c];
-      }
+  for (uint64_t q = r->h + 1; q <= r->win_hi && r->n_windows; ++q) {  // (the ring in seq order)
+    Window* wp = r->ring[q & r->ring_mask];
+    if (!wp || wp->seq != q) continue;
+    Window& w = *wp;
+    const bool rd[3] = {w.ph[0].n_pending > 0, force ? w.ph[1].n_pending > 0 : prepare_ready(r, view, w),
+                        force ? w.ph[2].n_pending > 0 : commit_ready(r, w)};
+    for (int kind = 0; kind < 3; ++kind) {
+      if (!rd[kind]) continue;
+      Phase& p = w.ph[kind];
+      r->segs.push_back({&w, Key{view, q}, N, N + p.size(), (uint32_t)p.size(), E, (uint8_t)kind});
+      N += p.size();
+      E += (uint32_t)p.digs.size();
     }
   }
   r->rows = N;

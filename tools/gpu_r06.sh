@@ -25,7 +25,6 @@ for s in $STEPS; do
     timeline) timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $D/tl -o tl -- python3 tools/ingress_probe.py --skip-ingress-leg --rounds 4 > $D/timeline.out 2>&1 ;;
     pieceab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_MANY_PIECE=131072,262144 > $D/pieceab.json 2> $D/pieceab.err ;;
     benchprof) timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D/benchprof -o bench -- python3 bench.py > $D/benchprof.json 2> $D/benchprof.err && rm -f $D/benchprof/bench_kernel_trace.csv ;;
-    parab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_PAR_WINDOWS=1024,1000000000 > $D/parab.json 2> $D/parab.err ;;
     heat) timeout -k 10 300 python -u tools/replica_heat_probe.py > $D/heat.json 2> $D/heat.err ;;
     replonly) timeout -k 10 300 python -u bench.py --replica-only --no-cpu > $D/replonly.json 2> $D/replonly.err ;;
     pfab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_APPLY_PREFETCH=1,2,4,0 > $D/pfab.json 2> $D/pfab.err ;;
