@@ -15,7 +15,7 @@ for s in $STEPS; do
     bench) timeout -k 10 600 python -u bench.py > $D/bench.json 2> $D/bench.err ;;
     finvar) timeout -k 10 400 python -u tools/ab.py build/ab/libpbft_finbase.so build/ab/libpbft_finpre.so build/ab/libpbft_findpp.so build/ab/libpbft_finpar.so build/ab/libpbft_finboth.so --replicas 16 --seqs 32768 --sizes 131072,1048576 --rounds 8 --iters 20 > $D/finvar.txt 2>&1 ;;
     step) timeout -k 10 120 tools/microbench/step_study > $D/step_study.txt 2>&1 ;;
-    hostinfo) { nproc; cat /sys/fs/cgroup/cpu.max; python -c "import os; print(len(os.sched_getaffinity(0)))"; grep -m1 "model name" /proc/cpuinfo; } > $D/hostinfo.txt 2>&1; true ;;
+    hostinfo) { nproc; cat /sys/fs/cgroup/cpu.max; python -c "import os; print(len(os.sched_getaffinity(0)))"; grep -m1 "model name" /proc/cpuinfo; for n in /sys/devices/system/node/node*; do echo "$n $(cat $n/cpulist)"; grep -E "MemTotal|MemFree" $n/meminfo; done; cat /sys/class/drm/card*/device/numa_node 2>/dev/null | head -3; cat /sys/kernel/mm/transparent_hugepage/enabled; cat /proc/sys/kernel/numa_balancing; } > $D/hostinfo.txt 2>&1; true ;;
     threads) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 36 --flush-ab PBFT_REPLICA_THREADS=16,15,12,8 > $D/threads.json 2> $D/threads.err ;;
     hostbw) timeout -k 10 120 tools/microbench/host_bw > $D/host_bw.txt 2>&1 ;;
     tail) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 > $D/tail.json 2> $D/tail.err ;;
