@@ -32,6 +32,8 @@
 #include <mutex>
 #include <thread>
 #include <unistd.h>
+#include <sched.h>
+#include <sys/syscall.h>
 #if defined(__x86_64__)
 #include <immintrin.h>
 #endif
@@ -217,8 +219,59 @@ struct Seg {
 // Worker threads for the batch fill and the bitmap application: one pool per process, started on first use and
 // reused by every large batch of every replica (creating 16 threads costs about a millisecond in a process that
 // maps the GPU's memory); one job at a time (start() holds the pool until wait()).
+// ---- NUMA (r06): the worker threads on the node whose memory they write ----
+// The node holding the page at p (get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR)); -1 if unknown.
+static int node_of(const void* p) {
+#if defined(SYS_get_mempolicy)
+  int node = -1;
+  if (p && syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL) == 0) return node;
+#else
+  (void)p;
+#endif
+  return -1;
+}
+// The CPUs of NUMA node n (sysfs cpulist, e.g. "0-63,128-191") that this process may use; false if none / unknown.
+static bool node_cpus(int n, cpu_set_t* out) {
+  CPU_ZERO(out);
+  if (n < 0) return false;
+  char path[96];
+  snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", n);
+  FILE* f = fopen(path, "r");
+  if (!f) return false;
+  char buf[4096];
+  const size_t len = fread(buf, 1, sizeof buf - 1, f);
+  fclose(f);
+  buf[len] = 0;
+  cpu_set_t allowed;
+  if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return false;
+  for (char* q = buf; *q;) {
+    char* e;
+    long a = strtol(q, &e, 10);
+    if (e == q) break;
+    long b = a;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET(c, &allowed)) CPU_SET(c, out);
+    q = *e == ',' ? e + 1 : e;
+    if (*q == '\n') break;
+  }
+  return CPU_COUNT(out) > 0;
+}
+
 class WorkerPool {
  public:
+  // Keep the workers on NUMA node n's CPUs (any of them: the scheduler still balances within the node), or let
+  // them float again (n < 0); applied to every worker now and at creation.  Call between jobs.
+  void bind(int n) {
+    if (n == node_) return;
+    cpu_set_t set;
+    if (n >= 0 && !node_cpus(n, &set)) n = -1;
+    if (n < 0 && sched_getaffinity(0, sizeof set, &set) != 0) return;
+    std::lock_guard<std::mutex> lk(job_mu_);
+    for (std::thread& t : th_) (void)pthread_setaffinity_np(t.native_handle(), sizeof set, &set);
+    node_ = n;
+    set_ = set;
+  }
   static WorkerPool& get() {
     static WorkerPool* p = new WorkerPool();  // never destroyed: idle workers may outlive static destructors
     return *p;
@@ -238,12 +291,14 @@ class WorkerPool {
       gen_ = 0;
       active_ = pending_ = running_ = 0;
       closed_ = false;
+      node_ = -1;
       pid_ = getpid();
     }
     job_mu_.lock();
     while (th_.size() < T) {
       const size_t id = th_.size();
       th_.emplace_back([this, id] { loop(id); });
+      if (node_ >= 0) (void)pthread_setaffinity_np(th_.back().native_handle(), sizeof set_, &set_);
     }
     {
       std::lock_guard<std::mutex> lk(mu_);
@@ -315,6 +370,8 @@ class WorkerPool {
   uint64_t gen_ = 0;
   size_t active_ = 0, pending_ = 0, running_ = 0;
   bool closed_ = false;
+  int node_ = -1;  // bind(): the NUMA node the workers are kept on (-1: anywhere the process may run)
+  cpu_set_t set_;
   pid_t pid_ = getpid();  // the process whose threads th_ holds
 };
 
@@ -1746,6 +1803,13 @@ static int push_slow(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq,
 
 // push_many of at least this many rows runs on the worker pool (PBFT_REPLICA_THREADS threads)
 static constexpr uint64_t PUSH_PAR_MIN = 1u << 14;
+// PBFT_NUMA_BIND=1 (read per call): push_many keeps the worker threads on the NUMA node of the caller's input (the
+// 149 B per vote they read); 0: anywhere the process may run
+static void numa_bind(const void* input) {
+  const char* e = getenv("PBFT_NUMA_BIND");
+  WorkerPool::get().bind(e && atoi(e) != 0 ? node_of(input) : -1);
+}
+
 // push_many's early-batch pieces: rows per piece (PBFT_MANY_PIECE, 2^12..2^22, default 2^17; read per call)
 static uint64_t many_piece_rows() {
   const char* e = getenv("PBFT_MANY_PIECE");
@@ -1784,6 +1848,7 @@ int pbft_replica_push_many(pbft_replica* r, uint64_t N, const uint8_t* kind, con
     //     one (view, seq); rejected rows are flagged and do not break a run;
     struct Run { uint64_t lo, hi, seq; Window* w; uint32_t owner; uint64_t good; bool first; };
     RTRACE(r, "push", n_ok);
+    numa_bind(digests);
     const uint64_t tp0 = now_ns();
     // (in 8 chunks per thread, taken dynamically: a worker the host deschedules holds up one chunk, not a
     // sixteenth of the call -- the r06 replica leg's slowest round had this pass at 4.1 ms against 0.3)

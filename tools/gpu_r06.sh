@@ -30,6 +30,7 @@ for s in $STEPS; do
     pfab) timeout -k 10 400 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 40 --flush-ab PBFT_APPLY_PREFETCH=1,2,4,0 > $D/pfab.json 2> $D/pfab.err ;;
     hostprof) rm -f $D/ingress_samples.txt; PBFT_INGRESS_PROFILE=$PWD/$D/ingress_samples.txt timeout -k 10 480 python -u tools/ingress_probe.py --skip-flush-leg > $D/hostprof.json 2> $D/hostprof.err && timeout -k 10 300 python tools/ingress_profile.py $D/ingress_samples.txt > $D/ingress_profile.txt 2>&1 ;;
     ntab) for k in 1 0 1 0; do PBFT_STREAM_STORES=$k timeout -k 10 480 python -u tools/ingress_probe.py --modes records_64 > $D/nt_$k.$RANDOM.json 2>> $D/ntab.err || exit 1; done ;;
+    numaab) for k in 0 1 0 1 0 1 0 1; do PBFT_NUMA_BIND=$k timeout -k 10 300 python -u tools/ingress_probe.py --skip-ingress-leg --rounds 20 > $D/numa_$k.$RANDOM.json 2>> $D/numaab.err || exit 1; done ;;
     pmu) timeout -k 10 30 tools/microbench/pmu_probe > $D/pmu.txt 2>&1; true ;;
     smoke) timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $D/smoke.log 2>&1 ;;
   esac
