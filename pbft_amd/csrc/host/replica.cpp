@@ -1803,11 +1803,13 @@ static int push_slow(pbft_replica* r, uint8_t kind, uint64_t view, uint64_t seq,
 
 // push_many of at least this many rows runs on the worker pool (PBFT_REPLICA_THREADS threads)
 static constexpr uint64_t PUSH_PAR_MIN = 1u << 14;
-// PBFT_NUMA_BIND=1 (read per call): push_many keeps the worker threads on the NUMA node of the caller's input (the
-// 149 B per vote they read); 0: anywhere the process may run
+// push_many keeps the worker threads on the NUMA node of the caller's input (the 149 B per vote they read; the GPU
+// boxes are two-socket, and the scheduler spread the workers over both: 8 processes interleaved, r06,
+// profiles/r06/replica/numa_ab/: round 3.08-3.14 ms bound against 3.03-3.50 ms, push_many 1.97-2.07 against
+// 2.05-2.40); PBFT_NUMA_BIND=0 (read per call): anywhere the process may run
 static void numa_bind(const void* input) {
   const char* e = getenv("PBFT_NUMA_BIND");
-  WorkerPool::get().bind(e && atoi(e) != 0 ? node_of(input) : -1);
+  WorkerPool::get().bind(e && atoi(e) == 0 ? -1 : node_of(input));
 }
 
 // push_many's early-batch pieces: rows per piece (PBFT_MANY_PIECE, 2^12..2^22, default 2^17; read per call)
