@@ -233,8 +233,9 @@ int pbft_replica_push(pbft_replica *r, uint8_t kind, uint64_t view, uint64_t seq
  * for A/B runs): PBFT_REPLICA_EARLY=0 (no early batch), PBFT_MANY_PIECE (rows per piece, default 2^17),
  * PBFT_PUSH_TASKS (tasks per thread, default 8), PBFT_ADOPT_PARTIAL=0 (an adopted batch applied once, when done),
  * PBFT_REPLICA_DIRECT=0 (flush_submit fills the context's staging instead of handing the arena over),
- * PBFT_APPLY_PREFETCH=0, PBFT_REPLICA_THREADS (worker threads, default 16); read once: PBFT_STREAM_STORES=0 (plain
- * stores for the rows). */
+ * PBFT_APPLY_PREFETCH (segments ahead, 0 = off, default 1), PBFT_REPLICA_THREADS (worker threads, default 16),
+ * PBFT_NUMA_BIND=0 (the workers are kept on the NUMA node of `digests` by default); read once: PBFT_STREAM_STORES=0
+ * (plain stores for the rows). */
 int pbft_replica_push_many(pbft_replica *r, uint64_t N, const uint8_t *kind, const uint64_t *view, const uint64_t *seq,
                            const uint8_t *digests, const uint32_t *signer, const uint8_t *sigs, uint64_t *queued);
 
