@@ -107,15 +107,25 @@ def test_gpu_phase_ordered_rounds_async_flush(gpu_cluster):
     c.close()
 
 
-@pytest.mark.parametrize("n_ctx,direct", [(1, "1"), (3, "1"), (1, "0"), (3, "0")])
-def test_gpu_replica_2p20_round(gpu_cluster, n_ctx, direct, monkeypatch):
+@pytest.mark.parametrize("n_ctx,direct,tasks,piece,shuffle", [(1, "1", None, None, False), (3, "1", None, None, False),
+                                                             (1, "0", None, None, False), (3, "0", None, None, False),
+                                                             (1, "1", "1", "4096", False), (3, "1", "64", "65536", True),
+                                                             (1, "1", None, None, True)])
+def test_gpu_replica_2p20_round(gpu_cluster, n_ctx, direct, tasks, piece, shuffle, monkeypatch):
     """Config #4's round through one replica on the GPU: n = 256, 2048 seqs, 2^20 GPU-signed votes + 2048
     PrePrepares pushed, ONE flush_submit, polled to completion; the windows whose quorum was broken by corrupted votes
     neither prepare nor commit, every other one commits.  n_ctx = 3: pbft_replica_create_multi over the context and
     two clones (a slice of the batch per context, each launched and applied on its own -- one GPU
     here, one per GPU on a node): the same events and counters.  direct "1": the replica's row arena (written at push
-    time) goes to the GPU as it is (r05); "0" (PBFT_REPLICA_DIRECT=0): the staging fill."""
+    time) goes to the GPU as it is (r05); "0" (PBFT_REPLICA_DIRECT=0): the staging fill.  r06:
+    push_many's tasks and early pieces at their extremes (one task per thread / 64; pieces of 4,096 rows: ~260 of
+    them, the short one first) and the votes in a shuffled order (tasks no longer in seq order: the pieces' partial
+    application waits for a seq-ordered prefix) -- the same events, in order, and counters."""
     monkeypatch.setenv("PBFT_REPLICA_DIRECT", direct)
+    if tasks:
+        monkeypatch.setenv("PBFT_PUSH_TASKS", tasks)
+    if piece:
+        monkeypatch.setenv("PBFT_MANY_PIECE", piece)
     import ctypes
     import hashlib
     import time
@@ -160,6 +170,11 @@ def test_gpu_replica_2p20_round(gpu_cluster, n_ctx, direct, monkeypatch):
                                              (pR[q - 1].tobytes() + pS[q - 1].tobytes()), None) == 1
     view = np.ones(N, np.uint64)
     digs = np.ascontiguousarray(dig[seq.astype(np.int64) - 1])
+    if shuffle:  # (every (seq, kind, signer) votes once: any arrival order gives the same outcome)
+        perm = np.random.default_rng(6).permutation(N)
+        kind, seq, signer = kind[perm].copy(), seq[perm].copy(), signer[perm].copy()
+        digs, sigs = np.ascontiguousarray(digs[perm]), np.ascontiguousarray(sigs[perm])
+        bad = bad[perm]
     q_ = ctypes.c_uint64()
     assert L.pbft_replica_push_many(rep, N, kind.ctypes.data, view.ctypes.data, seq.ctypes.data, digs.ctypes.data,
                                     signer.ctypes.data, sigs.ctypes.data, ctypes.byref(q_)) == 0 and q_.value == N
