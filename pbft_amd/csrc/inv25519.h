@@ -231,8 +231,11 @@ __host__ __device__ __forceinline__ int32_t divsteps30_var(int32_t eta, uint32_t
 #define DS_TZ (2 * DS_TN)
 #define DS_TAB_ENTRIES (DS_TZ * 16 * 32)
 
-// entry idx = ((zc + 5) * 16 + (f >> 1) % 16) * 32 + g % 32: u, v, q, r as int8 in bits 0..31, c (int8) in
-// bits 32..39, bit 40 = the map negates zeta
+// entry idx = ((zc + 5) * 16 + (f >> 1) % 16) * 32 + g % 32, i.e. byte offset 4096 (zc + 5) + 256 ((f >> 1) % 16) +
+// 8 (g % 32): u, v, q, r as int8 in the low word; the high word is the zeta map in the scaled form that indexes the
+// table, Z = 4096 (zeta + 5): 4096 c when zeta' = zeta + c, 4096 c + 40961 when zeta' = c - zeta, so that
+// Z' = (Z ^ -(hi & 1)) + hi (one v_xad_u32 after a one-bit sign extension) and the class's byte offset is
+// med3(Z, 0, 9 * 4096).
 __host__ __device__ constexpr uint64_t ds_tab_entry(uint32_t idx) {
   int32_t zeta = (int32_t)(idx / 512) - DS_TN;
   int32_t f = (int32_t)((((idx / 32) % 16) << 1) | 1), g = (int32_t)(idx % 32);
@@ -249,8 +252,9 @@ __host__ __device__ constexpr uint64_t ds_tab_entry(uint32_t idx) {
     u *= 2; v *= 2;
     g /= 2;  // exact: g is even here
   }
+  const int32_t hi = s < 0 ? 4096 * c + 40961 : 4096 * c;
   return (uint64_t)(uint8_t)(int8_t)u | (uint64_t)(uint8_t)(int8_t)v << 8 | (uint64_t)(uint8_t)(int8_t)q << 16 |
-         (uint64_t)(uint8_t)(int8_t)r << 24 | (uint64_t)(uint8_t)(int8_t)c << 32 | (uint64_t)(s < 0 ? 1 : 0) << 40;
+         (uint64_t)(uint8_t)(int8_t)r << 24 | (uint64_t)(uint32_t)hi << 32;
 }
 struct ds_table {
   uint64_t e[DS_TAB_ENTRIES];
@@ -259,28 +263,159 @@ struct ds_table {
   }
 };
 
+// low 24 bits, sign-extended: the operand v_mul_i32_i24 / v_mad_i32_i24 read (the compiler selects them for
+// products of such values and drops the extension)
+__host__ __device__ __forceinline__ int32_t ds_sext24(uint32_t x) { return (int32_t)(x << 8) >> 8; }
+
+// byte offset of the entry: scaled zeta Z's class, f's bits 1..4 moved to bits 8..11 and g's bits 0..4 to bits 3..7
+// by the shifts FS, GS (> 0 left, < 0 right)
+template <int FS, int GS>
+__host__ __device__ __forceinline__ uint32_t ds_offset(int32_t Z, uint32_t F, uint32_t G) {
+  const int32_t zc = Z < 0 ? 0 : (Z > 9 * 4096 ? 9 * 4096 : Z);
+  const uint32_t fp = FS >= 0 ? F << (FS & 31) : F >> (-FS & 31);
+  const uint32_t gp = GS >= 0 ? G << (GS & 31) : G >> (-GS & 31);
+  return (fp & 0xF00u) | (gp & 0xF8u) | (uint32_t)zc;
+}
+
+// Schedule pin (device): xs are treated as rewritten after `dep` exists, so work reading them is issued after the
+// instruction that produced `dep` -- the lookup chain below issues each ds_read first and fills its latency with
+// the independent products (the compiler otherwise interleaves them ahead of the address and the read).
+__host__ __device__ __forceinline__ void ds_after1(uint32_t dep, int32_t& x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(x) : "v"(dep));
+#else
+  (void)dep; (void)x;
+#endif
+}
+template <class... T>
+__host__ __device__ __forceinline__ void ds_after(uint32_t dep, T&... xs) {
+  (ds_after1(dep, xs), ...);
+}
+
+struct ds_mat {
+  int32_t u, v, q, r;
+};
+
+// 30 half-delta divsteps by 6 lookups on the scaled zeta Z = 4096 (zeta + 5); t as divsteps30.  The low bits of f
+// and g are never shifted: after lookup j they are F = 2^(5j) f_j, G = 2^(5j) g_j (mod 2^30), and lookup j reads
+// their bits 5j .. 5j+4 in place.  Lookups 0-2 multiply in 32 bits; from lookup 3 the window F >> 6 (bits 6..29 of
+// F, low 10 bits zero) is exact in 24-bit products, as are the matrix products up to T_5 (entries < 2^20 before the
+// fifth); the sixth, T_6 = S_5 T_5, is 32-bit.  Per lookup on the chain: the entry's fields, two products, the
+// offset, the read; the matrix products T <- S T and fill(k, off) (the caller's independent work) are pinned after
+// lookup k's read is issued.
+__host__ __device__ __forceinline__ uint64_t ds_load(const uint64_t* tab, uint32_t off) {
+  return *(const uint64_t*)((const char*)tab + off);
+}
+// lookup 0's offset (its entry e0 = ds_load(tab, off0) is read by the caller, which can issue it early)
+__host__ __device__ __forceinline__ uint32_t ds_first(int32_t Z, uint32_t f, uint32_t g) {
+  return ds_offset<7, 3>(Z, f, g);
+}
+
+template <class Fill>
+__host__ __device__ __forceinline__ int32_t divsteps30_tabz(int32_t Z, uint32_t f, uint32_t g, uint32_t off0,
+                                                            uint64_t e0, int32_t t[4], const uint64_t* tab,
+                                                            Fill&& fill) {
+  auto load = [&](uint32_t off) { return ds_load(tab, off); };
+  auto decode = [&](uint64_t e) {
+    const uint32_t lo = (uint32_t)e;
+    const int32_t hi = (int32_t)(e >> 32);
+    Z = (int32_t)(((uint32_t)Z ^ (uint32_t)((int32_t)((uint32_t)hi << 31) >> 31)) + (uint32_t)hi);
+    return ds_mat{(int8_t)lo, (int8_t)(lo >> 8), (int8_t)(lo >> 16), (int32_t)lo >> 24};
+  };
+  // products in 32 bits (wrapping) and in 24 bits (the low 24 bits of both operands, sign-extended)
+  auto mul32 = [](int32_t s, uint32_t x) { return (uint32_t)s * x; };
+  auto mul24 = [](int32_t s, uint32_t x) { return (uint32_t)s * (uint32_t)ds_sext24(x); };
+  // T <- S T while the entries stay < 2^23 (the compiler cannot bound them, and picks v_mul_lo_u32 /
+  // v_mad_u64_u32 for about half of such products: the 24-bit forms are spelled out on the device)
+  auto mad24 = [](int32_t a, int32_t b, int32_t c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+#else
+    return (int32_t)((uint32_t)a * (uint32_t)b + (uint32_t)c);
+#endif
+  };
+  auto mul24s = [](int32_t a, int32_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    int32_t d;
+    asm("v_mul_i32_i24 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+#else
+    return (int32_t)((uint32_t)a * (uint32_t)b);
+#endif
+  };
+  auto compose24 = [&](const ds_mat& S, const ds_mat& T) {
+    return ds_mat{mad24(S.u, T.u, mul24s(S.v, T.q)), mad24(S.u, T.v, mul24s(S.v, T.r)),
+                  mad24(S.q, T.u, mul24s(S.r, T.q)), mad24(S.q, T.v, mul24s(S.r, T.r))};
+  };
+  auto pin = [&](uint32_t off, ds_mat& a, ds_mat& b) { ds_after(off, a.u, a.v, a.q, a.r, b.u, b.v, b.q, b.r); };
+  // lookup 0
+  uint32_t off = off0;
+  uint64_t e = e0;
+  fill(0, off);
+  ds_mat S = decode(e);
+  // lookup 1: F = 2^5 f_1
+  uint32_t F = mul32(S.u, f) + mul32(S.v, g), G = mul32(S.q, f) + mul32(S.r, g);
+  off = ds_offset<2, -2>(Z, F, G);
+  e = load(off);
+  fill(1, off);
+  ds_mat T = S;
+  S = decode(e);
+  // lookup 2: F = 2^10 f_2, then the 24-bit window F >> 6
+  {
+    const uint32_t F2 = mul32(S.u, F) + mul32(S.v, G), G2 = mul32(S.q, F) + mul32(S.r, G);
+    off = ds_offset<-3, -7>(Z, F2, G2);
+    F = F2 >> 6; G = G2 >> 6;
+  }
+  e = load(off);
+  pin(off, S, T);
+  T = compose24(S, T);  // T_2
+  fill(2, off);
+  S = decode(e);
+  // lookups 3-5
+  {
+    const uint32_t F3 = mul24(S.u, F) + mul24(S.v, G), G3 = mul24(S.q, F) + mul24(S.r, G);
+    off = ds_offset<-2, -6>(Z, F3, G3);
+    F = F3; G = G3;
+  }
+  e = load(off);
+  pin(off, S, T);
+  T = compose24(S, T);  // T_3
+  fill(3, off);
+  S = decode(e);
+  {
+    const uint32_t F4 = mul24(S.u, F) + mul24(S.v, G), G4 = mul24(S.q, F) + mul24(S.r, G);
+    off = ds_offset<-7, -11>(Z, F4, G4);
+    F = F4; G = G4;
+  }
+  e = load(off);
+  pin(off, S, T);
+  T = compose24(S, T);  // T_4
+  fill(4, off);
+  S = decode(e);
+  {
+    const uint32_t F5 = mul24(S.u, F) + mul24(S.v, G), G5 = mul24(S.q, F) + mul24(S.r, G);
+    off = ds_offset<-12, -16>(Z, F5, G5);
+  }
+  e = load(off);
+  pin(off, S, T);
+  T = compose24(S, T);  // T_5: entries < 2^25
+  fill(5, off);
+  S = decode(e);
+  t[0] = (int32_t)(mul32(S.u, (uint32_t)T.u) + mul32(S.v, (uint32_t)T.q));
+  t[1] = (int32_t)(mul32(S.u, (uint32_t)T.v) + mul32(S.v, (uint32_t)T.r));
+  t[2] = (int32_t)(mul32(S.q, (uint32_t)T.u) + mul32(S.r, (uint32_t)T.q));
+  t[3] = (int32_t)(mul32(S.q, (uint32_t)T.v) + mul32(S.r, (uint32_t)T.r));
+  return Z;
+}
+
 // 30 half-delta divsteps by 6 lookups; same return value and t as divsteps30(zeta, f, g, t)
 __host__ __device__ __forceinline__ int32_t divsteps30_tab(int32_t zeta, uint32_t f, uint32_t g, int32_t t[4],
                                                            const uint64_t* tab) {
-  int32_t u = 1, v = 0, q = 0, r = 1;
-#pragma unroll
-  for (int k = 0; k < 30 / DS_TN; ++k) {
-    const int32_t zc = zeta < -DS_TN ? -DS_TN : (zeta > DS_TN - 1 ? DS_TN - 1 : zeta);
-    const uint32_t idx = (uint32_t)(zc + DS_TN) * 512u + ((f >> 1) & 15u) * 32u + (g & 31u);
-    const uint64_t e = tab[idx];
-    const int32_t su = (int8_t)e, sv = (int8_t)(e >> 8), sq = (int8_t)(e >> 16), sr = (int8_t)(e >> 24);
-    const int32_t c = (int8_t)(e >> 32);
-    zeta = ((e >> 40) & 1u ? -zeta : zeta) + c;
-    const uint32_t f2 = (uint32_t)su * f + (uint32_t)sv * g;  // low 32 bits of 2^5 f' (exactly divisible)
-    const uint32_t g2 = (uint32_t)sq * f + (uint32_t)sr * g;
-    f = f2 >> DS_TN;  // low 27, 22, ... bits exact: enough for the remaining lookups
-    g = g2 >> DS_TN;
-    const int32_t nu = su * u + sv * q, nv = su * v + sv * r;
-    const int32_t nq = sq * u + sr * q, nr = sq * v + sr * r;
-    u = nu; v = nv; q = nq; r = nr;
-  }
-  t[0] = u; t[1] = v; t[2] = q; t[3] = r;
-  return zeta;
+  const int32_t Z = (zeta + DS_TN) * 4096;
+  const uint32_t off0 = ds_first(Z, f, g);
+  return (divsteps30_tabz(Z, f, g, off0, ds_load(tab, off0), t, tab, [](int, uint32_t) {}) >> 12) - DS_TN;
 }
 
 // out = z^-1 (0 -> 0) for a wave-uniform z, table in `tab` (LDS on the device); z as for fe_invert_gcd.
@@ -371,7 +506,7 @@ __device__ __forceinline__ int32_t row_from_above(int32_t x) {  // lane j <- lan
 // Lane j of its row <- lane N of the same 16-lane row (DPP row_newbcast:N).
 template <int N>
 __device__ __forceinline__ int32_t row_lane(int32_t x) {
-  return __builtin_amdgcn_update_dpp(0, x, 0x150 + N, 0xF, 0xF, false);
+  return __builtin_amdgcn_mov_dpp(x, 0x150 + N, 0xF, 0xF, false);  // every lane written: no old value
 }
 
 // limb i of v = lane i of this lane's row, i = 0..9
@@ -414,43 +549,64 @@ __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint6
   const int32_t w19 = li == 0 ? 19 : 0;  // the carry out of limb 9 re-enters limb 0 times 19
   // (D, E) <- tp (D, E) mod p, two carry rounds (|h| < 2^31, |k| < 2^10 by the limb bounds above; lane 10 picks
   // up limb 9's carry too and the final mask drops it -- that carry re-enters at lane 0, times 19)
-  auto update_de = [&](const int32_t tp[4]) {
-    const int64_t u = tp[0], v = tp[1], q = tp[2], r = tp[3];
-    const int64_t ad = u * D + v * E, ae = q * D + r * E;
-    const int32_t hd = (int32_t)(ad >> dsh), he = (int32_t)(ae >> dsh);
-    const int32_t hd9 = ROWS ? row_lane<9>(hd) : __builtin_amdgcn_readlane(hd, 9);
-    const int32_t he9 = ROWS ? row_lane<9>(he) : __builtin_amdgcn_readlane(he, 9);
-    const int64_t nd = (int64_t)(int32_t)(((uint32_t)ad & dmask) + (uint32_t)row_from_below(hd)) + (int64_t)w19 * hd9;
-    const int64_t ne = (int64_t)(int32_t)(((uint32_t)ae & dmask) + (uint32_t)row_from_below(he)) + (int64_t)w19 * he9;
-    const int32_t kd = (int32_t)(nd >> dsh), ke = (int32_t)(ne >> dsh);
-    const int32_t kd9 = ROWS ? row_lane<9>(kd) : __builtin_amdgcn_readlane(kd, 9);
-    const int32_t ke9 = ROWS ? row_lane<9>(ke) : __builtin_amdgcn_readlane(ke, 9);
-    D = ((int32_t)((uint32_t)nd & dmask) + row_from_below(kd) + w19 * kd9) & dlive;
-    E = ((int32_t)((uint32_t)ne & dmask) + row_from_below(ke) + w19 * ke9) & dlive;
+  // one of D', E' from its product sum a = x D + y E
+  auto de_lane = [&](int64_t a) -> int32_t {
+    const int32_t h = (int32_t)(a >> dsh);
+    const int32_t h9 = ROWS ? row_lane<9>(h) : __builtin_amdgcn_readlane(h, 9);
+    const int64_t n = (int64_t)(int32_t)(((uint32_t)a & dmask) + (uint32_t)row_from_below(h)) + (int64_t)w19 * h9;
+    const int32_t kk = (int32_t)(n >> dsh);
+    const int32_t k9 = ROWS ? row_lane<9>(kk) : __builtin_amdgcn_readlane(kk, 9);
+    return ((int32_t)((uint32_t)n & dmask) + row_from_below(kk) + w19 * k9) & dlive;
   };
-  int32_t zeta = -1;
+  auto update_de = [&](const int32_t tp[4]) {
+    const int32_t nD = de_lane((int64_t)tp[0] * D + (int64_t)tp[1] * E);
+    const int32_t nE = de_lane((int64_t)tp[2] * D + (int64_t)tp[3] * E);
+    D = nD; E = nE;
+  };
+  int32_t Z = (DS_TN - 1) * 4096;  // zeta = -1, scaled (divsteps30_tabz)
   int32_t tp[4] = {1, 0, 0, 1};  // the previous batch's matrix: (D, E) lag one batch behind f, g
-  int k = 0;
-  for (; k < 20; ++k) {
-#if !PBFT_ABL_INV_NOLOOKUP
-    if (__ballot(g != 0) == 0) break;  // g = 0: f = +-1
-#else
-    if (k == 18) break;
-#endif
-    int32_t t[4];
-#if PBFT_ABL_INV_NOLOOKUP  // ablation (timing only, results wrong): a fixed matrix instead of the lookups
-    t[0] = 1 << 29; t[1] = (int32_t)(__builtin_amdgcn_readfirstlane(f) & 7); t[2] = 3; t[3] = 1 << 28;
-    zeta -= 30;
-#else
+  // the lookups read limb 0 mod 2^30 only: it is exact before the carry round (lane 0 receives no carry), so the
+  // next batch's limb 0 reaches the row (row_newbcast:0) and its first entry is read before the carries and the
+  // exit test; the test itself reads the limbs before the carries (all zero => g = 0; limbs that cancel only
+  // cost one more batch, which leaves the result unchanged, see above)
 #if PBFT_INV_VALU_LOOKUP
-    // limb 0 to every lane of its row by DPP (row_newbcast:0): the lookup chain then stays on the VALU (a scalar
-    // copy, v_readfirstlane, puts it on the SALU with two VALU <-> SALU crossings per lookup)
-    zeta = divsteps30_tab(zeta, (uint32_t)__builtin_amdgcn_update_dpp(0, f, 0x150, 0xF, 0xF, false),
-                          (uint32_t)__builtin_amdgcn_update_dpp(0, g, 0x150, 0xF, 0xF, false), t, tab);
+  auto low = [](int32_t x) { return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x150, 0xF, 0xF, false); };
 #else
-    zeta = divsteps30_tab(zeta, (uint32_t)__builtin_amdgcn_readfirstlane(f),
-                          (uint32_t)__builtin_amdgcn_readfirstlane(g), t, tab);
+  auto low = [](int32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane(x); };
 #endif
+  uint32_t fl = low(f), gl = low(g);
+  int32_t gtest = g;
+  uint32_t off0 = ds_first(Z, fl, gl);
+  uint64_t e0 = ds_load(tab, off0);
+  // exit test at the bottom (g = 0: f = +-1): the next batch's first read is issued before the branch (with the
+  // test at the top the compiler sinks the read past it)
+#if !PBFT_ABL_INV_NOLOOKUP
+  auto more = [&](int kk) { return kk < 20 && __ballot(gtest != 0) != 0; };
+#else
+  auto more = [&](int kk) { return kk < 18; };
+#endif
+  int k = 0;
+  if (more(0)) do {
+    int32_t t[4];
+    // the previous batch's (D, E) update, independent of this batch's lookups: D' in lookup 0's LDS wait, E' in
+    // lookup 1's (divsteps30_tabz pins them after the reads)
+    int32_t nD = D, nE = E;
+    auto fill = [&](int j, uint32_t off) {
+      if (j == 0) {
+        ds_after(off, D, E, tp[0], tp[1]);
+        nD = de_lane((int64_t)tp[0] * D + (int64_t)tp[1] * E);
+      } else if (j == 1) {
+        ds_after(off, D, E, tp[2], tp[3]);
+        nE = de_lane((int64_t)tp[2] * D + (int64_t)tp[3] * E);
+      }
+    };
+#if PBFT_ABL_INV_NOLOOKUP  // ablation (timing only, results wrong): a fixed matrix instead of the lookups
+    t[0] = 1 << 29; t[1] = (int32_t)(fl & 7); t[2] = 3; t[3] = 1 << 28;
+    Z -= 30 * 4096;
+    fill(0, off0);
+    fill(1, off0);
+#else
+    Z = divsteps30_tabz(Z, fl, gl, off0, e0, t, tab, fill);
 #endif
     // f, g <- (t [f, g]) / 2^30: the chain the next lookups wait for
     {
@@ -458,13 +614,19 @@ __device__ __forceinline__ void fe_invert_wave(fe& out, const fe& z, const uint6
       const int64_t af = u * f + v * g, ag = q * f + r * g;
       int32_t nf = (int32_t)(af >> 30) + row_from_above((int32_t)((uint32_t)af & INV_M30));
       int32_t ng = (int32_t)(ag >> 30) + row_from_above((int32_t)((uint32_t)ag & INV_M30));
+      fl = low(nf); gl = low(ng);
+      off0 = ds_first(Z, fl, gl);
+      e0 = ds_load(tab, off0);
+      gtest = ng;
       f = (int32_t)((uint32_t)nf & fmask) + row_from_below((nf >> 30) & fcarry);
       g = (int32_t)((uint32_t)ng & fmask) + row_from_below((ng >> 30) & fcarry);
     }
-    // the previous batch's (D, E) update: independent of this batch's lookups, so the scheduler overlaps them
-    update_de(tp);
+    D = nD; E = nE;
     tp[0] = t[0]; tp[1] = t[1]; tp[2] = t[2]; tp[3] = t[3];
-  }
+  } while (more(++k));
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" ::"v"(e0));  // the last speculative read is live on the exit edge too: it stays ahead of the branch
+#endif
   update_de(tp);
   // x^-1 = +-D 2^(-30 k): f = +1 iff its limb 0 is 1
   const bool neg = ((uint32_t)(ROWS ? row_lane<0>(f) : __builtin_amdgcn_readfirstlane(f)) & INV_M30) != 1u;
