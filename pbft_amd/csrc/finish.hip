@@ -81,3 +81,51 @@ hipError_t launch_finish(int fm, int lv, int w, const uint8_t* R, uint32_t rs_st
 #undef PBFT_LAUNCH_FIN
   return hipGetLastError();
 }
+
+
+// ---- test hook: the finish's row-wise inversion on arbitrary values ----------------------------------------
+// One value per 16-lane row (so every row of a wave inverts its own value, as in finish_kernel), through the same
+// fe_invert_wave<true> and LDS divstep table; tests/test_gpu_verify.py checks it against z^(p-2) on the inversion
+// extremes.  Not part of the verify path (and not declared in include/: a test hook, like pbft_debug_fin_stamps).
+__global__ void __launch_bounds__(64) debug_invert_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                          uint32_t n) {
+  __shared__ uint64_t ds_tab[DS_TAB_ENTRIES];
+  {
+    const uint4* src = (const uint4*)g_ds_tab.e;
+    uint4* dst = (uint4*)ds_tab;
+    for (int k = threadIdx.x; k < DS_TAB_ENTRIES / 2; k += 64) dst[k] = src[k];
+  }
+  __syncthreads();
+  const uint32_t row = blockIdx.x * 4 + (threadIdx.x >> 4);
+  const uint32_t i = row < n ? row : n - 1;  // (rows past n invert a copy of the last value: uniform per row)
+  uint32_t w[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) w[t] = in[(size_t)i * 8 + t];
+  fe z, inv;
+  fe_from_words(z, w);
+  fe_invert_wave<true>(inv, z, ds_tab);
+  fe_to_words(w, inv);
+  if ((threadIdx.x & 15) == 0 && row < n) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) out[(size_t)row * 8 + t] = w[t];
+  }
+}
+
+// in, out: n values as 8 little-endian 32-bit words each (in < 2^255, any residue; out canonical)
+extern "C" int pbft_debug_invert(const uint32_t* in, uint32_t* out, uint32_t n) {
+  if (!in || !out || n == 0 || n > (1u << 20)) return -1;
+  uint32_t *din = nullptr, *dout = nullptr;
+  const size_t bytes = (size_t)n * 32;
+  hipError_t e = hipMalloc(&din, bytes);
+  if (e == hipSuccess) e = hipMalloc(&dout, bytes);
+  if (e == hipSuccess) e = hipMemcpy(din, in, bytes, hipMemcpyHostToDevice);
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(debug_invert_kernel, dim3((n + 3) / 4), dim3(64), 0, 0, din, dout, n);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+  if (din) (void)hipFree(din);
+  if (dout) (void)hipFree(dout);
+  return e == hipSuccess ? 0 : -(int)e - 1;
+}

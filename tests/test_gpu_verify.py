@@ -208,6 +208,33 @@ def test_comb_pair_matches_oracle(gv, coracle):
         gv.set_option(gv.OPT_COMB_PAIR, 2)
 
 
+P = 2**255 - 19
+
+
+def test_wave_inversion_extremes_on_gpu(gv):
+    """The finish's row-wise inversion itself (inv25519.h fe_invert_wave<true>: table divsteps with the scaled zeta,
+    unshifted low bits, 24-bit products, the next batch's first read before the carries and the exit test on the
+    limbs before the carries), one value per 16-lane row through the library's test hook pbft_debug_invert, equals
+    z^(p-2) on the values that stress the divstep count and the limb ranges (powers of two, p - 2^k, all-ones
+    patterns, values just below and above p, 0) and on random values of every bit length."""
+    from pbft_amd._lib import load
+    lib = load()
+    lib.pbft_debug_invert.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]
+    vals = [2**k for k in range(255)] + [P - 2**k for k in range(1, 255)] + [(2**k - 1) for k in range(1, 256)]
+    vals += [P - k for k in range(1, 40)] + [P + k for k in range(0, 19)] + [2**255 - 1 - k for k in range(20)]
+    vals += [0, 1, 2, 19, 38, (P + 1) // 2, P - 1]
+    rnd = random.Random(20261018)
+    vals += [rnd.getrandbits(rnd.randrange(1, 256)) for _ in range(20000)]
+    vals = [v % 2**255 for v in vals]
+    words = np.array([[(v >> (32 * t)) & 0xFFFFFFFF for t in range(8)] for v in vals], dtype=np.uint32)
+    out = np.zeros_like(words)
+    assert lib.pbft_debug_invert(words.ctypes.data, out.ctypes.data, len(vals)) == 0
+    got = [sum(int(w) << (32 * t) for t, w in enumerate(row)) for row in out]
+    bad = [(v, g) for v, g in zip(vals, got) if g != pow(v, P - 2, P)]
+    assert not bad, f"{len(bad)} of {len(vals)} inverses differ, first: {bad[0]}"
+
+
+
 def test_comb_prio_match_oracle(gv, coracle):
     """r05 comb form PBFT_OPT_COMB_PRIO (8-wave blocks whose SIMD-sharing waves trade priorities), forced on and off
     and by size, against the oracle's bits -- at the 131k shard, ragged sizes whose last block is partial, and a size
