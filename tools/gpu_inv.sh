@@ -1,6 +1,8 @@
 #!/bin/bash
 # r06 inversion rewrite: GPU parity of the new divstep lookup chain, then an interleaved A/B of the old / new
 # finish (plain and stamped builds) at the 131k shard, at 2^20 and on the latency kernel.
+# (build/abx/libpbft_{invold,invpin,invbat}[_st].so: tools/build_variant.sh-style builds of the three source states;
+# ./build/abx is gpurun-ignored after r06 -- drop that line from .gpurunignore to run this again)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 D=gpurun_out/r06_inv; mkdir -p $D

@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 kernel durations of the old / new inversion at the 131k shard and at 2^20 (one library per run)
+# rocprofv3 kernel durations of the old / new inversion at the 131k shard and at 2^20 (one library per run;
+# build/abx is gpurun-ignored after r06, see tools/gpu_inv.sh)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out; export TMPDIR=/tmp
 D=gpurun_out/r06_invprof; mkdir -p $D
