@@ -296,13 +296,6 @@ struct ds_mat {
   int32_t u, v, q, r;
 };
 
-// 30 half-delta divsteps by 6 lookups on the scaled zeta Z = 4096 (zeta + 5); t as divsteps30.  The low bits of f
-// and g are never shifted: after lookup j they are F = 2^(5j) f_j, G = 2^(5j) g_j (mod 2^30), and lookup j reads
-// their bits 5j .. 5j+4 in place.  Lookups 0-2 multiply in 32 bits; from lookup 3 the window F >> 6 (bits 6..29 of
-// F, low 10 bits zero) is exact in 24-bit products, as are the matrix products up to T_5 (entries < 2^20 before the
-// fifth); the sixth, T_6 = S_5 T_5, is 32-bit.  Per lookup on the chain: the entry's fields, two products, the
-// offset, the read; the matrix products T <- S T and fill(k, off) (the caller's independent work) are pinned after
-// lookup k's read is issued.
 __host__ __device__ __forceinline__ uint64_t ds_load(const uint64_t* tab, uint32_t off) {
   return *(const uint64_t*)((const char*)tab + off);
 }
@@ -311,6 +304,13 @@ __host__ __device__ __forceinline__ uint32_t ds_first(int32_t Z, uint32_t f, uin
   return ds_offset<7, 3>(Z, f, g);
 }
 
+// 30 half-delta divsteps by 6 lookups on the scaled zeta Z = 4096 (zeta + 5); t as divsteps30.  The low bits of f
+// and g are never shifted: after lookup j they are F = 2^(5j) f_j, G = 2^(5j) g_j (mod 2^30), and lookup j reads
+// their bits 5j .. 5j+4 in place.  Lookups 0-2 multiply in 32 bits; from lookup 3 the window F >> 6 (bits 6..29 of
+// F, low 10 bits zero) is exact in 24-bit products, as are the matrix products up to T_5 (entries < 2^20 before the
+// fifth); the sixth, T_6 = S_5 T_5, is 32-bit.  Per lookup on the chain: the entry's fields, two products, the
+// offset, the read; the matrix products T <- S T and fill(k, off) (the caller's independent work) are pinned after
+// lookup k's read is issued; lookup 0's entry e0 (at off0) comes from the caller.
 template <class Fill>
 __host__ __device__ __forceinline__ int32_t divsteps30_tabz(int32_t Z, uint32_t f, uint32_t g, uint32_t off0,
                                                             uint64_t e0, int32_t t[4], const uint64_t* tab,
